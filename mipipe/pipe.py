@@ -1,0 +1,271 @@
+"""The ``Pipe`` module: synchronous GPipe pipeline parallelism.
+
+API parity with ``torch.distributed.pipeline.sync.Pipe`` as vendored in
+``/root/reference/pipe.py``:
+
+* ``Pipe(module, chunks=1, checkpoint="except_last", deferred_batch_norm=False)``
+  (``pipe.py:308-314``) with the same argument validation (``pipe.py:324-330``);
+* placement is implicit from each child's parameters, or explicit through
+  :class:`WithDevice`; consecutive children on the same device form one
+  partition, and every CPU child is its own partition (``pipe.py:191-218``);
+* ``len``/indexing/iteration over the layers (``pipe.py:358-386``);
+* ``cuda()``/``cpu()``/``to(device)`` are denied, ``to(dtype)`` is allowed
+  (``pipe.py:390-415``);
+* one copy stream per (partition, micro-batch) (``pipe.py:417-429``);
+* ``forward`` = check -> scatter -> run -> gather, returning an RRef
+  (``pipe.py:431-494``; see :mod:`mipipe.rref`).
+
+Extras: ``return_rref=False`` returns the plain output like the reference's
+edited copy (``pipe.py:491-494``); :meth:`Pipe.close` stops the workers.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Any, Iterator, List, Optional, Tuple, Union, cast
+
+import torch
+from torch import Tensor, nn
+
+from . import microbatch
+from .batchnorm import DeferredBatchNorm
+from .pipeline import Pipeline
+from .rref import make_rref
+from .skip.layout import SkipLayout, inspect_skip_layout
+from .skip.skippable import verify_skippables
+from .stream import AbstractStream, new_stream
+
+__all__ = ["Pipe", "BalanceError", "PipeSequential", "WithDevice"]
+
+Device = Union[torch.device, int, str]
+
+_CHECKPOINT_MODES = ("always", "except_last", "never")
+
+
+class BalanceError(ValueError):
+    """Raised when a requested balance does not fit the module."""
+
+
+class PipeSequential(nn.Sequential):
+    """``nn.Sequential`` whose layers may take several positional inputs.
+
+    A tuple produced by one layer is splatted into the next; any other value is
+    passed as a single argument.
+    """
+
+    def forward(self, *inputs):  # type: ignore[override]
+        carry: Any = inputs
+        for layer in self:
+            carry = layer(*carry) if isinstance(carry, tuple) else layer(carry)
+        return carry
+
+
+class WithDevice(nn.Module):
+    """Pins a child of the ``nn.Sequential`` given to :class:`Pipe` to ``device``.
+
+    Needed for parameter-less layers (dropout, activation, reshapes) that would
+    otherwise be treated as CPU layers.  ``Pipe`` moves the wrapped module there.
+    """
+
+    def __init__(self, module: nn.Module, device: Device) -> None:
+        super().__init__()
+        self._module = module
+        self._device = torch.device(device)
+
+    def forward(self, *args, **kwargs):
+        return self._module(*args, **kwargs)
+
+    @property
+    def module(self) -> nn.Module:
+        return self._module
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+
+def _verify_module(module: nn.Sequential) -> None:
+    if not isinstance(module, nn.Sequential):
+        raise TypeError("module must be nn.Sequential to be partitioned")
+    if len(list(module.named_children())) != len(module):
+        raise ValueError("module with duplicate children is not supported")
+
+
+def _module_device(module: nn.Module) -> torch.device:
+    """The single device holding all of ``module``'s parameters (CPU if none)."""
+    found: Optional[torch.device] = None
+    for p in module.parameters():
+        if found is None:
+            found = p.device
+        elif p.device != found:
+            raise ValueError(
+                f"nn.Module: {module}, should have all parameters on a single device,"
+                " please use .to() to place the module on a single device"
+            )
+    return found if found is not None else torch.device("cpu")
+
+
+# Upstream private name.
+_retrieve_device = _module_device
+
+
+def _flatten_partition(layers: List[nn.Module]) -> PipeSequential:
+    flat: List[nn.Module] = []
+    for layer in layers:
+        if isinstance(layer, nn.Sequential):
+            flat.extend(layer.children())
+        else:
+            flat.append(layer)
+    return PipeSequential(*flat)
+
+
+def _split_module(module: nn.Sequential) -> Tuple[List[nn.Sequential], List[torch.device]]:
+    """Groups consecutive children by device; each CPU child is its own group."""
+    groups: List[Tuple[torch.device, List[nn.Module]]] = []
+    for _, child in module.named_children():
+        if isinstance(child, WithDevice):
+            device = child.device
+            child = child.module
+            child.to(device)
+        else:
+            device = _module_device(child)
+        if groups and groups[-1][0] == device and device.type != "cpu":
+            groups[-1][1].append(child)
+        else:
+            groups.append((device, [child]))
+    partitions = cast(List[nn.Sequential], nn.ModuleList([_flatten_partition(layers) for _, layers in groups]))
+    devices = [d for d, _ in groups]
+    return partitions, devices
+
+
+def _verify_splitting(module: nn.Sequential, partitions: List[nn.Sequential], devices: List[torch.device]) -> None:
+    """A parameter shared between partitions on *different* devices is an error."""
+    total = len(list(module.parameters()))
+    per_child = sum(len(list(c.parameters())) for c in module.children())
+    if total == per_child:
+        return  # nothing is shared
+    owner: dict = {}
+    for idx, part in enumerate(partitions):
+        for p in part.parameters():
+            prev = owner.get(id(p))
+            if prev is not None and devices[prev] != devices[idx]:
+                raise ValueError("module with duplicate parameters on distinct devices is not supported")
+            owner.setdefault(id(p), idx)
+
+
+_MOVING_DENIED = "denied to move parameters and buffers, because Pipe should manage device placement"
+MOVING_DENIED = TypeError(_MOVING_DENIED)
+
+
+class Pipe(nn.Module):
+    """Wraps an ``nn.Sequential`` for synchronous pipeline-parallel training.
+
+    Args:
+        module: the sequential model; children must already sit on their devices
+            (or be wrapped in :class:`WithDevice`).
+        chunks: number of micro-batches per mini-batch.
+        checkpoint: ``"always"``, ``"except_last"`` or ``"never"``.
+        deferred_batch_norm: track BatchNorm statistics over the whole mini-batch.
+        return_rref: return an RRef (upstream behaviour, default) or the output.
+    """
+
+    def __init__(
+        self,
+        module: nn.Sequential,
+        chunks: int = 1,
+        checkpoint: str = "except_last",
+        deferred_batch_norm: bool = False,
+        *,
+        return_rref: bool = True,
+    ) -> None:
+        super().__init__()
+        chunks = int(chunks)
+        checkpoint = str(checkpoint)
+        if chunks <= 0:
+            raise ValueError("number of chunks must be positive integer")
+        if checkpoint not in _CHECKPOINT_MODES:
+            raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
+
+        _verify_module(module)
+        verify_skippables(module)
+
+        self.chunks = chunks
+        self.checkpoint = checkpoint
+        self.return_rref = return_rref
+
+        if deferred_batch_norm:
+            module = DeferredBatchNorm.convert_deferred_batch_norm(module, chunks)
+
+        self.partitions, self.devices = _split_module(module)
+        _verify_splitting(module, self.partitions, self.devices)
+
+        self._copy_streams: List[List[AbstractStream]] = []
+        self._skip_layout: SkipLayout = inspect_skip_layout(self.partitions)
+        copy_streams = self._ensure_copy_streams()
+
+        # The pipeline derives the checkpoint boundary from the actual number of
+        # micro-batches at run time (see pipeline.checkpoint_stop_for).
+        self.pipeline = Pipeline(self.partitions, self.devices, copy_streams, self._skip_layout, checkpoint)
+
+    # -- sequence façade -------------------------------------------------------
+    def __len__(self) -> int:
+        return sum(len(p) for p in self.partitions)
+
+    def __getitem__(self, index: int) -> nn.Module:
+        layers = [layer for part in self.partitions for layer in part]
+        if -len(layers) <= index < len(layers):
+            return layers[index]
+        raise IndexError
+
+    def __iter__(self) -> Iterator[nn.Module]:
+        for part in self.partitions:
+            yield from part
+
+    # -- placement guards ----------------------------------------------------------
+    def cuda(self, device: Optional[Device] = None) -> "Pipe":
+        raise MOVING_DENIED
+
+    def cpu(self) -> "Pipe":
+        raise MOVING_DENIED
+
+    def to(self, *args: Any, **kwargs: Any) -> "Pipe":
+        # Only dtype casts are allowed: to(dtype[, non_blocking]).
+        if "device" in kwargs or "tensor" in kwargs:
+            raise MOVING_DENIED
+        if args and (isinstance(args[0], (torch.device, int, str)) or torch.is_tensor(args[0])):
+            raise MOVING_DENIED
+        return super().to(*args, **kwargs)
+
+    # -- streams -------------------------------------------------------------------
+    def _ensure_copy_streams(self) -> List[List[AbstractStream]]:
+        """One dedicated copy stream per (partition, micro-batch), created once and
+        cached -- reusing streams keeps the caching allocator's per-stream pools
+        small (``/root/reference/pipe.py:417-424``)."""
+        if not self._copy_streams:
+            for device in self.devices:
+                self._copy_streams.append([new_stream(device) for _ in range(self.chunks)])
+        return self._copy_streams
+
+    def close(self) -> None:
+        self.pipeline.close()
+
+    # -- forward -------------------------------------------------------------------
+    def forward(self, *inputs: Any):  # type: ignore[override]
+        """Runs one mini-batch through the pipeline.
+
+        Tensors are split on dim 0 into ``chunks`` micro-batches (fewer if the
+        batch is smaller); non-tensors and :class:`~mipipe.NoChunk` tensors are
+        replicated.  All input tensors must be on the first partition's device.
+        Returns an RRef to the output (or the output with ``return_rref=False``).
+        """
+        first_device = self.devices[0] if self.devices else torch.device("cpu")
+        microbatch.check(first_device, *inputs)
+
+        if not self.devices:
+            # An empty Sequential is legal: identity.
+            value = inputs[0] if len(inputs) == 1 else inputs
+            return make_rref(value) if self.return_rref else value
+
+        batches = microbatch.scatter(*inputs, chunks=self.chunks)
+        self.pipeline.run(batches)
+        output = microbatch.gather(batches)
+        return make_rref(output) if self.return_rref else output
