@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""mipipe headline benchmark: pipeline-parallel LM training throughput on MI355X.
+
+Metric (BASELINE.json): tokens/sec for the 12-layer Transformer (d_model 4096,
+nhead 16) at PP = 1/2/4/8, plus the pipeline bubble.  One process per GPU,
+pipeline stages connected by RCCL send/recv, GPipe schedule, chunks = 4 x PP
+(BASELINE configs #2/#3: PP=2 chunks=8, PP=8 chunks=32), fixed micro-batch, so
+per-GPU work is constant as PP grows ("weak" scaling).
+
+Model = the reference driver's LM (/root/reference/main.py): embedding x sqrt(E)
++ sinusoidal positions -> 12 x post-norm TransformerEncoderLayer (ReLU,
+dim_feedforward = d_model, dropout 0.2) -> Linear decoder over the WikiText-2
+vocabulary (28,782) -> cross-entropy; Adam with clip_grad_norm(0.5).  Random
+init, synthetic tokens (no dataset access).  bf16 compute, fp32 master weights
+and gradient accumulation.
+
+    python bench.py                                  # 1 GPU
+    torchrun --nproc-per-node 8 bench.py --gpus 8    # PP = 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REF_TOKENS_PER_S = 3500.0  # reference, checkpoint='never', 2 GPUs (derived)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="enc12_d4096")
+    ap.add_argument("--micro-batch", type=int, default=16, help="sequences per micro-batch")
+    ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
+    ap.add_argument("--checkpoint", default="never", choices=["never", "except_last", "always"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--clip", type=float, default=0.5)
+    ap.add_argument("--no-bubble", action="store_true", help="skip the extra instrumented step")
+    return ap.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import mipipe  # noqa: F401
+    from mipipe import ops
+    from mipipe.models import CONFIGS
+    from mipipe.optim import FlatAdam
+    from mipipe.parallel import PipelineEngine, plan_stages
+    from mipipe.parallel.stage import build_stage, stage_input_shape
+
+    cfg = CONFIGS[args.config]
+    if args.seq_len:
+        cfg.seq_len = args.seq_len
+    S, E, V = cfg.seq_len, cfg.d_model, cfg.vocab
+    pp = world
+    m = args.chunks or 4 * pp
+    mb = args.micro_batch
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    plan = plan_stages(cfg, pp)
+    torch.manual_seed(1234 + rank)
+    # Build only this rank's units (analytic plan; nothing else is instantiated).
+    stage = build_stage(cfg, plan, rank, device=device, dtype=dtype)
+    stage.train()
+    n_params_local = sum(p.numel() for p in stage.parameters())
+
+    opt = FlatAdam(stage.parameters(), lr=args.lr, max_grad_norm=args.clip)
+
+    is_last = rank == world - 1
+
+    def loss_fn(y, t):
+        return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
+
+    engine = PipelineEngine(stage, chunks=m, checkpoint=args.checkpoint,
+                            act_shape=stage_input_shape(cfg, plan, rank, mb), act_dtype=dtype,
+                            loss_fn=loss_fn if is_last else None, device=device)
+
+    g = torch.Generator(device="cpu").manual_seed(0)
+    tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)
+    inputs = [tokens[i, :, :S].to(device) for i in range(m)] if rank == 0 else None
+    targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(m)] if is_last else None
+
+    def train_step():
+        opt.zero_grad()
+        st = engine.step(inputs, targets)
+        sq = opt.grad_sumsq()
+        if world > 1:
+            dist.all_reduce(sq)
+        opt.step(sq)
+        return st
+
+    for _ in range(args.warmup):
+        st = train_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = train_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / max(args.steps, 1) * 1e3
+    ms_t = torch.tensor([ms], device=device)
+    if world > 1:
+        dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
+    ms = float(ms_t.item())
+
+    loss_val = None
+    if is_last and st.loss is not None:
+        loss_val = float(st.loss.item())
+
+    # Bubble: one extra instrumented step, per-stage GPU busy time vs step time.
+    bubble = None
+    if not args.no_bubble:
+        engine.measure = True
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        st = train_step()
+        torch.cuda.synchronize()
+        busy = torch.tensor([st.busy_ms, st.step_ms], device=device)
+        if world > 1:
+            gathered = [torch.zeros_like(busy) for _ in range(world)]
+            dist.all_gather(gathered, busy)
+        else:
+            gathered = [busy]
+        engine.measure = False
+        step_ms = max(float(x[1]) for x in gathered)
+        busys = [float(x[0]) for x in gathered]
+        bubble = 100.0 * (1.0 - (sum(busys) / len(busys)) / step_ms) if step_ms > 0 else None
+
+    if world > 1:
+        lt = torch.tensor([loss_val if loss_val is not None else 0.0], device=device)
+        dist.broadcast(lt, src=world - 1)
+        loss_val = float(lt.item())
+
+    tokens_per_step = m * mb * S
+    value = tokens_per_step / (ms / 1e3)
+    total_params = sum(int(x) for x in _allsum([n_params_local], device, world))
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec for 12-layer Transformer at PP=N (pipeline-parallel training)",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / REF_TOKENS_PER_S, 2),
+            "dtype": args.dtype,
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {
+                "model": f"{cfg.name}: {cfg.num_layers}x TransformerEncoderLayer(d_model={E}, nhead={cfg.nhead}, "
+                         f"dim_feedforward={cfg.dim_feedforward}, dropout={cfg.dropout}, {cfg.activation}, "
+                         f"{'pre' if cfg.norm_first else 'post'}-norm) + embedding/decoder V={V}",
+                "params": total_params,
+                "global_batch": m * mb,
+                "seq_len": S,
+                "micro_batch": mb,
+                "chunks": m,
+                "checkpoint": args.checkpoint,
+                "schedule": "gpipe",
+                "parallelism": f"pp{world}",
+                "balance": plan.balance,
+                "stage_imbalance": round(plan.imbalance(), 3),
+            },
+            "bubble_pct": None if bubble is None else round(bubble, 2),
+            "bubble_theory_pct": round(100.0 * (pp - 1) / (m + pp - 1), 2),
+            "loss": loss_val,
+            "baseline_note": "vs_baseline divides by the reference's ~3.5k tokens/s (BASELINE.md, 2 GPUs, fp32, "
+                             "16x d2048 model, checkpoint='never'); see BASELINE.md",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def _allsum(vals, device, world):
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t)
+    return t.tolist()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,408 @@
+// Python bindings of mipipe._C: the native runtime and the HIP kernels.
+//
+// Every kernel entry point validates shapes/dtypes/devices on the host before
+// launching (a faulting kernel can take down every GPU on the node), allocates
+// outputs through the torch caching allocator and launches on the current HIP
+// stream of the tensors' device.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/HIPGeneratorImpl.h>
+#include <ATen/core/Generator.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <mutex>
+#include <optional>
+#include <tuple>
+
+#include "kernels/kernels.h"
+#include "runtime/runtime.h"
+
+namespace py = pybind11;
+using at::Tensor;
+
+namespace mipipe {
+namespace {
+
+#define MP_CHECK(cond, ...) TORCH_CHECK(cond, "mipipe: ", __VA_ARGS__)
+
+hipStream_t cur_stream(const Tensor& t) { return at::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+// (seed, offset) from the torch device generator; `increment` philox words per
+// thread are reserved so successive ops never reuse a counter.
+std::pair<uint64_t, uint64_t> philox_draw(const at::Device& dev, uint64_t increment) {
+  auto gen = at::get_generator_or_default<at::CUDAGeneratorImpl>(
+      std::nullopt, at::cuda::detail::getDefaultCUDAGenerator(dev.index()));
+  std::lock_guard<std::mutex> lock(gen->mutex_);
+  return gen->philox_engine_inputs(increment);
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  MP_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  MP_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_same(const Tensor& a, const Tensor& b, const char* an, const char* bn) {
+  MP_CHECK(a.device() == b.device(), an, " and ", bn, " must be on the same device");
+  MP_CHECK(a.scalar_type() == b.scalar_type(), an, " and ", bn, " must have the same dtype");
+}
+
+template <typename T>
+T* ptr(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+const T* cptr(const Tensor& t) {
+  return reinterpret_cast<const T*>(t.data_ptr());
+}
+template <typename T>
+const T* optr(const std::optional<Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<const T*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------------ runtime
+int64_t py_stream_acquire(int64_t device, int64_t priority) {
+  return reinterpret_cast<int64_t>(rt::stream_acquire((int)device, (int)priority));
+}
+
+void py_stream_wait(int64_t waiting, int64_t waited, int64_t device) {
+  rt::stream_wait(reinterpret_cast<hipStream_t>(waiting), reinterpret_cast<hipStream_t>(waited), (int)device);
+}
+
+void py_peer_copy(Tensor dst, Tensor src, int64_t src_stream, int64_t dst_stream, int64_t src_dev, int64_t dst_dev) {
+  MP_CHECK(dst.is_contiguous() && src.is_contiguous(), "peer_copy needs contiguous tensors");
+  MP_CHECK(dst.nbytes() == src.nbytes(), "peer_copy size mismatch");
+  rt::peer_copy(dst.data_ptr(), (int)dst_dev, src.data_ptr(), (int)src_dev, src.nbytes(),
+                reinterpret_cast<hipStream_t>(src_stream), reinterpret_cast<hipStream_t>(dst_stream));
+}
+
+void py_gpu_sleep(int64_t us) { mipipe::gpu_sleep(us, at::hip::getCurrentHIPStream().stream()); }
+
+// ------------------------------------------------------------------ LayerNorm
+std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor, int64_t, int64_t> py_layernorm_fwd(
+    Tensor x, std::optional<Tensor> res, Tensor gamma, Tensor beta, double eps, double p, bool save_z) {
+  check_cuda(x, "x");
+  check_cuda(gamma, "gamma");
+  check_cuda(beta, "beta");
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / cols;
+  MP_CHECK(cols % 8 == 0, "layernorm: hidden size must be a multiple of 8, got ", cols);
+  MP_CHECK(ln_max_vec((int)cols) > 0, "layernorm: hidden size too large: ", cols);
+  MP_CHECK(gamma.numel() == cols && beta.numel() == cols, "layernorm: gamma/beta size mismatch");
+  check_same(x, gamma, "x", "gamma");
+  check_same(x, beta, "x", "beta");
+  if (res.has_value()) {
+    check_cuda(*res, "residual");
+    check_same(x, *res, "x", "residual");
+    MP_CHECK(res->numel() == x.numel(), "layernorm: residual shape mismatch");
+  }
+  MP_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  c10::hip::HIPGuard guard(x.device());
+  auto y = at::empty_like(x);
+  std::optional<Tensor> z;
+  if (save_z) z = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({rows}, fopt);
+  auto rstd = at::empty({rows}, fopt);
+  uint64_t seed = 0, offset = 0;
+  if (p > 0.0) std::tie(seed, offset) = philox_draw(x.device(), 4);
+  auto s = cur_stream(x);
+  if (rows == 0) return {y, z, mean, rstd, (int64_t)seed, (int64_t)offset};
+  if (x.scalar_type() == at::kBFloat16) {
+    LnArgs<bf16_t> a;
+    a.x = cptr<bf16_t>(x); a.res = optr<bf16_t>(res); a.gamma = cptr<bf16_t>(gamma); a.beta = cptr<bf16_t>(beta);
+    a.y = ptr<bf16_t>(y); a.z = z ? ptr<bf16_t>(*z) : nullptr; a.mean = ptr<float>(mean); a.rstd = ptr<float>(rstd);
+    a.rows = (int)rows; a.cols = (int)cols; a.eps = (float)eps; a.p = (float)p; a.seed = seed; a.offset = offset;
+    layernorm_fwd<bf16_t>(a, s);
+  } else if (x.scalar_type() == at::kFloat) {
+    LnArgs<float> a;
+    a.x = cptr<float>(x); a.res = optr<float>(res); a.gamma = cptr<float>(gamma); a.beta = cptr<float>(beta);
+    a.y = ptr<float>(y); a.z = z ? ptr<float>(*z) : nullptr; a.mean = ptr<float>(mean); a.rstd = ptr<float>(rstd);
+    a.rows = (int)rows; a.cols = (int)cols; a.eps = (float)eps; a.p = (float)p; a.seed = seed; a.offset = offset;
+    layernorm_fwd<float>(a, s);
+  } else {
+    MP_CHECK(false, "layernorm: unsupported dtype ", x.scalar_type());
+  }
+  return {y, z, mean, rstd, (int64_t)seed, (int64_t)offset};
+}
+
+std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor> py_layernorm_bwd(Tensor dy, Tensor z, Tensor mean,
+                                                                          Tensor rstd, Tensor gamma, double p,
+                                                                          int64_t seed, int64_t offset) {
+  check_cuda(dy, "dy");
+  check_cuda(z, "z");
+  check_same(dy, z, "dy", "z");
+  check_same(dy, gamma, "dy", "gamma");
+  const int64_t cols = dy.size(-1);
+  const int64_t rows = dy.numel() / cols;
+  MP_CHECK(z.numel() == dy.numel(), "layernorm_bwd: shape mismatch");
+  MP_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: stats size mismatch");
+  MP_CHECK(cols % 8 == 0 && ln_max_vec((int)cols) > 0, "layernorm_bwd: bad hidden size");
+  c10::hip::HIPGuard guard(dy.device());
+  auto dz = at::empty_like(dy);
+  std::optional<Tensor> dx;
+  if (p > 0.0) dx = at::empty_like(dy);
+  auto dgamma = at::empty_like(gamma);
+  auto dbeta = at::empty_like(gamma);
+  const int nparts = std::max(1, ln_bwd_parts((int)rows));
+  auto part = at::empty({2, nparts, cols}, dy.options().dtype(at::kFloat));
+  auto s = cur_stream(dy);
+  if (rows == 0) {
+    dgamma.zero_();
+    dbeta.zero_();
+    return {dz, dx, dgamma, dbeta};
+  }
+  auto fill = [&](auto& a, auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    a.dy = cptr<T>(dy); a.z = cptr<T>(z); a.mean = cptr<float>(mean); a.rstd = cptr<float>(rstd);
+    a.gamma = cptr<T>(gamma); a.dz = ptr<T>(dz); a.dx = dx ? ptr<T>(*dx) : nullptr;
+    a.dgamma_part = ptr<float>(part); a.dbeta_part = ptr<float>(part) + (size_t)nparts * cols;
+    a.dgamma = ptr<T>(dgamma); a.dbeta = ptr<T>(dbeta);
+    a.rows = (int)rows; a.cols = (int)cols; a.nparts = nparts; a.p = (float)p;
+    a.seed = (uint64_t)seed; a.offset = (uint64_t)offset;
+  };
+  if (dy.scalar_type() == at::kBFloat16) {
+    LnBwdArgs<bf16_t> a;
+    fill(a, (bf16_t*)nullptr);
+    layernorm_bwd<bf16_t>(a, s);
+  } else if (dy.scalar_type() == at::kFloat) {
+    LnBwdArgs<float> a;
+    fill(a, (float*)nullptr);
+    layernorm_bwd<float>(a, s);
+  } else {
+    MP_CHECK(false, "layernorm_bwd: unsupported dtype");
+  }
+  return {dz, dx, dgamma, dbeta};
+}
+
+// ------------------------------------------------------------------ elementwise
+template <typename F>
+void dispatch_fb(const Tensor& t, const char* what, F&& f) {
+  if (t.scalar_type() == at::kBFloat16) {
+    f((bf16_t*)nullptr);
+  } else if (t.scalar_type() == at::kFloat) {
+    f((float*)nullptr);
+  } else {
+    MP_CHECK(false, what, ": unsupported dtype ", t.scalar_type());
+  }
+}
+
+std::tuple<Tensor, int64_t, int64_t> py_bias_act_fwd(Tensor x, std::optional<Tensor> bias, int64_t act, double p) {
+  check_cuda(x, "x");
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / std::max<int64_t>(cols, 1);
+  MP_CHECK(cols % 8 == 0, "bias_act: last dim must be a multiple of 8");
+  MP_CHECK(act >= 0 && act <= 2, "bias_act: bad activation");
+  MP_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  if (bias) {
+    check_cuda(*bias, "bias");
+    check_same(x, *bias, "x", "bias");
+    MP_CHECK(bias->numel() == cols, "bias_act: bias size mismatch");
+  }
+  c10::hip::HIPGuard guard(x.device());
+  auto y = at::empty_like(x);
+  uint64_t seed = 0, offset = 0;
+  if (p > 0.0) std::tie(seed, offset) = philox_draw(x.device(), 4);
+  auto s = cur_stream(x);
+  dispatch_fb(x, "bias_act_fwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    bias_act_dropout_fwd<T>(cptr<T>(x), optr<T>(bias), ptr<T>(y), rows, (int)cols, (int)act, (float)p, seed, offset, s);
+  });
+  return {y, (int64_t)seed, (int64_t)offset};
+}
+
+Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate);
+
+std::tuple<Tensor, std::optional<Tensor>> py_bias_act_bwd(Tensor dy, Tensor saved, std::optional<Tensor> bias,
+                                                          int64_t act, double p, int64_t seed, int64_t offset,
+                                                          bool need_dbias) {
+  check_cuda(dy, "dy");
+  check_cuda(saved, "saved");
+  check_same(dy, saved, "dy", "saved");
+  MP_CHECK(dy.numel() == saved.numel(), "bias_act_bwd: shape mismatch");
+  const int64_t cols = dy.size(-1);
+  const int64_t rows = dy.numel() / std::max<int64_t>(cols, 1);
+  MP_CHECK(cols % 8 == 0, "bias_act_bwd: last dim must be a multiple of 8");
+  if (bias) MP_CHECK(bias->numel() == cols, "bias_act_bwd: bias size mismatch");
+  c10::hip::HIPGuard guard(dy.device());
+  auto dx = at::empty_like(dy);
+  auto s = cur_stream(dy);
+  dispatch_fb(dy, "bias_act_bwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    bias_act_dropout_bwd<T>(cptr<T>(dy), cptr<T>(saved), optr<T>(bias), ptr<T>(dx), rows, (int)cols, (int)act,
+                            (float)p, (uint64_t)seed, (uint64_t)offset, s);
+  });
+  std::optional<Tensor> db;
+  if (need_dbias) db = py_column_sum(dx.view({rows, cols}), std::nullopt, false);
+  return {dx, db};
+}
+
+Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate) {
+  check_cuda(x, "x");
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / std::max<int64_t>(cols, 1);
+  MP_CHECK(cols % 8 == 0, "column_sum: last dim must be a multiple of 8");
+  c10::hip::HIPGuard guard(x.device());
+  Tensor o = out.has_value() ? *out : at::empty({cols}, x.options());
+  MP_CHECK(o.numel() == cols && o.is_contiguous(), "column_sum: bad out");
+  MP_CHECK(o.scalar_type() == x.scalar_type(), "column_sum: out dtype must match input");
+  if (!out.has_value() && rows == 0) return o.zero_();
+  const int nparts = colsum_parts(rows);
+  auto part = at::empty({nparts, cols}, x.options().dtype(at::kFloat));
+  auto s = cur_stream(x);
+  dispatch_fb(x, "column_sum", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    column_sum<T>(cptr<T>(x), rows, (int)cols, ptr<float>(part), nparts, ptr<T>(o), accumulate, s);
+  });
+  return o;
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignore_index) {
+  check_cuda(logits, "logits");
+  check_cuda(target, "target");
+  MP_CHECK(target.scalar_type() == at::kLong, "cross_entropy: target must be int64");
+  MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0), "cross_entropy: expects [N, V] logits and [N] target");
+  c10::hip::HIPGuard guard(logits.device());
+  const int64_t rows = logits.size(0), V = logits.size(1);
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({rows}, fopt);
+  auto lse = at::empty({rows}, fopt);
+  auto s = cur_stream(logits);
+  dispatch_fb(logits, "cross_entropy_fwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    cross_entropy_fwd<T>(cptr<T>(logits), cptr<int64_t>(target), rows, V, ignore_index, ptr<float>(loss), ptr<float>(lse), s);
+  });
+  return {loss, lse};
+}
+
+Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int64_t ignore_index) {
+  check_cuda(logits, "logits");
+  MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0) && lse.numel() == logits.size(0),
+           "cross_entropy_bwd: shape mismatch");
+  MP_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && scale.is_cuda(), "cross_entropy_bwd: bad scale");
+  c10::hip::HIPGuard guard(logits.device());
+  auto d = at::empty_like(logits);
+  auto s = cur_stream(logits);
+  dispatch_fb(logits, "cross_entropy_bwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    cross_entropy_bwd<T>(cptr<T>(logits), cptr<int64_t>(target), cptr<float>(lse), cptr<float>(scale),
+                         logits.size(0), logits.size(1), ignore_index, ptr<T>(d), s);
+  });
+  return d;
+}
+
+// ------------------------------------------------------------------ embedding
+std::tuple<Tensor, int64_t, int64_t> py_embed_fwd(Tensor tokens, Tensor weight, std::optional<Tensor> pe,
+                                                  double scale, double p) {
+  check_cuda(tokens, "tokens");
+  check_cuda(weight, "weight");
+  MP_CHECK(tokens.scalar_type() == at::kLong && tokens.dim() == 2, "embedding: tokens must be int64 [B, S]");
+  MP_CHECK(weight.dim() == 2 && weight.size(1) % 8 == 0, "embedding: weight must be [V, E] with E % 8 == 0");
+  const int64_t S = tokens.size(1), E = weight.size(1), V = weight.size(0);
+  if (pe) {
+    check_cuda(*pe, "pe");
+    MP_CHECK(pe->scalar_type() == at::kFloat && pe->dim() == 2 && pe->size(1) == E && pe->size(0) >= S,
+             "embedding: pe must be fp32 [max_len >= S, E]");
+  }
+  c10::hip::HIPGuard guard(weight.device());
+  auto out = at::empty({tokens.size(0), S, E}, weight.options());
+  uint64_t seed = 0, offset = 0;
+  if (p > 0.0) std::tie(seed, offset) = philox_draw(weight.device(), 4);
+  auto s = cur_stream(weight);
+  dispatch_fb(weight, "embedding_fwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    embedding_fwd<T>(cptr<int64_t>(tokens), cptr<T>(weight), pe ? cptr<float>(*pe) : nullptr, ptr<T>(out),
+                     tokens.numel(), (int)S, (int)E, V, (float)scale, (float)p, seed, offset, s);
+  });
+  return {out, (int64_t)seed, (int64_t)offset};
+}
+
+void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, double p, int64_t seed, int64_t offset) {
+  check_cuda(dout, "dout");
+  check_cuda(dweight, "dweight");
+  MP_CHECK(dweight.scalar_type() == at::kFloat && dweight.dim() == 2, "embedding_bwd: dweight must be fp32 [V, E]");
+  const int64_t E = dweight.size(1), V = dweight.size(0);
+  MP_CHECK(dout.numel() == tokens.numel() * E, "embedding_bwd: shape mismatch");
+  c10::hip::HIPGuard guard(dout.device());
+  auto s = cur_stream(dout);
+  dispatch_fb(dout, "embedding_bwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    embedding_bwd<T>(cptr<int64_t>(tokens), cptr<T>(dout), ptr<float>(dweight), tokens.numel(), (int)E, V,
+                     (float)scale, (float)p, (uint64_t)seed, (uint64_t)offset, s);
+  });
+}
+
+// ------------------------------------------------------------------ optimizer
+Tensor py_sumsq(Tensor g) {
+  check_cuda(g, "g");
+  MP_CHECK(g.scalar_type() == at::kFloat, "sumsq: fp32 only");
+  c10::hip::HIPGuard guard(g.device());
+  auto out = at::empty({1}, g.options());
+  const int nparts = sumsq_parts(g.numel());
+  auto part = at::empty({nparts}, g.options());
+  sumsq(cptr<float>(g), g.numel(), ptr<float>(part), nparts, ptr<float>(out), cur_stream(g));
+  return out;
+}
+
+void py_adam(Tensor master, std::optional<Tensor> model, Tensor grad, Tensor m, Tensor v, double lr, double b1,
+             double b2, double eps, double wd, double bc1, double bc2, std::optional<Tensor> sumsq_t, double max_norm,
+             bool adamw) {
+  for (auto* t : {&master, &grad, &m, &v}) {
+    check_cuda(*t, "adam buffer");
+    MP_CHECK(t->scalar_type() == at::kFloat, "adam: master/grad/m/v must be fp32");
+    MP_CHECK(t->numel() == master.numel(), "adam: size mismatch");
+  }
+  if (model) MP_CHECK(model->numel() == master.numel() && model->is_contiguous(), "adam: model size mismatch");
+  if (sumsq_t) MP_CHECK(sumsq_t->scalar_type() == at::kFloat && sumsq_t->numel() == 1, "adam: bad sumsq");
+  c10::hip::HIPGuard guard(master.device());
+  AdamHyper h;
+  h.lr = (float)lr; h.beta1 = (float)b1; h.beta2 = (float)b2; h.eps = (float)eps; h.weight_decay = (float)wd;
+  h.bias_correction1 = (float)bc1; h.bias_correction2 = (float)bc2; h.max_norm = (float)max_norm; h.adamw = adamw;
+  auto s = cur_stream(master);
+  const float* sq = sumsq_t ? cptr<float>(*sumsq_t) : nullptr;
+  if (!model) {
+    adam_step<float>(ptr<float>(master), (float*)nullptr, cptr<float>(grad), ptr<float>(m), ptr<float>(v),
+                     master.numel(), h, sq, s);
+  } else if (model->scalar_type() == at::kBFloat16) {
+    adam_step<bf16_t>(ptr<float>(master), ptr<bf16_t>(*model), cptr<float>(grad), ptr<float>(m), ptr<float>(v),
+                      master.numel(), h, sq, s);
+  } else {
+    MP_CHECK(model->scalar_type() == at::kFloat, "adam: model copy must be bf16 or fp32");
+    adam_step<float>(ptr<float>(master), ptr<float>(*model), cptr<float>(grad), ptr<float>(m), ptr<float>(v),
+                     master.numel(), h, sq, s);
+  }
+}
+
+}  // namespace
+}  // namespace mipipe
+
+PYBIND11_MODULE(_C, m) {
+  using namespace mipipe;
+  m.doc() = "mipipe native runtime + CDNA4 HIP kernels (gfx950)";
+  // runtime
+  m.def("stream_pool_acquire", &py_stream_acquire, py::arg("device"), py::arg("priority") = -1);
+  m.def("stream_wait", &py_stream_wait);
+  m.def("peer_copy", &py_peer_copy);
+  m.def("enable_peer_access", [](std::vector<int> d) { rt::enable_peer_access(d); });
+  m.def("can_access_peer", [](int d, int q) { return rt::can_access_peer(d, q); });
+  m.def("range_push", [](const std::string& s) { rt::range_push(s); });
+  m.def("range_pop", []() { rt::range_pop(); });
+  m.def("mark", [](const std::string& s) { rt::mark(s); });
+  m.def("gpu_sleep", &py_gpu_sleep);
+  m.def("philox_draw", [](int64_t device, int64_t inc) {
+    auto r = philox_draw(at::Device(at::kCUDA, (c10::DeviceIndex)device), (uint64_t)inc);
+    return std::make_pair((int64_t)r.first, (int64_t)r.second);
+  });
+  // kernels
+  m.def("layernorm_fwd", &py_layernorm_fwd);
+  m.def("layernorm_bwd", &py_layernorm_bwd);
+  m.def("bias_act_fwd", &py_bias_act_fwd);
+  m.def("bias_act_bwd", &py_bias_act_bwd);
+  m.def("column_sum", &py_column_sum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
+  m.def("cross_entropy_fwd", &py_ce_fwd);
+  m.def("cross_entropy_bwd", &py_ce_bwd);
+  m.def("embedding_fwd", &py_embed_fwd);
+  m.def("embedding_bwd", &py_embed_bwd);
+  m.def("sumsq", &py_sumsq);
+  m.def("adam_step", &py_adam);
+}

@@ -1,0 +1,100 @@
+// Host-side launch interface of the mipipe HIP kernels.
+//
+// Kernel translation units include only HIP headers (fast to build); the
+// torch-facing bindings (../bindings.cpp) include this header and call the
+// launchers with raw pointers and the current HIP stream.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mipipe {
+
+typedef uint16_t bf16_t;
+
+// ------------------------------------------------------------------ LayerNorm
+template <typename T>
+struct LnArgs {
+  const T* x = nullptr;      // branch input (dropout applies here)
+  const T* res = nullptr;    // residual input (optional)
+  const T* gamma = nullptr;
+  const T* beta = nullptr;
+  T* y = nullptr;
+  T* z = nullptr;            // optional: saved pre-norm sum for backward
+  float* mean = nullptr;
+  float* rstd = nullptr;
+  int rows = 0, cols = 0;
+  float eps = 1e-5f;
+  float p = 0.f;
+  uint64_t seed = 0, offset = 0;
+};
+
+template <typename T>
+struct LnBwdArgs {
+  const T* dy = nullptr;
+  const T* z = nullptr;
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const T* gamma = nullptr;
+  T* dz = nullptr;           // grad of z (= grad of the residual input)
+  T* dx = nullptr;           // grad of the dropout branch (nullptr if p == 0)
+  float* dgamma_part = nullptr;  // [nparts, cols] workspace
+  float* dbeta_part = nullptr;
+  T* dgamma = nullptr;
+  T* dbeta = nullptr;
+  int rows = 0, cols = 0, nparts = 0;
+  float p = 0.f;
+  uint64_t seed = 0, offset = 0;
+};
+
+int ln_max_vec(int cols);
+int ln_bwd_parts(int rows);
+template <typename T> void layernorm_fwd(const LnArgs<T>& a, hipStream_t s);
+template <typename T> void layernorm_bwd(const LnBwdArgs<T>& a, hipStream_t s);
+
+// ------------------------------------------------------------------ elementwise
+enum Activation : int { kActNone = 0, kActRelu = 1, kActGelu = 2 };
+
+template <typename T>
+void bias_act_dropout_fwd(const T* x, const T* bias, T* y, int64_t rows, int cols, int act, float p, uint64_t seed,
+                          uint64_t offset, hipStream_t s);
+template <typename T>
+void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int64_t rows, int cols, int act, float p,
+                          uint64_t seed, uint64_t offset, hipStream_t s);
+int colsum_parts(int64_t rows);
+template <typename T>
+void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, T* out, bool accumulate, hipStream_t s);
+
+// ------------------------------------------------------------------ loss
+template <typename T>
+void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ignore_index,
+                       float* loss, float* lse, hipStream_t s);
+template <typename T>
+void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale, int64_t rows,
+                       int64_t V, int64_t ignore_index, T* dlogits, hipStream_t s);
+
+// ------------------------------------------------------------------ embedding
+template <typename T>
+void embedding_fwd(const int64_t* tokens, const T* weight, const float* pe, T* out, int64_t rows, int seq_len, int E,
+                   int64_t V, float scale, float p, uint64_t seed, uint64_t offset, hipStream_t s);
+template <typename T>
+void embedding_bwd(const int64_t* tokens, const T* dout, float* dweight, int64_t rows, int E, int64_t V, float scale,
+                   float p, uint64_t seed, uint64_t offset, hipStream_t s);
+
+// ------------------------------------------------------------------ optimizer
+struct AdamHyper {
+  float lr = 1e-3f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
+  float bias_correction1 = 1.f, bias_correction2 = 1.f;
+  float max_norm = 0.f;  // <= 0: no clipping
+  int adamw = 0;
+};
+int sumsq_parts(int64_t n);
+void sumsq(const float* g, int64_t n, float* partial, int nparts, float* out, hipStream_t s);
+template <typename M>
+void adam_step(float* master, M* model, const float* grad, float* m, float* v, int64_t n, const AdamHyper& h,
+               const float* sumsq_ptr, hipStream_t s);
+
+// ------------------------------------------------------------------ misc
+void gpu_sleep(int64_t microseconds, hipStream_t s);
+
+}  // namespace mipipe

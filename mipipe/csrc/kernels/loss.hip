@@ -1,0 +1,107 @@
+// Fused cross-entropy (log-softmax + NLL), forward and backward.
+//
+// One 256-thread workgroup per row.  Forward streams the row once with an
+// online (running max, running sum) reduction and writes only the per-row loss
+// and log-sum-exp -- the log-probabilities are never materialised.  Backward
+// streams the row once more and writes dlogits = scale * (softmax - onehot),
+// where `scale` (= dL / n_valid) is read from device memory so no host sync is
+// needed.  Vocabularies need not be multiples of 8 (28,782 in the reference
+// driver), so rows are read in 4-byte bf16 pairs when the row stride allows.
+#include "common.h"
+#include "kernels.h"
+
+namespace mipipe {
+
+namespace {
+
+constexpr int kT = 256;
+
+template <typename T>
+__global__ void __launch_bounds__(kT) ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                    int64_t V, int64_t ignore_index, float* __restrict__ loss,
+                                                    float* __restrict__ lse_out) {
+  __shared__ float sm[2 * (kT / 64)];
+  const int64_t row = blockIdx.x;
+  const T* x = logits + row * V;
+  float m = -INFINITY, s = 0.f;
+  for (int64_t c = threadIdx.x; c < V; c += kT) {
+    const float v = Io<T>::load(x + c);
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+    } else {
+      s += __expf(v - m);
+    }
+  }
+  // combine (m, s) across the wave, then the block
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const float os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if (lane == 0) {
+    sm[wid] = m;
+    sm[kT / 64 + wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = -INFINITY;
+    for (int w = 0; w < kT / 64; ++w) M = fmaxf(M, sm[w]);
+    float S = 0.f;
+    for (int w = 0; w < kT / 64; ++w) S += sm[kT / 64 + w] * __expf(sm[w] - M);
+    const float lse = M + __logf(S);
+    lse_out[row] = lse;
+    const int64_t t = target[row];
+    if (t == ignore_index || t < 0 || t >= V) {
+      loss[row] = 0.f;
+    } else {
+      loss[row] = lse - Io<T>::load(x + t);
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kT) ce_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                    const float* __restrict__ lse_in, const float* __restrict__ scale_p,
+                                                    int64_t V, int64_t ignore_index, T* __restrict__ dlogits) {
+  const int64_t row = blockIdx.x;
+  const T* x = logits + row * V;
+  T* d = dlogits + row * V;
+  const int64_t t = target[row];
+  const bool valid = !(t == ignore_index || t < 0 || t >= V);
+  const float scale = valid ? *scale_p : 0.f;
+  const float lse = lse_in[row];
+  for (int64_t c = threadIdx.x; c < V; c += kT) {
+    const float pr = __expf(Io<T>::load(x + c) - lse);
+    const float g = (pr - (c == t ? 1.f : 0.f)) * scale;
+    Io<T>::store(d + c, g);
+  }
+}
+
+}  // namespace
+
+template <typename T>
+void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ignore_index,
+                       float* loss, float* lse, hipStream_t s) {
+  if (rows == 0) return;
+  hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, V, ignore_index, loss, lse);
+}
+
+template <typename T>
+void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale, int64_t rows,
+                       int64_t V, int64_t ignore_index, T* dlogits, hipStream_t s) {
+  if (rows == 0) return;
+  hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, lse, scale, V,
+                     ignore_index, dlogits);
+}
+
+template void cross_entropy_fwd<float>(const float*, const int64_t*, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
+template void cross_entropy_fwd<bf16_t>(const bf16_t*, const int64_t*, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
+template void cross_entropy_bwd<float>(const float*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
+template void cross_entropy_bwd<bf16_t>(const bf16_t*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, bf16_t*, hipStream_t);
+
+}  // namespace mipipe

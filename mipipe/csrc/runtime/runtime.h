@@ -1,0 +1,37 @@
+// Native pipeline runtime: streams, events, peer copies, roctx ranges
+// (§5.1).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace mipipe {
+namespace rt {
+
+// Dedicated non-blocking stream on `device` (never recycled while the process
+// lives).  `priority`: 0 = normal, -1 = high (hipDeviceGetStreamPriorityRange).
+hipStream_t stream_acquire(int device, int priority);
+
+// `waiting` will not run work enqueued after this call before everything
+// enqueued on `waited` so far has finished.  Uses a pooled event.
+void stream_wait(hipStream_t waiting, hipStream_t waited, int device);
+
+// Async peer copy of `bytes` from src (on src_device) to dst (on dst_device).
+// Ordering: dst_stream's prior work -> copy on src_stream -> dst_stream.
+// The copy itself runs on src_stream (SDMA engine over xGMI).
+void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_t bytes, hipStream_t src_stream,
+               hipStream_t dst_stream);
+
+// Enables peer access between every ordered pair of `devices` (idempotent).
+void enable_peer_access(const std::vector<int>& devices);
+bool can_access_peer(int device, int peer);
+
+void range_push(const std::string& label);
+void range_pop();
+void mark(const std::string& label);
+
+}  // namespace rt
+}  // namespace mipipe

@@ -1,0 +1,341 @@
+"""Transformer blocks on the mipipe HIP ops (SURVEY §7.1 'Models').
+
+A :class:`TransformerEncoderLayer` is the drop-in equivalent of
+``nn.TransformerEncoderLayer`` as the reference driver uses it
+(``/root/reference/main.py:115-120,139-157``: post-norm, ReLU, dropout, no
+mask), but batch-first ``[B, S, E]`` and built from two *pipeline-splittable*
+halves, each a single-tensor module:
+
+* :class:`SelfAttentionBlock` -- ``LN1(x + drop(out_proj(attn(qkv(x)))))``
+  (pre-norm: ``x + drop(out_proj(attn(qkv(LN1(x)))))``);
+* :class:`FeedForwardBlock`   -- ``LN2(x + drop(W2 drop(act(W1 x))))``.
+
+Splitting at sub-layer granularity lets the balancer put stage boundaries
+between the attention and MLP halves, which matters when 12 layers are spread
+over 8 MI355X stages.
+
+Hot path per block: MFMA GEMMs with fused bias/activation/dropout epilogues,
+flash attention, fused dropout+residual+LayerNorm -- see ``mipipe.ops``.
+``from_torch`` copies weights from an ``nn.TransformerEncoderLayer`` so the
+blocks can be checked against PyTorch.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+from torch import Tensor, nn
+
+from .. import ops
+
+__all__ = [
+    "AttentionCore",
+    "AttentionOutput",
+    "PackedAttentionCore",
+    "PackedAttentionOutput",
+    "SelfAttentionBlock",
+    "FeedForwardBlock",
+    "TransformerEncoderLayer",
+    "transformer_blocks",
+    "block_flops",
+]
+
+
+class AttentionCore(nn.Module):
+    """QKV projection + scaled-dot-product attention (pre-norm: LN first).
+
+    ``x [B, S, E] -> o [B, S, E]`` (attention output before ``out_proj``).
+    """
+
+    def __init__(self, d_model: int, nhead: int, dropout: float, *, norm_first: bool, causal: bool,
+                 layer_norm_eps: float, device=None, dtype=None) -> None:
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model, self.nhead, self.head_dim = d_model, nhead, d_model // nhead
+        self.dropout, self.norm_first, self.causal, self.eps = dropout, norm_first, causal, layer_norm_eps
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d_model, d_model, **fk))
+        self.in_proj_bias = nn.Parameter(torch.empty(3 * d_model, **fk))
+        if norm_first:
+            self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
+            self.norm_bias = nn.Parameter(torch.empty(d_model, **fk))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        # nn.MultiheadAttention's init: xavier on in_proj, zero biases.
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.in_proj_bias)
+        if self.norm_first:
+            nn.init.ones_(self.norm_weight)
+            nn.init.zeros_(self.norm_bias)
+
+    def forward(self, x: Tensor) -> Tensor:
+        B, S, E = x.shape
+        H, D = self.nhead, self.head_dim
+        if self.norm_first:
+            x = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
+        qkv = ops.linear(x, self.in_proj_weight, self.in_proj_bias)
+        # [B, S, 3, H, D] -> 3 x [B, H, S, D]
+        qkv = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+        o = ops.attention(qkv[0], qkv[1], qkv[2], causal=self.causal, dropout_p=self.dropout, training=self.training)
+        return o.transpose(1, 2).reshape(B, S, E)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        e = self.d_model
+        return 2 * 3 * e * e + 4 * seq_len * e * (0.5 if self.causal else 1.0)
+
+
+class AttentionOutput(nn.Module):
+    """``out_proj`` + dropout + residual (+ LayerNorm for post-norm): ``(x, o) -> y``."""
+
+    def __init__(self, d_model: int, dropout: float, *, norm_first: bool, layer_norm_eps: float,
+                 device=None, dtype=None) -> None:
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model, self.dropout, self.norm_first, self.eps = d_model, dropout, norm_first, layer_norm_eps
+        self.out_proj_weight = nn.Parameter(torch.empty(d_model, d_model, **fk))
+        self.out_proj_bias = nn.Parameter(torch.empty(d_model, **fk))
+        if not norm_first:
+            self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
+            self.norm_bias = nn.Parameter(torch.empty(d_model, **fk))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        bound = 1.0 / math.sqrt(self.d_model)
+        nn.init.uniform_(self.out_proj_weight, -bound, bound)
+        nn.init.zeros_(self.out_proj_bias)
+        if not self.norm_first:
+            nn.init.ones_(self.norm_weight)
+            nn.init.zeros_(self.norm_bias)
+
+    def forward(self, x: Tensor, o: Tensor) -> Tensor:
+        p = self.dropout if self.training else 0.0
+        if self.norm_first:
+            a = ops.linear(o, self.out_proj_weight, self.out_proj_bias, None, p, self.training)
+            return x + a
+        a = ops.linear(o, self.out_proj_weight, self.out_proj_bias)
+        return ops.add_dropout_layer_norm(a, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return 2 * self.d_model * self.d_model
+
+
+class SelfAttentionBlock(nn.Module):
+    """Attention half of a Transformer layer: ``y = out(x, core(x))``.
+
+    Post-norm: ``LN1(x + drop(out_proj(attn(qkv(x)))))``; pre-norm:
+    ``x + drop(out_proj(attn(qkv(LN1(x)))))``.
+    """
+
+    def __init__(self, d_model: int, nhead: int, dropout: float = 0.1, *, norm_first: bool = False,
+                 causal: bool = False, layer_norm_eps: float = 1e-5, device=None, dtype=None) -> None:
+        super().__init__()
+        if d_model % nhead != 0:
+            raise ValueError("d_model must be divisible by nhead")
+        self.core = AttentionCore(d_model, nhead, dropout, norm_first=norm_first, causal=causal,
+                                  layer_norm_eps=layer_norm_eps, device=device, dtype=dtype)
+        self.out = AttentionOutput(d_model, dropout, norm_first=norm_first, layer_norm_eps=layer_norm_eps,
+                                   device=device, dtype=dtype)
+
+    def reset_parameters(self) -> None:
+        self.core.reset_parameters()
+        self.out.reset_parameters()
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.out(x, self.core(x))
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return self.core.flops_per_token(seq_len) + self.out.flops_per_token(seq_len)
+
+
+class PackedAttentionCore(nn.Module):
+    """Pipeline unit: ``x -> stack(x, core(x))`` so a stage boundary can fall
+    between the attention core and its output projection."""
+
+    def __init__(self, core: AttentionCore) -> None:
+        super().__init__()
+        self.core = core
+
+    def reset_parameters(self) -> None:
+        self.core.reset_parameters()
+
+    def forward(self, x: Tensor) -> Tensor:
+        return torch.stack((x, self.core(x)))
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return self.core.flops_per_token(seq_len)
+
+
+class PackedAttentionOutput(nn.Module):
+    """Pipeline unit: ``stack(x, o) -> out(x, o)``."""
+
+    def __init__(self, out: AttentionOutput) -> None:
+        super().__init__()
+        self.out = out
+
+    def reset_parameters(self) -> None:
+        self.out.reset_parameters()
+
+    def forward(self, packed: Tensor) -> Tensor:
+        return self.out(packed[0], packed[1])
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return self.out.flops_per_token(seq_len)
+
+
+class FeedForwardBlock(nn.Module):
+    def __init__(
+        self,
+        d_model: int,
+        dim_feedforward: int,
+        dropout: float = 0.1,
+        activation: str = "relu",
+        *,
+        norm_first: bool = False,
+        layer_norm_eps: float = 1e-5,
+        device=None,
+        dtype=None,
+    ) -> None:
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model, self.dim_feedforward = d_model, dim_feedforward
+        self.dropout = dropout
+        self.activation = activation
+        self.norm_first = norm_first
+        self.eps = layer_norm_eps
+        self.linear1_weight = nn.Parameter(torch.empty(dim_feedforward, d_model, **fk))
+        self.linear1_bias = nn.Parameter(torch.empty(dim_feedforward, **fk))
+        self.linear2_weight = nn.Parameter(torch.empty(d_model, dim_feedforward, **fk))
+        self.linear2_bias = nn.Parameter(torch.empty(d_model, **fk))
+        self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
+        self.norm_bias = nn.Parameter(torch.empty(d_model, **fk))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        for w, b in ((self.linear1_weight, self.linear1_bias), (self.linear2_weight, self.linear2_bias)):
+            nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+            bound = 1.0 / math.sqrt(w.shape[1])
+            nn.init.uniform_(b, -bound, bound)
+        nn.init.ones_(self.norm_weight)
+        nn.init.zeros_(self.norm_bias)
+
+    def forward(self, x: Tensor) -> Tensor:
+        p = self.dropout if self.training else 0.0
+        if self.norm_first:
+            h = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
+            h = ops.linear(h, self.linear1_weight, self.linear1_bias, self.activation, p, self.training)
+            h = ops.linear(h, self.linear2_weight, self.linear2_bias, None, p, self.training)
+            return x + h
+        h = ops.linear(x, self.linear1_weight, self.linear1_bias, self.activation, p, self.training)
+        h = ops.linear(h, self.linear2_weight, self.linear2_bias)
+        return ops.add_dropout_layer_norm(h, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return 2 * 2 * self.d_model * self.dim_feedforward
+
+
+class TransformerEncoderLayer(nn.Sequential):
+    """``nn.TransformerEncoderLayer`` equivalent (batch-first) as a 2-block Sequential."""
+
+    def __init__(
+        self,
+        d_model: int,
+        nhead: int,
+        dim_feedforward: int = 2048,
+        dropout: float = 0.1,
+        activation: str = "relu",
+        layer_norm_eps: float = 1e-5,
+        norm_first: bool = False,
+        causal: bool = False,
+        device=None,
+        dtype=None,
+    ) -> None:
+        super().__init__(
+            SelfAttentionBlock(d_model, nhead, dropout, norm_first=norm_first, causal=causal,
+                               layer_norm_eps=layer_norm_eps, device=device, dtype=dtype),
+            FeedForwardBlock(d_model, dim_feedforward, dropout, activation, norm_first=norm_first,
+                             layer_norm_eps=layer_norm_eps, device=device, dtype=dtype),
+        )
+
+    @torch.no_grad()
+    def load_from_torch(self, layer: nn.TransformerEncoderLayer) -> "TransformerEncoderLayer":
+        """Copies weights from ``nn.TransformerEncoderLayer``."""
+        attn, ff = self[0], self[1]
+        attn.core.in_proj_weight.copy_(layer.self_attn.in_proj_weight)
+        attn.core.in_proj_bias.copy_(layer.self_attn.in_proj_bias)
+        attn.out.out_proj_weight.copy_(layer.self_attn.out_proj.weight)
+        attn.out.out_proj_bias.copy_(layer.self_attn.out_proj.bias)
+        norm1 = attn.core if attn.core.norm_first else attn.out
+        norm1.norm_weight.copy_(layer.norm1.weight)
+        norm1.norm_bias.copy_(layer.norm1.bias)
+        ff.linear1_weight.copy_(layer.linear1.weight)
+        ff.linear1_bias.copy_(layer.linear1.bias)
+        ff.linear2_weight.copy_(layer.linear2.weight)
+        ff.linear2_bias.copy_(layer.linear2.bias)
+        ff.norm_weight.copy_(layer.norm2.weight)
+        ff.norm_bias.copy_(layer.norm2.bias)
+        return self
+
+
+def transformer_blocks(
+    num_layers: int,
+    d_model: int,
+    nhead: int,
+    dim_feedforward: int,
+    dropout: float,
+    activation: str = "relu",
+    *,
+    norm_first: bool = False,
+    causal: bool = False,
+    device=None,
+    dtype=None,
+) -> List[nn.Module]:
+    """``2 * num_layers`` single-tensor blocks (attention, MLP, attention, ...)."""
+    blocks: List[nn.Module] = []
+    for _ in range(num_layers):
+        layer = TransformerEncoderLayer(d_model, nhead, dim_feedforward, dropout, activation,
+                                        norm_first=norm_first, causal=causal, device=device, dtype=dtype)
+        blocks.extend(layer.children())
+    return blocks
+
+
+def pipeline_units(blocks: List[nn.Module]) -> List[nn.Module]:
+    """Expands every :class:`SelfAttentionBlock` into its two packed halves so a
+    pipeline stage boundary may fall inside it (see :func:`merge_units`)."""
+    units: List[nn.Module] = []
+    for b in blocks:
+        if isinstance(b, SelfAttentionBlock):
+            units += [PackedAttentionCore(b.core), PackedAttentionOutput(b.out)]
+        else:
+            units.append(b)
+    return units
+
+
+def merge_units(units: List[nn.Module]) -> List[nn.Module]:
+    """Inverse of :func:`pipeline_units` within one stage: an adjacent
+    (PackedAttentionCore, PackedAttentionOutput) pair of the same layer runs
+    unpacked (no stack copy)."""
+    out: List[nn.Module] = []
+    i = 0
+    while i < len(units):
+        u = units[i]
+        if (isinstance(u, PackedAttentionCore) and i + 1 < len(units)
+                and isinstance(units[i + 1], PackedAttentionOutput)):
+            blk = SelfAttentionBlock.__new__(SelfAttentionBlock)
+            nn.Module.__init__(blk)
+            blk.core = u.core
+            blk.out = units[i + 1].out
+            out.append(blk)
+            i += 2
+            continue
+        out.append(u)
+        i += 1
+    return out
+
+
+def block_flops(block: nn.Module, seq_len: int) -> float:
+    """Training FLOPs per token of a block (forward x 3)."""
+    f = getattr(block, "flops_per_token", None)
+    if f is None:
+        return 0.0
+    return 3.0 * f(seq_len)

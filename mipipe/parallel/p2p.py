@@ -1,0 +1,71 @@
+"""Point-to-point transport between pipeline ranks over RCCL.
+
+On ROCm the ``nccl`` backend of ``torch.distributed`` *is* RCCL; between two
+MI355X GPUs of a node a send/recv pair moves over the single xGMI link that
+joins them (every GPU pair has its own link, so stage placement order does not
+matter).  Receives are posted ahead of use so transfers overlap compute; a
+received tensor is made usable on the current compute stream by
+``Work.wait()`` (a stream wait, not a host block).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+from torch import Tensor
+
+__all__ = ["P2P", "exchange_shape"]
+
+
+class P2P:
+    """Sends/receives tensors to/from neighbour ranks of a process group."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None) -> None:
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def global_rank(self, group_rank: int) -> int:
+        if self.group is None:
+            return group_rank
+        return dist.get_global_rank(self.group, group_rank)
+
+    def isend(self, t: Tensor, dst: int) -> dist.Work:
+        return dist.isend(t.contiguous(), self.global_rank(dst), group=self.group)
+
+    def irecv(self, t: Tensor, src: int) -> dist.Work:
+        return dist.irecv(t, self.global_rank(src), group=self.group)
+
+    def send_obj_shape(self, shape: Sequence[int], dtype_code: int, dst: int, device: torch.device) -> None:
+        meta = torch.tensor([len(shape), dtype_code, *shape] + [0] * (8 - len(shape)), dtype=torch.int64, device=device)
+        dist.send(meta, self.global_rank(dst), group=self.group)
+
+    def recv_obj_shape(self, src: int, device: torch.device) -> Tuple[List[int], int]:
+        meta = torch.empty(10, dtype=torch.int64, device=device)
+        dist.recv(meta, self.global_rank(src), group=self.group)
+        m = meta.tolist()
+        n = m[0]
+        return m[2 : 2 + n], m[1]
+
+
+_DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32]
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    return _DTYPES.index(dt)
+
+
+def code_dtype(code: int) -> torch.dtype:
+    return _DTYPES[code]
+
+
+def exchange_shape(p2p: P2P, out: Optional[Tensor], device: torch.device) -> Optional[Tuple[List[int], torch.dtype]]:
+    """Stage j sends its output's (shape, dtype) to j+1 and receives its input's from j-1."""
+    recv = None
+    if p2p.rank > 0:
+        shape, code = p2p.recv_obj_shape(p2p.rank - 1, device)
+        recv = (shape, code_dtype(code))
+    if p2p.rank < p2p.world - 1 and out is not None:
+        p2p.send_obj_shape(list(out.shape), dtype_code(out.dtype), p2p.rank + 1, device)
+    return recv

@@ -1,0 +1,171 @@
+"""Multi-process pipeline engine (mipipe.parallel) on CPU with gloo, world_size 2.
+
+The distributed path the benchmark runs over RCCL is exercised here rank-for-
+rank over gloo: each rank owns a slice of the same LM; losses and gradients must
+match the unpartitioned model (dropout 0 for exact comparison)."""
+import copy
+import dataclasses
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mipipe import ops
+from mipipe.models import CONFIGS, build_lm_blocks
+from mipipe.optim import FlatAdam
+from mipipe.parallel import PipelineEngine, plan_stages, schedule_actions
+from mipipe.models.transformer import merge_units, pipeline_units
+from mipipe.parallel.stage import block_costs, stage_input_shape
+
+
+def test_schedule_actions():
+    assert schedule_actions("gpipe", 3, 2, 0) == [("F", 0), ("F", 1), ("F", 2), ("B", 2), ("B", 1), ("B", 0)]
+    a = schedule_actions("1f1b", 4, 2, 0)
+    assert a == [("F", 0), ("F", 1), ("B", 0), ("F", 2), ("B", 1), ("F", 3), ("B", 2), ("B", 3)]
+    last = schedule_actions("1f1b", 4, 2, 1)
+    assert last == [("F", 0), ("B", 0), ("F", 1), ("B", 1), ("F", 2), ("B", 2), ("F", 3), ("B", 3)]
+    for kind in ("gpipe", "1f1b"):
+        for j in range(3):
+            acts = schedule_actions(kind, 5, 3, j)
+            assert sorted(acts) == sorted([("F", i) for i in range(5)] + [("B", i) for i in range(5)])
+
+
+def test_plan_stages_balance():
+    cfg = CONFIGS["enc12_d4096"]
+    for n in (1, 2, 4, 8):
+        plan = plan_stages(cfg, n)
+        assert sum(plan.balance) == len(block_costs(cfg)) and len(plan.balance) == n
+        assert plan.imbalance() < 1.25
+    # 8 stages: split between attention and MLP halves keeps imbalance low
+    assert plan_stages(cfg, 8).imbalance() < 1.13
+
+
+def _tiny(dropout=0.0):
+    return dataclasses.replace(CONFIGS["tiny"], dropout=dropout, num_layers=2, d_model=32, nhead=4,
+                               dim_feedforward=64, vocab=50, seq_len=8)
+
+
+def _loss_fn(cfg):
+    return lambda y, t: ops.cross_entropy(y.reshape(-1, cfg.vocab), t.reshape(-1))
+
+
+def _data(cfg, m, mb):
+    g = torch.Generator().manual_seed(7)
+    tok = torch.randint(0, cfg.vocab, (m, mb, cfg.seq_len + 1), generator=g)
+    return [tok[i, :, :-1] for i in range(m)], [tok[i, :, 1:].contiguous() for i in range(m)]
+
+
+def _reference(cfg, m, mb):
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(*build_lm_blocks(cfg)).train()
+    inputs, targets = _data(cfg, m, mb)
+    total = 0.0
+    for x, t in zip(inputs, targets):
+        loss = _loss_fn(cfg)(model(x), t) / m
+        loss.backward()
+        total += float(loss.detach()) * m
+    return model, total / m
+
+
+@pytest.mark.parametrize("checkpoint", ["never", "except_last", "always"])
+def test_engine_single_rank_matches_reference(checkpoint):
+    cfg = _tiny()
+    m, mb = 3, 2
+    ref, ref_loss = _reference(cfg, m, mb)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(*build_lm_blocks(cfg)).train()
+    eng = PipelineEngine(model, chunks=m, checkpoint=checkpoint, act_shape=(mb, cfg.seq_len, cfg.d_model),
+                         act_dtype=torch.float32, loss_fn=_loss_fn(cfg), device=torch.device("cpu"))
+    inputs, targets = _data(cfg, m, mb)
+    st = eng.step(inputs, targets)
+    assert abs(float(st.loss) - ref_loss) < 1e-5
+    for (n, p), q in zip(model.named_parameters(), ref.parameters()):
+        assert torch.allclose(p.grad, q.grad, atol=1e-5), n
+
+
+def test_engine_dropout_recompute_consistent():
+    """With dropout, checkpoint='always' must reproduce 'never' exactly (RNG replay)."""
+    cfg = _tiny(dropout=0.3)
+    m, mb = 2, 2
+    grads = {}
+    for mode in ("never", "always"):
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(*build_lm_blocks(cfg)).train()
+        eng = PipelineEngine(model, chunks=m, checkpoint=mode, act_shape=(mb, cfg.seq_len, cfg.d_model),
+                             act_dtype=torch.float32, loss_fn=_loss_fn(cfg), device=torch.device("cpu"))
+        inputs, targets = _data(cfg, m, mb)
+        torch.manual_seed(99)
+        eng.step(inputs, targets)
+        grads[mode] = [p.grad.clone() for p in model.parameters()]
+    for a, b in zip(grads["never"], grads["always"]):
+        assert torch.allclose(a, b, atol=1e-6)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, checkpoint, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = _tiny()
+        m, mb = 4, 2
+        torch.manual_seed(0)
+        full = torch.nn.Sequential(*build_lm_blocks(cfg))
+        names = {id(p): n for n, p in full.named_parameters()}
+        units = pipeline_units(list(full.children()))
+        plan = plan_stages(cfg, world)
+        stage = torch.nn.Sequential(*merge_units([units[i] for i in plan.slice(rank)])).train()
+        opt = FlatAdam(stage.parameters(), lr=1e-3, max_grad_norm=0.5)
+        eng = PipelineEngine(stage, chunks=m, checkpoint=checkpoint,
+                             act_shape=stage_input_shape(cfg, plan, rank, mb),
+                             act_dtype=torch.float32, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
+                             device=torch.device("cpu"))
+        inputs, targets = _data(cfg, m, mb)
+        opt.zero_grad()
+        st = eng.step(inputs if rank == 0 else None, targets if rank == world - 1 else None)
+        opt.fold_grads()
+        grads = {names[id(p)]: p.main_grad.clone() for p in stage.parameters()}
+        sq = opt.grad_sumsq()
+        dist.all_reduce(sq)
+        q.put((rank, None if st.loss is None else float(st.loss), grads, float(sq)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("checkpoint", ["never", "except_last"])
+def test_engine_two_ranks_gloo(checkpoint):
+    cfg = _tiny()
+    m, mb = 4, 2
+    ref, ref_loss = _reference(cfg, m, mb)
+    ref_params = dict(ref.named_parameters())
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total_sq = 0.0
+    seen = set()
+    for rank, loss, grads, sq in results:
+        if loss is not None:
+            assert abs(loss - ref_loss) < 1e-5
+        for name, g in grads.items():
+            assert torch.allclose(g, ref_params[name].grad, atol=1e-5), name
+            seen.add(name)
+        total_sq = sq
+    assert seen == set(ref_params)
+    ref_sq = sum(float(p.grad.double().pow(2).sum()) for p in ref.parameters())
+    assert abs(total_sq - ref_sq) / ref_sq < 1e-4
