@@ -8,7 +8,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/HIPGeneratorImpl.h>
 #include <ATen/core/Generator.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <mutex>
 #include <optional>
@@ -25,7 +26,7 @@ namespace {
 
 #define MP_CHECK(cond, ...) TORCH_CHECK(cond, "mipipe: ", __VA_ARGS__)
 
-hipStream_t cur_stream(const Tensor& t) { return at::hip::getCurrentHIPStream(t.device().index()).stream(); }
+hipStream_t cur_stream(const Tensor& t) { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream(); }
 
 // (seed, offset) from the torch device generator; `increment` philox words per
 // thread are reserved so successive ops never reuse a counter.
@@ -75,7 +76,7 @@ void py_peer_copy(Tensor dst, Tensor src, int64_t src_stream, int64_t dst_stream
                 reinterpret_cast<hipStream_t>(src_stream), reinterpret_cast<hipStream_t>(dst_stream));
 }
 
-void py_gpu_sleep(int64_t us) { mipipe::gpu_sleep(us, at::hip::getCurrentHIPStream().stream()); }
+void py_gpu_sleep(int64_t us) { mipipe::gpu_sleep(us, at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()); }
 
 // ------------------------------------------------------------------ LayerNorm
 std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor, int64_t, int64_t> py_layernorm_fwd(
@@ -96,7 +97,7 @@ std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor, int64_t, int64_t> py_l
     MP_CHECK(res->numel() == x.numel(), "layernorm: residual shape mismatch");
   }
   MP_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
-  c10::hip::HIPGuard guard(x.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty_like(x);
   std::optional<Tensor> z;
   if (save_z) z = at::empty_like(x);
@@ -137,7 +138,7 @@ std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor> py_layernorm_bwd(Tenso
   MP_CHECK(z.numel() == dy.numel(), "layernorm_bwd: shape mismatch");
   MP_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: stats size mismatch");
   MP_CHECK(cols % 8 == 0 && ln_max_vec((int)cols) > 0, "layernorm_bwd: bad hidden size");
-  c10::hip::HIPGuard guard(dy.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   auto dz = at::empty_like(dy);
   std::optional<Tensor> dx;
   if (p > 0.0) dx = at::empty_like(dy);
@@ -198,7 +199,7 @@ std::tuple<Tensor, int64_t, int64_t> py_bias_act_fwd(Tensor x, std::optional<Ten
     check_same(x, *bias, "x", "bias");
     MP_CHECK(bias->numel() == cols, "bias_act: bias size mismatch");
   }
-  c10::hip::HIPGuard guard(x.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty_like(x);
   uint64_t seed = 0, offset = 0;
   if (p > 0.0) std::tie(seed, offset) = philox_draw(x.device(), 4);
@@ -223,7 +224,7 @@ std::tuple<Tensor, std::optional<Tensor>> py_bias_act_bwd(Tensor dy, Tensor save
   const int64_t rows = dy.numel() / std::max<int64_t>(cols, 1);
   MP_CHECK(cols % 8 == 0, "bias_act_bwd: last dim must be a multiple of 8");
   if (bias) MP_CHECK(bias->numel() == cols, "bias_act_bwd: bias size mismatch");
-  c10::hip::HIPGuard guard(dy.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   auto dx = at::empty_like(dy);
   auto s = cur_stream(dy);
   dispatch_fb(dy, "bias_act_bwd", [&](auto* tag) {
@@ -240,8 +241,7 @@ Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate) {
   check_cuda(x, "x");
   const int64_t cols = x.size(-1);
   const int64_t rows = x.numel() / std::max<int64_t>(cols, 1);
-  MP_CHECK(cols % 8 == 0, "column_sum: last dim must be a multiple of 8");
-  c10::hip::HIPGuard guard(x.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Tensor o = out.has_value() ? *out : at::empty({cols}, x.options());
   MP_CHECK(o.numel() == cols && o.is_contiguous(), "column_sum: bad out");
   MP_CHECK(o.scalar_type() == x.scalar_type(), "column_sum: out dtype must match input");
@@ -262,7 +262,7 @@ std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignor
   check_cuda(target, "target");
   MP_CHECK(target.scalar_type() == at::kLong, "cross_entropy: target must be int64");
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0), "cross_entropy: expects [N, V] logits and [N] target");
-  c10::hip::HIPGuard guard(logits.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
   const int64_t rows = logits.size(0), V = logits.size(1);
   auto fopt = logits.options().dtype(at::kFloat);
   auto loss = at::empty({rows}, fopt);
@@ -280,7 +280,7 @@ Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int64_t
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0) && lse.numel() == logits.size(0),
            "cross_entropy_bwd: shape mismatch");
   MP_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && scale.is_cuda(), "cross_entropy_bwd: bad scale");
-  c10::hip::HIPGuard guard(logits.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
   auto d = at::empty_like(logits);
   auto s = cur_stream(logits);
   dispatch_fb(logits, "cross_entropy_bwd", [&](auto* tag) {
@@ -304,7 +304,7 @@ std::tuple<Tensor, int64_t, int64_t> py_embed_fwd(Tensor tokens, Tensor weight, 
     MP_CHECK(pe->scalar_type() == at::kFloat && pe->dim() == 2 && pe->size(1) == E && pe->size(0) >= S,
              "embedding: pe must be fp32 [max_len >= S, E]");
   }
-  c10::hip::HIPGuard guard(weight.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(weight.device());
   auto out = at::empty({tokens.size(0), S, E}, weight.options());
   uint64_t seed = 0, offset = 0;
   if (p > 0.0) std::tie(seed, offset) = philox_draw(weight.device(), 4);
@@ -323,7 +323,7 @@ void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, doub
   MP_CHECK(dweight.scalar_type() == at::kFloat && dweight.dim() == 2, "embedding_bwd: dweight must be fp32 [V, E]");
   const int64_t E = dweight.size(1), V = dweight.size(0);
   MP_CHECK(dout.numel() == tokens.numel() * E, "embedding_bwd: shape mismatch");
-  c10::hip::HIPGuard guard(dout.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dout.device());
   auto s = cur_stream(dout);
   dispatch_fb(dout, "embedding_bwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
@@ -336,7 +336,7 @@ void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, doub
 Tensor py_sumsq(Tensor g) {
   check_cuda(g, "g");
   MP_CHECK(g.scalar_type() == at::kFloat, "sumsq: fp32 only");
-  c10::hip::HIPGuard guard(g.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
   auto out = at::empty({1}, g.options());
   const int nparts = sumsq_parts(g.numel());
   auto part = at::empty({nparts}, g.options());
@@ -354,7 +354,7 @@ void py_adam(Tensor master, std::optional<Tensor> model, Tensor grad, Tensor m, 
   }
   if (model) MP_CHECK(model->numel() == master.numel() && model->is_contiguous(), "adam: model size mismatch");
   if (sumsq_t) MP_CHECK(sumsq_t->scalar_type() == at::kFloat && sumsq_t->numel() == 1, "adam: bad sumsq");
-  c10::hip::HIPGuard guard(master.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(master.device());
   AdamHyper h;
   h.lr = (float)lr; h.beta1 = (float)b1; h.beta2 = (float)b2; h.eps = (float)eps; h.weight_decay = (float)wd;
   h.bias_correction1 = (float)bc1; h.bias_correction2 = (float)bc2; h.max_norm = (float)max_norm; h.adamw = adamw;

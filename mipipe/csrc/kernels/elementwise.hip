@@ -108,6 +108,20 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ 
   }
 }
 
+// Same for widths that are not a multiple of 8 (e.g. a 28,782-word decoder bias):
+// one column per thread, consecutive threads on consecutive columns.
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_part_scalar_kernel(const T* __restrict__ x, int rows, int cols,
+                                                                 int rows_per, float* __restrict__ part) {
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(rows, r0 + rows_per);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cols; c += gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int r = r0; r < r1; ++r) acc += Io<T>::load(x + (size_t)r * cols + c);
+    part[(size_t)blockIdx.y * cols + c] = acc;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ part, int nparts, int cols,
                                                            T* __restrict__ out, int accumulate) {
@@ -163,9 +177,14 @@ template <typename T>
 void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, T* out, bool accumulate, hipStream_t s) {
   if (rows == 0 || cols == 0) return;
   const int rows_per = (int)((rows + nparts - 1) / nparts);
-  const int nvec = cols / 8;
-  dim3 g1((unsigned)((nvec + 255) / 256), (unsigned)nparts);
-  hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+  if (cols % 8 == 0) {
+    const int nvec = cols / 8;
+    dim3 g1((unsigned)((nvec + 255) / 256), (unsigned)nparts);
+    hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+  } else {
+    dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);
+    hipLaunchKernelGGL((colsum_part_scalar_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+  }
   hipLaunchKernelGGL((colsum_final_kernel<T>), dim3((cols + 255) / 256), dim3(256), 0, s, part, nparts, cols, out,
                      accumulate ? 1 : 0);
 }

@@ -68,8 +68,7 @@ def test_layernorm_dropout_mask_consistent(k):
     torch.manual_seed(5)
     y2 = add_dropout_layer_norm(x, r, w, b, 1e-5, p, True)
     assert torch.equal(y, y2)
-    # Recover the mask from a reference: LN of (x*mask/(1-p)).
-    y.sum().backward()
+    y.backward(torch.randn_like(y))
     g = x.grad
     # gradient is exactly zero where the element was dropped
     dropped = (g == 0).float().mean().item()
@@ -108,10 +107,11 @@ def test_bias_act_dropout_stats(k):
     assert torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1 / 0.75))
 
 
-def test_column_sum(k):
-    x = torch.randn(1000, 264, device=DEV)
+@pytest.mark.parametrize("cols", [264, 28782])
+def test_column_sum(k, cols):
+    x = torch.randn(1000, cols, device=DEV)
     assert torch.allclose(k.column_sum(x), x.sum(0), atol=1e-3)
-    out = torch.ones(264, device=DEV)
+    out = torch.ones(cols, device=DEV)
     k.column_sum(x, out, True)
     assert torch.allclose(out, x.sum(0) + 1, atol=1e-3)
 
