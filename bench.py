@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="enc12_d4096")
-    ap.add_argument("--micro-batch", type=int, default=16, help="sequences per micro-batch")
+    ap.add_argument("--micro-batch", type=int, default=32, help="sequences per micro-batch")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
     ap.add_argument("--checkpoint", default="never", choices=["never", "except_last", "always"])

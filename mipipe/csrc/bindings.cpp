@@ -257,8 +257,13 @@ Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate) {
 }
 
 // ------------------------------------------------------------------ cross entropy
+void check_rows(const Tensor& t, const char* name) {
+  MP_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  MP_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) >= t.size(1), name, " must be 2-D with unit column stride");
+}
+
 std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignore_index) {
-  check_cuda(logits, "logits");
+  check_rows(logits, "logits");
   check_cuda(target, "target");
   MP_CHECK(target.scalar_type() == at::kLong, "cross_entropy: target must be int64");
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0), "cross_entropy: expects [N, V] logits and [N] target");
@@ -270,23 +275,24 @@ std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignor
   auto s = cur_stream(logits);
   dispatch_fb(logits, "cross_entropy_fwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    cross_entropy_fwd<T>(cptr<T>(logits), cptr<int64_t>(target), rows, V, ignore_index, ptr<float>(loss), ptr<float>(lse), s);
+    cross_entropy_fwd<T>(cptr<T>(logits), cptr<int64_t>(target), rows, V, logits.stride(0), ignore_index,
+                         ptr<float>(loss), ptr<float>(lse), s);
   });
   return {loss, lse};
 }
 
 Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int64_t ignore_index) {
-  check_cuda(logits, "logits");
+  check_rows(logits, "logits");
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0) && lse.numel() == logits.size(0),
            "cross_entropy_bwd: shape mismatch");
   MP_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && scale.is_cuda(), "cross_entropy_bwd: bad scale");
   at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
-  auto d = at::empty_like(logits);
+  auto d = at::empty({logits.size(0), logits.size(1)}, logits.options());
   auto s = cur_stream(logits);
   dispatch_fb(logits, "cross_entropy_bwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     cross_entropy_bwd<T>(cptr<T>(logits), cptr<int64_t>(target), cptr<float>(lse), cptr<float>(scale),
-                         logits.size(0), logits.size(1), ignore_index, ptr<T>(d), s);
+                         logits.size(0), logits.size(1), logits.stride(0), ignore_index, ptr<T>(d), s);
   });
   return d;
 }
@@ -330,6 +336,99 @@ void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, doub
     embedding_bwd<T>(cptr<int64_t>(tokens), cptr<T>(dout), ptr<float>(dweight), tokens.numel(), (int)E, V,
                      (float)scale, (float)p, (uint64_t)seed, (uint64_t)offset, s);
   });
+}
+
+// ------------------------------------------------------------------ GEMM
+void check_bf16_2d(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  MP_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  MP_CHECK(t.dim() == 2, name, " must be 2-D");
+}
+
+bool py_gemm_supported(int64_t M, int64_t N, int64_t K) { return gemm_supported(M, N, K); }
+
+// y[M,N] = act(x[M,K] . w[N,K]^T + bias) with dropout; optional pre-activation.
+std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor x, Tensor w,
+                                                                           std::optional<Tensor> bias, int64_t act,
+                                                                           double p, bool save_preact) {
+  check_bf16_2d(x, "x");
+  check_bf16_2d(w, "w");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  MP_CHECK(w.size(1) == K, "linear_fwd: inner dims differ");
+  MP_CHECK(gemm_supported(M, N, K), "linear_fwd: unsupported shape ", M, "x", N, "x", K);
+  MP_CHECK(act >= 0 && act <= 2 && p >= 0.0 && p < 1.0, "linear_fwd: bad act/p");
+  if (bias) {
+    check_cuda(*bias, "bias");
+    MP_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N, "linear_fwd: bad bias");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({M, N}, x.options());
+  std::optional<Tensor> pre;
+  if (save_preact) pre = at::empty({M, N}, x.options());
+  uint64_t seed = 0, offset = 0;
+  if (p > 0.0) std::tie(seed, offset) = philox_draw(x.device(), 4);
+  GemmArgs g;
+  g.A = x.data_ptr(); g.B = w.data_ptr(); g.C = y.data_ptr();
+  g.bias = bias ? bias->data_ptr() : nullptr; g.aux = pre ? pre->data_ptr() : nullptr;
+  g.lda = K; g.ldb = K; g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreBf16; g.act = (int)act; g.p = (float)p;
+  g.seed = seed; g.offset = offset;
+  gemm_bf16(g, cur_stream(x));
+  return {y, pre, (int64_t)seed, (int64_t)offset};
+}
+
+// dx[M,K] = dy[M,N] . w[N,K]
+Tensor py_linear_dgrad(Tensor dy, Tensor w) {
+  check_bf16_2d(dy, "dy");
+  check_bf16_2d(w, "w");
+  const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
+  MP_CHECK(w.size(0) == N, "linear_dgrad: inner dims differ");
+  MP_CHECK(gemm_supported(M, K, N), "linear_dgrad: unsupported shape");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  auto dx = at::empty({M, K}, dy.options());
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = w.data_ptr(); g.C = dx.data_ptr();
+  g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)M; g.N = (int)K; g.K = (int)N;
+  g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreBf16;
+  gemm_bf16(g, cur_stream(dy));
+  return dx;
+}
+
+// main_grad[N,K] (fp32) += dy[T,N]^T . x[T,K]
+void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad) {
+  check_bf16_2d(dy, "dy");
+  check_bf16_2d(x, "x");
+  check_cuda(main_grad, "main_grad");
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  MP_CHECK(x.size(0) == T, "linear_wgrad: token dims differ");
+  MP_CHECK(main_grad.scalar_type() == at::kFloat && main_grad.numel() == N * K, "linear_wgrad: bad main_grad");
+  MP_CHECK(gemm_supported(N, K, T), "linear_wgrad: unsupported shape");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = x.data_ptr(); g.C = main_grad.data_ptr();
+  g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)T;
+  g.a_kc = false; g.b_kc = false; g.epi = kEpiAccumF32;
+  gemm_bf16(g, cur_stream(dy));
+}
+
+// Generic test entry: C[M,N] (fp32) = A . B with A given [M,K] (a_kc) or [K,M],
+// B given [N,K] (b_kc) or [K,N].
+Tensor py_gemm_f32(Tensor a, Tensor b, bool a_kc, bool b_kc) {
+  check_bf16_2d(a, "a");
+  check_bf16_2d(b, "b");
+  const int64_t M = a_kc ? a.size(0) : a.size(1);
+  const int64_t K = a_kc ? a.size(1) : a.size(0);
+  const int64_t N = b_kc ? b.size(0) : b.size(1);
+  MP_CHECK((b_kc ? b.size(1) : b.size(0)) == K, "gemm: inner dims differ");
+  MP_CHECK(gemm_supported(M, N, K), "gemm: unsupported shape");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto c = at::empty({M, N}, a.options().dtype(at::kFloat));
+  GemmArgs g;
+  g.A = a.data_ptr(); g.B = b.data_ptr(); g.C = c.data_ptr();
+  g.lda = a.size(1); g.ldb = b.size(1); g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.a_kc = a_kc; g.b_kc = b_kc; g.epi = kEpiStoreF32;
+  gemm_bf16(g, cur_stream(a));
+  return c;
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -403,6 +502,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("cross_entropy_bwd", &py_ce_bwd);
   m.def("embedding_fwd", &py_embed_fwd);
   m.def("embedding_bwd", &py_embed_bwd);
+  m.def("gemm_supported", &py_gemm_supported);
+  m.def("linear_fwd", &py_linear_fwd);
+  m.def("linear_dgrad", &py_linear_dgrad);
+  m.def("linear_wgrad", &py_linear_wgrad);
+  m.def("gemm_f32", &py_gemm_f32);
   m.def("sumsq", &py_sumsq);
   m.def("adam_step", &py_adam);
 }

@@ -23,68 +23,70 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return cdf + x * pdf;
 }
 
-template <typename T, int ACT>
-__global__ void __launch_bounds__(256) bias_act_fwd_kernel(const T* __restrict__ x, const T* __restrict__ bias,
-                                                           T* __restrict__ y, int64_t nvec, int cols, float p,
-                                                           uint32_t threshold, uint64_t seed, uint64_t offset) {
+// Dropout mask layout shared with the GEMM epilogue (gemm.hip): element
+// (row, col) uses word (row & 3) of Philox(seed, (row / 4) * cols + col, offset).
+// Each thread therefore owns a 4-row x 8-column tile: 8 Philox calls produce
+// exactly its 32 mask words.
+template <typename T, int ACT, bool BWD>
+__global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in, const T* __restrict__ saved,
+                                                       const T* __restrict__ bias, T* __restrict__ out,
+                                                       int64_t rows, int cols, float p, uint32_t threshold,
+                                                       uint64_t seed, uint64_t offset) {
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = v * 8;
-    float a[8];
-    Io<T>::load8(x + e, a);
+  const int cvec = cols >> 3;
+  const int64_t quads = (rows + 3) >> 2;
+  const int64_t ntiles = quads * cvec;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = t / cvec;
+    const int c0 = (int)(t - q * cvec) * 8;
+    float b[8];
     if (bias != nullptr) {
-      float b[8];
-      Io<T>::load8(bias + (int)(e % cols), b);
+      Io<T>::load8(bias + c0, b);
+    } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] += b[i];
+      for (int i = 0; i < 8; ++i) b[i] = 0.f;
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (ACT == kActRelu) a[i] = fmaxf(a[i], 0.f);
-      if (ACT == kActGelu) a[i] = gelu_f(a[i]);
-    }
+    uint32_t w[8][4];
     if (p > 0.f) {
-      const uint32_t keep = dropout_keep8(seed, offset, (uint64_t)e, threshold);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = ((keep >> i) & 1) ? a[i] * scale : 0.f;
-    }
-    Io<T>::store8(y + e, a);
-  }
-}
-
-template <typename T, int ACT>
-__global__ void __launch_bounds__(256) bias_act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ saved,
-                                                           const T* __restrict__ bias, T* __restrict__ dx,
-                                                           int64_t nvec, int cols, float p, uint32_t threshold,
-                                                           uint64_t seed, uint64_t offset) {
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = v * 8;
-    float g[8];
-    Io<T>::load8(dy + e, g);
-    if (ACT == kActRelu) {
-      float s[8];
-      Io<T>::load8(saved + e, s);  // the op's output
-#pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = s[i] > 0.f ? g[i] : 0.f;
-    } else if (ACT == kActGelu) {
-      float s[8];
-      Io<T>::load8(saved + e, s);  // pre-bias input
-      if (bias != nullptr) {
-        float b[8];
-        Io<T>::load8(bias + (int)(e % cols), b);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s[i] += b[i];
+      for (int i = 0; i < 8; ++i) {
+        const uint4 r = Philox(seed, (uint64_t)q * (uint64_t)cols + (uint64_t)(c0 + i), offset).next4();
+        w[i][0] = r.x; w[i][1] = r.y; w[i][2] = r.z; w[i][3] = r.w;
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] *= gelu_grad(s[i]);
     }
-    if (p > 0.f) {
-      const uint32_t keep = dropout_keep8(seed, offset, (uint64_t)e, threshold);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = ((keep >> i) & 1) ? g[i] * scale : 0.f;
+    for (int rr = 0; rr < 4; ++rr) {
+      const int64_t row = q * 4 + rr;
+      if (row >= rows) break;
+      const int64_t e = row * cols + c0;
+      float a[8];
+      Io<T>::load8(in + e, a);
+      if (!BWD) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float v = a[i] + b[i];
+          if (ACT == kActRelu) v = fmaxf(v, 0.f);
+          if (ACT == kActGelu) v = gelu_f(v);
+          if (p > 0.f) v = w[i][rr] >= threshold ? v * scale : 0.f;
+          a[i] = v;
+        }
+      } else {
+        if (ACT != kActNone) {
+          float sv[8];
+          Io<T>::load8(saved + e, sv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (ACT == kActRelu) a[i] = sv[i] > 0.f ? a[i] : 0.f;   // saved = the op's output
+            if (ACT == kActGelu) a[i] *= gelu_grad(sv[i] + b[i]);  // saved = pre-bias input
+          }
+        }
+        if (p > 0.f) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = w[i][rr] >= threshold ? a[i] * scale : 0.f;
+        }
+      }
+      Io<T>::store8(out + e, a);
     }
-    Io<T>::store8(dx + e, g);
   }
 }
 
@@ -139,32 +141,30 @@ int64_t grid_for(int64_t nvec) {
 
 }  // namespace
 
+template <typename T, bool BWD>
+void launch_bias_act(const T* in, const T* saved, const T* bias, T* out, int64_t rows, int cols, int act, float p,
+                     uint64_t seed, uint64_t offset, hipStream_t s) {
+  const int64_t ntiles = ((rows + 3) / 4) * (cols / 8);
+  if (ntiles == 0) return;
+  const dim3 grid((unsigned)grid_for(ntiles)), block(256);
+  const uint32_t thr = dropout_threshold(p);
+  switch (act) {
+    case kActNone: hipLaunchKernelGGL((bias_act_kernel<T, kActNone, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset); break;
+    case kActRelu: hipLaunchKernelGGL((bias_act_kernel<T, kActRelu, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset); break;
+    case kActGelu: hipLaunchKernelGGL((bias_act_kernel<T, kActGelu, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset); break;
+  }
+}
+
 template <typename T>
 void bias_act_dropout_fwd(const T* x, const T* bias, T* y, int64_t rows, int cols, int act, float p, uint64_t seed,
                           uint64_t offset, hipStream_t s) {
-  const int64_t nvec = rows * cols / 8;
-  if (nvec == 0) return;
-  const dim3 grid((unsigned)grid_for(nvec)), block(256);
-  const uint32_t thr = dropout_threshold(p);
-  switch (act) {
-    case kActNone: hipLaunchKernelGGL((bias_act_fwd_kernel<T, kActNone>), grid, block, 0, s, x, bias, y, nvec, cols, p, thr, seed, offset); break;
-    case kActRelu: hipLaunchKernelGGL((bias_act_fwd_kernel<T, kActRelu>), grid, block, 0, s, x, bias, y, nvec, cols, p, thr, seed, offset); break;
-    case kActGelu: hipLaunchKernelGGL((bias_act_fwd_kernel<T, kActGelu>), grid, block, 0, s, x, bias, y, nvec, cols, p, thr, seed, offset); break;
-  }
+  launch_bias_act<T, false>(x, nullptr, bias, y, rows, cols, act, p, seed, offset, s);
 }
 
 template <typename T>
 void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int64_t rows, int cols, int act, float p,
                           uint64_t seed, uint64_t offset, hipStream_t s) {
-  const int64_t nvec = rows * cols / 8;
-  if (nvec == 0) return;
-  const dim3 grid((unsigned)grid_for(nvec)), block(256);
-  const uint32_t thr = dropout_threshold(p);
-  switch (act) {
-    case kActNone: hipLaunchKernelGGL((bias_act_bwd_kernel<T, kActNone>), grid, block, 0, s, dy, saved, bias, dx, nvec, cols, p, thr, seed, offset); break;
-    case kActRelu: hipLaunchKernelGGL((bias_act_bwd_kernel<T, kActRelu>), grid, block, 0, s, dy, saved, bias, dx, nvec, cols, p, thr, seed, offset); break;
-    case kActGelu: hipLaunchKernelGGL((bias_act_bwd_kernel<T, kActGelu>), grid, block, 0, s, dy, saved, bias, dx, nvec, cols, p, thr, seed, offset); break;
-  }
+  launch_bias_act<T, true>(dy, saved, bias, dx, rows, cols, act, p, seed, offset, s);
 }
 
 int colsum_parts(int64_t rows) {

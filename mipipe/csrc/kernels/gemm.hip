@@ -1,0 +1,445 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues.
+//
+//   C[M, N] = A[M, K] . B[K, N]      (bf16 operands, fp32 accumulation)
+//
+// Every Transformer linear runs on this one kernel template, in three
+// operand layouts:
+//   forward  Y  = X  . W^T   A = X  [T, K] (K-contiguous)  B = W  [N, K] (K-contiguous)
+//   dgrad    dX = dY . W     A = dY [T, N] (K-contiguous)  B = W  [N, K] read as [K, N] (N-contiguous)
+//   wgrad    dW += dY^T . X  A = dY read as [K=T, M] (M-contiguous), B = X [K=T, N] (N-contiguous)
+// Operand tiles are staged into LDS in their memory layout (16-byte global
+// loads, coalesced); K-contiguous fragments are read with ds_read_b128 and
+// K-strided ones with the gfx950 transposing read ds_read_b64_tr_b16, so no
+// layout ever needs a transpose pass in HBM.  Both LDS images are XOR-swizzled
+// so the 16-lane read groups hit distinct banks (T2/T10).
+//
+// Geometry: 128x128x64 block tile, 4 waves (2x2), 64x64 per wave as 4x4
+// v_mfma_f32_16x16x32_bf16 tiles; global->register prefetch of tile k+1 is
+// issued before the MFMAs of tile k and written to the other LDS buffer after
+// them (T14), one barrier per K-tile.  Block ids are remapped so consecutive
+// tiles of an 8-row group share an XCD's L2 (T1, bijective form).
+//
+// Epilogues:
+//   kEpiStoreBf16 -- + bias, activation (ReLU/GELU), dropout (Philox mask in
+//                    the "column-quad" layout shared with the elementwise
+//                    backward), optional pre-activation aux output, bf16 store;
+//   kEpiAccumF32  -- C(fp32) += acc  (weight gradients straight into main_grad);
+//   kEpiStoreF32  -- fp32 store.
+#include "common.h"
+#include "kernels.h"
+
+namespace mipipe {
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int kThreads = 256;
+constexpr int kTileBytes = BM * BK * 2;  // 16 KiB per operand tile (BM == BN)
+constexpr int kBufBytes = 2 * kTileBytes;  // A + B
+constexpr int kSmemBytes = 2 * kBufBytes;  // double buffered = 64 KiB
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ---- LDS images --------------------------------------------------------------
+// K-contiguous tile [128 rows (i)][64 k]: 128-byte rows, 16-byte chunk c of
+// row r stored at chunk c ^ ((r >> 1) & 7).
+__device__ __forceinline__ int kc_off(int r, int c16) { return r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4); }
+
+// I-contiguous tile [64 rows (k)][128 i]: 256-byte rows, 8-byte chunk c of row
+// r stored at chunk c ^ (4 * rk(r)), rk(r) = (r & 3) | (((r >> 3) & 1) << 2).
+__device__ __forceinline__ int ic_rk(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int ic_off(int r, int c8) { return r * 256 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
+
+// ---- global -> registers -> LDS staging ------------------------------------------
+template <bool KC>
+struct Stager {
+  uint4 v[4];
+  // Loads the tile whose first element is (i0, k0) of an operand of leading
+  // dimension ld.
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, int64_t ld, int i0, int k0, int tid) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int id = tid + u * kThreads;
+      const bf16_t* p;
+      if (KC) {
+        const int r = id >> 3, c = id & 7;
+        p = base + (int64_t)(i0 + r) * ld + k0 + c * 8;
+      } else {
+        const int r = id >> 4, c = id & 15;
+        p = base + (int64_t)(k0 + r) * ld + i0 + c * 8;
+      }
+      v[u] = *reinterpret_cast<const uint4*>(p);
+    }
+  }
+  __device__ __forceinline__ void store(char* tile, int tid) const {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int id = tid + u * kThreads;
+      int off;
+      if (KC) {
+        off = kc_off(id >> 3, id & 7);
+      } else {
+        off = ic_off(id >> 4, (id & 15) * 2);
+      }
+      *reinterpret_cast<uint4*>(tile + off) = v[u];
+    }
+  }
+};
+
+// ---- LDS -> fragment ---------------------------------------------------------------
+// Fragment of the 16x16x32 operand for rows/cols [ib, ib+16) and k-step s:
+// lane l holds element (i = ib + (l & 15), k = 32 s + 8 (l >> 4) + j), j = 0..7.
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag(const char* tile, int ib, int s, int lane) {
+  if (KC) {
+    const int r = ib + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(tile + kc_off(r, c));
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int r0 = 32 * s + 8 * g + q;
+    const int c8 = (ib >> 2) + p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0, c8)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0 + 4, c8)));
+    const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, both);
+  }
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// Bijective XCD-aware remap + grouped (8 tile-rows) ordering.
+__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  int wg = bid;
+  if (nwg > 8) {
+    const int xcd = bid & 7, local = bid >> 3;
+    const int q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  }
+  constexpr int G = 8;
+  const int group = wg / (G * tiles_n);
+  const int first_m = group * G;
+  const int gsize = min(tiles_m - first_m, G);
+  const int in_group = wg % (G * tiles_n);
+  tm = first_m + in_group % gsize;
+  tn = in_group / gsize;
+}
+
+template <bool A_KC, bool B_KC, int EPI, int ACT>
+__global__ void __launch_bounds__(kThreads, 2) gemm_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  int tm, tn;
+  tile_coords(g.M / BM, g.N / BN, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(g.A);
+  const bf16_t* B = reinterpret_cast<const bf16_t*>(g.B);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stager<A_KC> sa;
+  Stager<B_KC> sb;
+  const int nk = g.K / BK;
+
+  sa.load(A, g.lda, m0, 0, tid);
+  sb.load(B, g.ldb, n0, 0, tid);
+  sa.store(smem, tid);
+  sb.store(smem + kTileBytes, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * kBufBytes;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(A, g.lda, m0, (kt + 1) * BK, tid);
+      sb.load(B, g.ldb, n0, (kt + 1) * BK, tid);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) af[t] = read_frag<A_KC>(cur, wm * 64 + 16 * t, s, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bfr[t] = read_frag<B_KC>(cur + kTileBytes, wn * 64 + 16 * t, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* nxt = smem + ((kt + 1) & 1) * kBufBytes;
+      sa.store(nxt, tid);
+      sb.store(nxt + kTileBytes, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  const int quad = lane >> 4, col_in = lane & 15;
+  const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row0 = m0 + wm * 64 + 16 * i + 4 * quad;  // rows row0 .. row0+3
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn * 64 + 16 * j + col_in;
+      f32x4 v = acc[i][j];
+      if (EPI == kEpiAccumF32) {
+        float* C = reinterpret_cast<float*>(g.C);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* p = C + (int64_t)(row0 + r) * g.ldc + col;
+          *p += v[r];
+        }
+      } else if (EPI == kEpiStoreF32) {
+        float* C = reinterpret_cast<float*>(g.C);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(int64_t)(row0 + r) * g.ldc + col] = v[r];
+      } else {
+        bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+        const float b = g.bias != nullptr ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
+        float pre[4], out[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pre[r] = v[r] + b;
+          out[r] = ACT == kActRelu ? fmaxf(pre[r], 0.f) : (ACT == kActGelu ? gelu_f(pre[r]) : pre[r]);
+        }
+        if (g.p > 0.f) {
+          // column-quad mask layout: subsequence (row/4) * N + col, word row & 3
+          const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
+          const uint4 w = Philox(g.seed, sub, g.offset).next4();
+          const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[r] = ws[r] >= g.threshold ? out[r] * pscale : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          C[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out[r]);
+          if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre[r]);
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================
+// Large-tile variant: 256x256x64, 8 waves (2 M x 4 N, 128x64 per wave as 8x4
+// MFMA tiles), operand tiles staged by LDS-DMA (global_load_lds_dwordx4: no
+// VGPR round trip, no ds_write), two 64 KiB LDS buffers, one barrier per K-tile.
+// LDS images are lane-linear per wave-instruction (1 KiB), so the bank swizzle
+// is applied to the per-lane *source* address and undone on the read (rule 21).
+namespace big {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int kThreads = 512;
+constexpr int kTileBytes = BM * BK * 2;      // 32 KiB per operand tile
+constexpr int kBufBytes = 2 * kTileBytes;    // A + B
+constexpr int kSmemBytes = 2 * kBufBytes;    // 128 KiB
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// I-contiguous image with 512-byte rows (256 i values).
+__device__ __forceinline__ int ic_off(int r, int c8) { return r * 512 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
+
+template <bool KC>
+__device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t ld, int i0, int k0, char* tile,
+                                      int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int inst = wave * 4 + u;  // 32 x 1 KiB pieces per tile
+    const bf16_t* src;
+    if (KC) {
+      const int row = 8 * inst + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      src = base + (int64_t)(i0 + row) * ld + k0 + 8 * c;
+    } else {
+      const int row = 2 * inst + (lane >> 5);
+      const int c16 = (lane & 31) ^ (ic_rk(row) << 1);
+      src = base + (int64_t)(k0 + row) * ld + i0 + 8 * c16;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(tile + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane) {
+  if (KC) {
+    const int r = ib + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(tile + kc_off(r, c));
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int r0 = 32 * s + 8 * g + q;
+    const int c8 = (ib >> 2) + p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0, c8)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0 + 4, c8)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI, int ACT>
+__global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  int tm, tn;
+  tile_coords(g.M / BM, g.N / BN, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(g.A);
+  const bf16_t* B = reinterpret_cast<const bf16_t*>(g.B);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+  stage<A_KC>(A, g.lda, m0, 0, smem, wave, lane);
+  stage<B_KC>(B, g.ldb, n0, 0, smem + kTileBytes, wave, lane);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // Tile kt has landed (every wave drained its own DMA) and every wave is
+    // done reading the buffer the next prefetch overwrites.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * kBufBytes;
+      stage<A_KC>(A, g.lda, m0, (kt + 1) * BK, nxt, wave, lane);
+      stage<B_KC>(B, g.ldb, n0, (kt + 1) * BK, nxt + kTileBytes, wave, lane);
+    }
+    const char* cur = smem + (kt & 1) * kBufBytes;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bfr[t] = frag<B_KC>(cur + kTileBytes, wn * 64 + 16 * t, s, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 af = frag<A_KC>(cur, wm * 128 + 16 * i, s, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  const int quad = lane >> 4, col_in = lane & 15;
+  const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn * 64 + 16 * j + col_in;
+      const f32x4 v = acc[i][j];
+      if (EPI == kEpiAccumF32) {
+        float* C = reinterpret_cast<float*>(g.C);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(int64_t)(row0 + r) * g.ldc + col] += v[r];
+      } else if (EPI == kEpiStoreF32) {
+        float* C = reinterpret_cast<float*>(g.C);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(int64_t)(row0 + r) * g.ldc + col] = v[r];
+      } else {
+        bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+        const float b = g.bias != nullptr ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
+        float pre[4], out[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pre[r] = v[r] + b;
+          out[r] = ACT == kActRelu ? fmaxf(pre[r], 0.f) : (ACT == kActGelu ? gelu_f(pre[r]) : pre[r]);
+        }
+        if (g.p > 0.f) {
+          const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
+          const uint4 w = Philox(g.seed, sub, g.offset).next4();
+          const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[r] = ws[r] >= g.threshold ? out[r] * pscale : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          C[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out[r]);
+          if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre[r]);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace big
+
+bool use_big(const GemmArgs& g) {
+  return g.M % big::BM == 0 && g.N % big::BN == 0 && (g.M / big::BM) * (g.N / big::BN) >= 128;
+}
+
+template <bool A_KC, bool B_KC, int EPI, int ACT>
+void launch(const GemmArgs& g, hipStream_t s) {
+  if (use_big(g)) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
+      attr_set = true;
+    }
+    const int blocks = (g.M / big::BM) * (g.N / big::BN);
+    hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT>), dim3(blocks), dim3(big::kThreads),
+                       big::kSmemBytes, s, g);
+    return;
+  }
+  const int blocks = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, ACT>), dim3(blocks), dim3(kThreads), kSmemBytes, s, g);
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+void launch_act(const GemmArgs& g, hipStream_t s) {
+  switch (g.act) {
+    case kActRelu: launch<A_KC, B_KC, EPI, kActRelu>(g, s); break;
+    case kActGelu: launch<A_KC, B_KC, EPI, kActGelu>(g, s); break;
+    default: launch<A_KC, B_KC, EPI, kActNone>(g, s); break;
+  }
+}
+
+}  // namespace
+
+bool gemm_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0;
+}
+
+void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
+  GemmArgs g = gi;
+  g.threshold = dropout_threshold(g.p);
+  if (g.epi == kEpiStoreBf16) {
+    if (g.a_kc && g.b_kc) launch_act<true, true, kEpiStoreBf16>(g, s);
+    else if (g.a_kc && !g.b_kc) launch_act<true, false, kEpiStoreBf16>(g, s);
+    else if (!g.a_kc && !g.b_kc) launch_act<false, false, kEpiStoreBf16>(g, s);
+    else launch_act<false, true, kEpiStoreBf16>(g, s);
+  } else if (g.epi == kEpiAccumF32) {
+    if (g.a_kc && g.b_kc) launch<true, true, kEpiAccumF32, kActNone>(g, s);
+    else if (g.a_kc && !g.b_kc) launch<true, false, kEpiAccumF32, kActNone>(g, s);
+    else if (!g.a_kc && !g.b_kc) launch<false, false, kEpiAccumF32, kActNone>(g, s);
+    else launch<false, true, kEpiAccumF32, kActNone>(g, s);
+  } else {
+    if (g.a_kc && g.b_kc) launch<true, true, kEpiStoreF32, kActNone>(g, s);
+    else if (g.a_kc && !g.b_kc) launch<true, false, kEpiStoreF32, kActNone>(g, s);
+    else if (!g.a_kc && !g.b_kc) launch<false, false, kEpiStoreF32, kActNone>(g, s);
+    else launch<false, true, kEpiStoreF32, kActNone>(g, s);
+  }
+}
+
+}  // namespace mipipe

@@ -65,13 +65,35 @@ int colsum_parts(int64_t rows);
 template <typename T>
 void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, T* out, bool accumulate, hipStream_t s);
 
+// ------------------------------------------------------------------ GEMM
+enum GemmEpilogue : int { kEpiStoreBf16 = 0, kEpiAccumF32 = 1, kEpiStoreF32 = 2 };
+
+struct GemmArgs {
+  const void* A = nullptr;  // bf16
+  const void* B = nullptr;  // bf16
+  void* C = nullptr;        // bf16 or fp32 (epilogue)
+  const void* bias = nullptr;  // bf16 [N] (kEpiStoreBf16 only)
+  void* aux = nullptr;         // bf16 pre-activation output (optional)
+  int64_t lda = 0, ldb = 0, ldc = 0;
+  int M = 0, N = 0, K = 0;
+  bool a_kc = true;   // A stored [M, K] (true) or [K, M] (false)
+  bool b_kc = true;   // B stored [N, K] (true) or [K, N] (false)
+  int epi = kEpiStoreBf16;
+  int act = kActNone;
+  float p = 0.f;
+  uint32_t threshold = 0;
+  uint64_t seed = 0, offset = 0;
+};
+bool gemm_supported(int64_t M, int64_t N, int64_t K);
+void gemm_bf16(const GemmArgs& g, hipStream_t s);
+
 // ------------------------------------------------------------------ loss
 template <typename T>
-void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ignore_index,
-                       float* loss, float* lse, hipStream_t s);
+void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
+                       int64_t ignore_index, float* loss, float* lse, hipStream_t s);
 template <typename T>
 void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale, int64_t rows,
-                       int64_t V, int64_t ignore_index, T* dlogits, hipStream_t s);
+                       int64_t V, int64_t ld, int64_t ignore_index, T* dlogits, hipStream_t s);
 
 // ------------------------------------------------------------------ embedding
 template <typename T>

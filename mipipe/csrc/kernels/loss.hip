@@ -18,11 +18,11 @@ constexpr int kT = 256;
 
 template <typename T>
 __global__ void __launch_bounds__(kT) ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
-                                                    int64_t V, int64_t ignore_index, float* __restrict__ loss,
-                                                    float* __restrict__ lse_out) {
+                                                    int64_t V, int64_t ld, int64_t ignore_index,
+                                                    float* __restrict__ loss, float* __restrict__ lse_out) {
   __shared__ float sm[2 * (kT / 64)];
   const int64_t row = blockIdx.x;
-  const T* x = logits + row * V;
+  const T* x = logits + row * ld;
   float m = -INFINITY, s = 0.f;
   for (int64_t c = threadIdx.x; c < V; c += kT) {
     const float v = Io<T>::load(x + c);
@@ -67,9 +67,10 @@ __global__ void __launch_bounds__(kT) ce_fwd_kernel(const T* __restrict__ logits
 template <typename T>
 __global__ void __launch_bounds__(kT) ce_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
                                                     const float* __restrict__ lse_in, const float* __restrict__ scale_p,
-                                                    int64_t V, int64_t ignore_index, T* __restrict__ dlogits) {
+                                                    int64_t V, int64_t ld, int64_t ignore_index,
+                                                    T* __restrict__ dlogits) {
   const int64_t row = blockIdx.x;
-  const T* x = logits + row * V;
+  const T* x = logits + row * ld;
   T* d = dlogits + row * V;
   const int64_t t = target[row];
   const bool valid = !(t == ignore_index || t < 0 || t >= V);
@@ -85,23 +86,24 @@ __global__ void __launch_bounds__(kT) ce_bwd_kernel(const T* __restrict__ logits
 }  // namespace
 
 template <typename T>
-void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ignore_index,
-                       float* loss, float* lse, hipStream_t s) {
+void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
+                       int64_t ignore_index, float* loss, float* lse, hipStream_t s) {
   if (rows == 0) return;
-  hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, V, ignore_index, loss, lse);
+  hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, V, ld, ignore_index,
+                     loss, lse);
 }
 
 template <typename T>
 void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale, int64_t rows,
-                       int64_t V, int64_t ignore_index, T* dlogits, hipStream_t s) {
+                       int64_t V, int64_t ld, int64_t ignore_index, T* dlogits, hipStream_t s) {
   if (rows == 0) return;
-  hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, lse, scale, V,
+  hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, lse, scale, V, ld,
                      ignore_index, dlogits);
 }
 
-template void cross_entropy_fwd<float>(const float*, const int64_t*, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
-template void cross_entropy_fwd<bf16_t>(const bf16_t*, const int64_t*, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
-template void cross_entropy_bwd<float>(const float*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
-template void cross_entropy_bwd<bf16_t>(const bf16_t*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, bf16_t*, hipStream_t);
+template void cross_entropy_fwd<float>(const float*, const int64_t*, int64_t, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
+template void cross_entropy_fwd<bf16_t>(const bf16_t*, const int64_t*, int64_t, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
+template void cross_entropy_bwd<float>(const float*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, int64_t, float*, hipStream_t);
+template void cross_entropy_bwd<bf16_t>(const bf16_t*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, int64_t, bf16_t*, hipStream_t);
 
 }  // namespace mipipe

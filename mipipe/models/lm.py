@@ -86,21 +86,32 @@ class Encoder(nn.Module):
 
 
 class Decoder(nn.Module):
-    """Linear ``E -> V`` (``main.py:42-55``)."""
+    """Linear ``E -> V`` (``main.py:42-55``).
 
-    def __init__(self, ntoken: int, d_model: int, *, device=None, dtype=None) -> None:
+    The weight is stored with the vocabulary padded to a multiple of
+    ``pad_to`` (256: the large GEMM tile) -- zero rows, zero bias -- so the logits
+    GEMM runs on the MFMA tile kernel; ``forward`` returns the ``[..., :V]``
+    view and the fused cross-entropy reads it in place (strided rows).
+    """
+
+    def __init__(self, ntoken: int, d_model: int, *, pad_to: int = 256, device=None, dtype=None) -> None:
         super().__init__()
         fk = {"device": device, "dtype": dtype}
-        self.weight = nn.Parameter(torch.empty(ntoken, d_model, **fk))
-        self.bias = nn.Parameter(torch.zeros(ntoken, **fk))
+        self.ntoken = ntoken
+        self.padded = (ntoken + pad_to - 1) // pad_to * pad_to
+        self.weight = nn.Parameter(torch.empty(self.padded, d_model, **fk))
+        self.bias = nn.Parameter(torch.zeros(self.padded, **fk))
         self.reset_parameters()
 
     def reset_parameters(self) -> None:
-        nn.init.uniform_(self.weight, -0.1, 0.1)  # main.py:47-50
-        nn.init.zeros_(self.bias)
+        with torch.no_grad():
+            nn.init.uniform_(self.weight, -0.1, 0.1)  # main.py:47-50
+            self.weight[self.ntoken:].zero_()
+            nn.init.zeros_(self.bias)
 
     def forward(self, x: Tensor) -> Tensor:
-        return ops.linear(x, self.weight, self.bias)
+        y = ops.linear(x, self.weight, self.bias)
+        return y[..., : self.ntoken] if self.padded != self.ntoken else y
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2.0 * self.weight.shape[0] * self.weight.shape[1]

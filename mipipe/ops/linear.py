@@ -1,12 +1,18 @@
-"""Linear layers: GEMM + fused bias / activation / dropout epilogue.
+"""Linear layers on the MFMA GEMM (csrc/kernels/gemm.hip) with fused epilogues.
 
-Forward:  ``y = dropout(act(x @ W^T + b))``.
-Backward: the epilogue's backward is one fused elementwise pass
-(csrc/kernels/elementwise.hip) that also yields ``db``; then
-``dx = dpre @ W`` and ``dW = dpre^T @ x``.  When the weight carries a
-``main_grad`` fp32 buffer (flat-buffer optimizer, :mod:`mipipe.optim`) ``dW``
-is accumulated there in fp32 and autograd receives no weight gradient, so
-micro-batch gradient accumulation never rounds through bf16.
+Forward:  ``y = dropout(act(x @ W^T + b))`` -- one GEMM launch; bias,
+          activation and dropout live in the epilogue (GELU also writes its
+          pre-activation for backward).
+Backward: the activation/dropout backward is one elementwise pass
+          (csrc/kernels/elementwise.hip, same Philox mask layout as the
+          epilogue) that also yields ``db``; then ``dx = dpre @ W`` (GEMM with a
+          transposing LDS read of W) and ``dW += dpre^T @ x`` accumulated in
+          fp32 straight into ``weight.main_grad`` when the flat optimizer owns
+          the parameter, so micro-batch accumulation never rounds to bf16.
+
+Shapes the tile kernel does not cover (dims not multiples of 128/64) and
+non-bf16 GPU tensors run the plain GEMM through hipBLASLt (torch.matmul) with
+the same fused elementwise kernels.
 """
 from __future__ import annotations
 
@@ -19,65 +25,77 @@ from torch import Tensor
 from ._util import native_or_none
 from .activation import ACTIVATIONS, bias_act_reference
 
-__all__ = ["linear", "accumulate_wgrad"]
-
-_MIXED_ADDMM: Optional[bool] = None
+__all__ = ["linear"]
 
 
-def accumulate_wgrad(main_grad: Tensor, dy2d: Tensor, x2d: Tensor) -> None:
-    """``main_grad (fp32) += dy2d^T @ x2d`` with bf16 operands."""
-    global _MIXED_ADDMM
-    if _MIXED_ADDMM is None or _MIXED_ADDMM:
-        try:
-            torch.addmm(main_grad, dy2d.t(), x2d, out_dtype=torch.float32, out=main_grad)
-            _MIXED_ADDMM = True
-            return
-        except (RuntimeError, TypeError):
-            _MIXED_ADDMM = False
-    main_grad.add_(torch.matmul(dy2d.t(), x2d).float())
+def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
+    return (
+        x2.dtype == torch.bfloat16
+        and weight.dtype == torch.bfloat16
+        and k.gemm_supported(x2.shape[0], weight.shape[0], weight.shape[1])
+    )
 
 
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act, p):  # type: ignore[override]
         k = native_or_none(x)
-        y = torch.matmul(x, weight.t())
-        fused = act != 0 or p > 0.0
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        w = weight.contiguous()
+        fused_tile = _tile_ok(k, x2, w)
         seed = offset = 0
-        if fused:
-            pre = y
-            y, seed, offset = k.bias_act_fwd(pre, bias, act, p)
-            saved = pre if act == 2 else y
+        preact = None
+        if fused_tile:
+            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2)
         else:
-            if bias is not None:
-                y = y + bias
-            saved = None
-        ctx.save_for_backward(x, weight, bias, saved)
-        ctx.act, ctx.p, ctx.seed, ctx.offset, ctx.fused = act, p, seed, offset, fused
-        return y
+            y = torch.matmul(x2, w.t())
+            if act != 0 or p > 0.0 or bias is not None:
+                pre_bias = y
+                y, seed, offset = k.bias_act_fwd(y.contiguous(), bias, act, p)
+                if act == 2:
+                    preact = pre_bias  # pre-BIAS; backward adds the bias back
+        saved = preact if act == 2 else (y if act == 1 else None)
+        ctx.save_for_backward(x2, w, bias, saved)
+        ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
+        ctx.fused_tile = fused_tile
+        ctx.in_shape = shape
+        return y.view(*shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):  # type: ignore[override]
-        x, weight, bias, saved = ctx.saved_tensors
+        x2, w, bias, saved = ctx.saved_tensors
         k = native_or_none(dy)
-        dy = dy.contiguous()
+        d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
-        if ctx.fused:
-            dpre, db = k.bias_act_bwd(dy, saved, bias, ctx.act, ctx.p, ctx.seed, ctx.offset, need_db)
+        act, p = ctx.act, ctx.p
+        if act != 0 or p > 0.0:
+            # GEMM-saved GELU pre-activation already includes the bias.
+            bias_for_bwd = None if ctx.fused_tile else bias
+            dpre, db = k.bias_act_bwd(d2, saved if saved is not None else d2, bias_for_bwd, act, p,
+                                      ctx.seed, ctx.offset, need_db)
         else:
-            dpre = dy
-            db = k.column_sum(dy.view(-1, dy.shape[-1])) if need_db else None
-        dx = torch.matmul(dpre, weight) if ctx.needs_input_grad[0] else None
+            dpre = d2
+            db = k.column_sum(d2) if need_db else None
+
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.fused_tile:
+                dx = k.linear_dgrad(dpre, w)
+            else:
+                dx = torch.matmul(dpre, w)
+            dx = dx.view(ctx.in_shape)
+
         dw = None
         if ctx.needs_input_grad[1]:
-            d2 = dpre.reshape(-1, dpre.shape[-1])
-            x2 = x.reshape(-1, x.shape[-1])
-            main = getattr(weight, "main_grad", None)
-            if main is not None:
-                accumulate_wgrad(main, d2, x2)
+            main = getattr(w, "main_grad", None)
+            if main is not None and ctx.fused_tile:
+                k.linear_wgrad(dpre, x2, main)
+            elif main is not None:
+                main.add_(torch.matmul(dpre.t(), x2).float())
             else:
-                dw = torch.matmul(d2.t(), x2)
-        if db is not None and bias is not None:
+                dw = torch.matmul(dpre.t(), x2)
+        if db is not None:
             main_b = getattr(bias, "main_grad", None)
             if main_b is not None:
                 main_b.add_(db)

@@ -19,7 +19,7 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, ignore_index):  # type: ignore[override]
         k = native_or_none(logits)
-        lc = logits.contiguous()
+        lc = logits if (logits.dim() == 2 and logits.stride(1) == 1) else logits.contiguous()
         loss_rows, lse = k.cross_entropy_fwd(lc, target.contiguous(), ignore_index)
         count = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
         ctx.save_for_backward(lc, target, lse, count)
@@ -34,9 +34,23 @@ class _CrossEntropy(torch.autograd.Function):
         return k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index), None, None
 
 
+def _rows_uniform(t: Tensor) -> bool:
+    """True if all leading dims collapse to one row stride (e.g. a [B, S, :V] slice of [B, S, Vpad])."""
+    stride = t.stride(-2)
+    expect = stride
+    for size, st in zip(reversed(t.shape[:-1]), reversed(t.stride()[:-1])):
+        if size != 1 and st != expect:
+            return False
+        expect = st * size
+    return True
+
+
 def cross_entropy(logits: Tensor, target: Tensor, ignore_index: int = -100) -> Tensor:
     if logits.dim() != 2:
-        logits = logits.reshape(-1, logits.shape[-1])
+        # keeps a padded-vocabulary view strided (no copy)
+        lead = logits.shape[:-1].numel()
+        logits = logits.as_strided((lead, logits.shape[-1]), (logits.stride(-2), 1)) \
+            if logits.stride(-1) == 1 and _rows_uniform(logits) else logits.reshape(-1, logits.shape[-1])
     target = target.reshape(-1)
     if not logits.is_cuda:
         return F.cross_entropy(logits.float(), target, ignore_index=ignore_index)

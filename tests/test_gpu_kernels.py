@@ -317,3 +317,65 @@ def test_engine_one_gpu_step(k):
     assert all(l == l for l in losses)
     assert losses[-1] < losses[0]  # it learns the fixed batch
     assert st.busy_ms > 0
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (512, 256, 1024), (2048, 4096, 256), (4096, 2048, 128)])
+def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
+    torch.manual_seed(1)
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    # asymmetric, non-trivial operands (A = I style checks hide transposes)
+    a_store = a if a_kc else a.t().contiguous()
+    b_store = b.t().contiguous() if b_kc else b
+    c = k.gemm_f32(a_store, b_store, a_kc, b_kc)
+    ref = a.float() @ b.float()
+    err = (c - ref).abs().max().item()
+    assert err < 1e-2 * math.sqrt(K / 64), err
+
+
+def test_linear_op_matches_reference(k):
+    from mipipe.ops import linear
+
+    torch.manual_seed(2)
+    T, K, N = 256, 512, 384
+    for act in (None, "relu", "gelu"):
+        x = torch.randn(2, T // 2, K, device=DEV).to(torch.bfloat16).requires_grad_()
+        w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16).requires_grad_()
+        b = torch.randn(N, device=DEV).to(torch.bfloat16).requires_grad_()
+        y = linear(x, w, b, act, 0.0, True)
+        xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+        ref = xf @ wf.t() + bf
+        ref = torch.relu(ref) if act == "relu" else (F.gelu(ref) if act == "gelu" else ref)
+        assert torch.allclose(y.float(), ref, atol=3e-2, rtol=3e-2), act
+        g = torch.randn_like(ref)
+        y.backward(g.to(torch.bfloat16))
+        ref.backward(g)
+        assert torch.allclose(x.grad.float(), xf.grad, atol=6e-2, rtol=5e-2), act
+        assert torch.allclose(w.grad.float(), wf.grad, atol=2e-1, rtol=5e-2), act
+        assert torch.allclose(b.grad.float(), bf.grad, atol=2e-1, rtol=5e-2), act
+
+
+def test_linear_dropout_mask_and_main_grad(k):
+    from mipipe.ops import linear
+
+    torch.manual_seed(3)
+    T, K, N, p = 256, 256, 256, 0.4
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / 16).to(torch.bfloat16).requires_grad_()
+    w.main_grad = torch.zeros(N, K, device=DEV)
+    y = linear(x, w, None, None, p, True)
+    keep = (y != 0).float()
+    assert abs(keep.mean().item() - (1 - p)) < 0.02
+    g = torch.randn(T, N, device=DEV)
+    y.backward(g.to(torch.bfloat16))
+    assert w.grad is None  # accumulated in main_grad instead
+    expect = ((g.to(torch.bfloat16).float() * keep / (1 - p)).t() @ x.float())
+    assert torch.allclose(w.main_grad, expect, atol=2e-1, rtol=3e-2)
+    # second micro-batch accumulates
+    y2 = linear(x, w, None, None, p, True)
+    y2.backward(g.to(torch.bfloat16))
+    keep2 = (y2 != 0).float()
+    expect2 = expect + ((g.to(torch.bfloat16).float() * keep2 / (1 - p)).t() @ x.float())
+    assert torch.allclose(w.main_grad, expect2, atol=3e-1, rtol=3e-2)

@@ -1,0 +1,56 @@
+"""Interleaved GEMM timing: mipipe MFMA kernel vs hipBLASLt (torch.matmul), one process.
+
+    python tools/bench_gemm.py > profiles/gemm_bench.txt
+"""
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+from mipipe._native_loader import kernels  # noqa: E402
+
+k = kernels()
+dev = "cuda"
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+def main(T=int(sys.argv[1]) if len(sys.argv) > 1 else 4096):
+
+    shapes = [("qkv fwd", T, 12288, 4096), ("out fwd", T, 4096, 4096), ("ffn fwd", T, 4096, 4096),
+              ("dec fwd", T, 28928, 4096)]
+    print(f"{'case':12s} {'M':>6s} {'N':>6s} {'K':>6s} | {'mipipe ms':>9s} {'TF/s':>7s} | {'hipBLASLt ms':>12s} {'TF/s':>7s}")
+    for name, M, N, K in shapes:
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        fl = 2.0 * M * N * K
+        t_m = timeit(lambda: k.linear_fwd(x, w, None, 0, 0.0, False))
+        t_h = timeit(lambda: torch.matmul(x, w.t()))
+        print(f"{name:12s} {M:6d} {N:6d} {K:6d} | {t_m:9.3f} {fl / t_m / 1e9:7.0f} | {t_h:12.3f} {fl / t_h / 1e9:7.0f}")
+        dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        t_m = timeit(lambda: k.linear_dgrad(dy, w))
+        t_h = timeit(lambda: torch.matmul(dy, w))
+        print(f"{name[:3]+' dgrad':12s} {M:6d} {K:6d} {N:6d} | {t_m:9.3f} {fl / t_m / 1e9:7.0f} | {t_h:12.3f} {fl / t_h / 1e9:7.0f}")
+        mg = torch.zeros(N, K, device=dev)
+        t_m = timeit(lambda: k.linear_wgrad(dy, x, mg))
+        t_h = timeit(lambda: mg.add_(torch.matmul(dy.t(), x)))
+        print(f"{name[:3]+' wgrad+acc':12s} {N:6d} {K:6d} {M:6d} | {t_m:9.3f} {fl / t_m / 1e9:7.0f} | {t_h:12.3f} {fl / t_h / 1e9:7.0f}")
+
+
+if __name__ == "__main__":
+    main()
