@@ -126,9 +126,11 @@ std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor, int64_t, int64_t> py_l
   return {y, z, mean, rstd, (int64_t)seed, (int64_t)offset};
 }
 
-std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor> py_layernorm_bwd(Tensor dy, Tensor z, Tensor mean,
-                                                                          Tensor rstd, Tensor gamma, double p,
-                                                                          int64_t seed, int64_t offset) {
+// With acc_gamma/acc_beta (fp32 main_grad views) the parameter gradients are
+// accumulated there and None is returned for them.
+std::tuple<Tensor, std::optional<Tensor>, std::optional<Tensor>, std::optional<Tensor>> py_layernorm_bwd(
+    Tensor dy, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double p, int64_t seed, int64_t offset,
+    std::optional<Tensor> acc_gamma, std::optional<Tensor> acc_beta) {
   check_cuda(dy, "dy");
   check_cuda(z, "z");
   check_same(dy, z, "dy", "z");
@@ -142,22 +144,38 @@ std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor> py_layernorm_bwd(Tenso
   auto dz = at::empty_like(dy);
   std::optional<Tensor> dx;
   if (p > 0.0) dx = at::empty_like(dy);
-  auto dgamma = at::empty_like(gamma);
-  auto dbeta = at::empty_like(gamma);
+  const bool acc = acc_gamma.has_value();
+  MP_CHECK(acc == acc_beta.has_value(), "layernorm_bwd: pass both accumulation targets or neither");
+  if (acc) {
+    for (auto* t : {&*acc_gamma, &*acc_beta}) {
+      MP_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == cols,
+               "layernorm_bwd: accumulation targets must be contiguous fp32 [cols]");
+    }
+  }
+  Tensor dgamma = acc ? *acc_gamma : at::empty_like(gamma);
+  Tensor dbeta = acc ? *acc_beta : at::empty_like(gamma);
   const int nparts = std::max(1, ln_bwd_parts((int)rows));
   auto part = at::empty({2, nparts, cols}, dy.options().dtype(at::kFloat));
   auto s = cur_stream(dy);
+  std::optional<Tensor> rg, rb;
+  if (!acc) {
+    rg = dgamma;
+    rb = dbeta;
+  }
   if (rows == 0) {
-    dgamma.zero_();
-    dbeta.zero_();
-    return {dz, dx, dgamma, dbeta};
+    if (!acc) {
+      dgamma.zero_();
+      dbeta.zero_();
+    }
+    return {dz, dx, rg, rb};
   }
   auto fill = [&](auto& a, auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     a.dy = cptr<T>(dy); a.z = cptr<T>(z); a.mean = cptr<float>(mean); a.rstd = cptr<float>(rstd);
     a.gamma = cptr<T>(gamma); a.dz = ptr<T>(dz); a.dx = dx ? ptr<T>(*dx) : nullptr;
     a.dgamma_part = ptr<float>(part); a.dbeta_part = ptr<float>(part) + (size_t)nparts * cols;
-    a.dgamma = ptr<T>(dgamma); a.dbeta = ptr<T>(dbeta);
+    a.dgamma = dgamma.data_ptr(); a.dbeta = dbeta.data_ptr();
+    a.out_f32 = dgamma.scalar_type() == at::kFloat; a.accumulate = acc;
     a.rows = (int)rows; a.cols = (int)cols; a.nparts = nparts; a.p = (float)p;
     a.seed = (uint64_t)seed; a.offset = (uint64_t)offset;
   };
@@ -172,7 +190,7 @@ std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor> py_layernorm_bwd(Tenso
   } else {
     MP_CHECK(false, "layernorm_bwd: unsupported dtype");
   }
-  return {dz, dx, dgamma, dbeta};
+  return {dz, dx, rg, rb};
 }
 
 // ------------------------------------------------------------------ elementwise
@@ -215,7 +233,7 @@ Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate);
 
 std::tuple<Tensor, std::optional<Tensor>> py_bias_act_bwd(Tensor dy, Tensor saved, std::optional<Tensor> bias,
                                                           int64_t act, double p, int64_t seed, int64_t offset,
-                                                          bool need_dbias) {
+                                                          bool need_dbias, std::optional<Tensor> dbias_acc) {
   check_cuda(dy, "dy");
   check_cuda(saved, "saved");
   check_same(dy, saved, "dy", "saved");
@@ -233,7 +251,11 @@ std::tuple<Tensor, std::optional<Tensor>> py_bias_act_bwd(Tensor dy, Tensor save
                             (float)p, (uint64_t)seed, (uint64_t)offset, s);
   });
   std::optional<Tensor> db;
-  if (need_dbias) db = py_column_sum(dx.view({rows, cols}), std::nullopt, false);
+  if (dbias_acc.has_value()) {
+    py_column_sum(dx.view({rows, cols}), dbias_acc, true);  // fp32 main_grad += colsum
+  } else if (need_dbias) {
+    db = py_column_sum(dx.view({rows, cols}), std::nullopt, false);
+  }
   return {dx, db};
 }
 
@@ -244,14 +266,18 @@ Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate) {
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Tensor o = out.has_value() ? *out : at::empty({cols}, x.options());
   MP_CHECK(o.numel() == cols && o.is_contiguous(), "column_sum: bad out");
-  MP_CHECK(o.scalar_type() == x.scalar_type(), "column_sum: out dtype must match input");
-  if (!out.has_value() && rows == 0) return o.zero_();
+  const bool out_f32 = o.scalar_type() == at::kFloat;
+  MP_CHECK(out_f32 || o.scalar_type() == x.scalar_type(), "column_sum: out must be fp32 or the input dtype");
+  if (rows == 0) {
+    if (!accumulate) o.zero_();
+    return o;
+  }
   const int nparts = colsum_parts(rows);
   auto part = at::empty({nparts, cols}, x.options().dtype(at::kFloat));
   auto s = cur_stream(x);
   dispatch_fb(x, "column_sum", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    column_sum<T>(cptr<T>(x), rows, (int)cols, ptr<float>(part), nparts, ptr<T>(o), accumulate, s);
+    column_sum<T>(cptr<T>(x), rows, (int)cols, ptr<float>(part), nparts, o.data_ptr(), out_f32, accumulate, s);
   });
   return o;
 }
@@ -431,6 +457,66 @@ Tensor py_gemm_f32(Tensor a, Tensor b, bool a_kc, bool b_kc) {
   return c;
 }
 
+// ------------------------------------------------------------------ attention
+// q, k, v: [B, S, H, D] views (unit stride on D, identical strides), bf16.
+void check_bshd(const Tensor& t, const char* name) {
+  MP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
+  MP_CHECK(t.dim() == 4 && t.stride(3) == 1, name, " must be [B, S, H, D] with unit stride on D");
+  MP_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+               reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+           name, ": strides must keep 16-byte alignment");
+}
+
+void fill_qkv(AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
+  check_bshd(q, "q");
+  check_bshd(k, "k");
+  check_bshd(v, "v");
+  MP_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes(), "attention: q, k, v shapes differ");
+  MP_CHECK(q.strides() == k.strides() && q.strides() == v.strides(), "attention: q, k, v strides differ");
+  a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr();
+  a.B = (int)q.size(0); a.S = (int)q.size(1); a.H = (int)q.size(2); a.D = (int)q.size(3);
+  a.sb_qkv = q.stride(0); a.ld_qkv = q.stride(1); a.sh_qkv = q.stride(2);
+  MP_CHECK(attention_supported(a.S, a.D), "attention: unsupported S=", a.S, " D=", a.D,
+           " (S % 64 == 0, D in {64,128,256})");
+}
+
+std::tuple<Tensor, Tensor, int64_t, int64_t> py_attention_fwd(Tensor q, Tensor k, Tensor v, bool causal, double p,
+                                                              double scale) {
+  AttnArgs a;
+  fill_qkv(a, q, k, v);
+  MP_CHECK(p >= 0.0 && p < 1.0, "attention: bad dropout p");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  auto o = at::empty({a.B, a.S, a.H, a.D}, q.options());
+  auto lse = at::empty({a.B, a.H, a.S}, q.options().dtype(at::kFloat));
+  uint64_t seed = 0, offset = 0;
+  if (p > 0.0) std::tie(seed, offset) = philox_draw(q.device(), 4);
+  a.o = o.data_ptr(); a.sb_o = o.stride(0); a.ld_o = o.stride(1); a.sh_o = o.stride(2);
+  a.lse = ptr<float>(lse);
+  a.scale = (float)scale; a.p = (float)p; a.seed = seed; a.offset = offset; a.causal = causal;
+  attention_fwd(a, cur_stream(q));
+  return {o, lse, (int64_t)seed, (int64_t)offset};
+}
+
+void py_attention_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, double p,
+                      double scale, int64_t seed, int64_t offset, Tensor dq, Tensor dk, Tensor dv) {
+  AttnArgs a;
+  fill_qkv(a, q, k, v);
+  check_bshd(o, "o");
+  check_bshd(dout, "dout");
+  MP_CHECK(o.strides() == dout.strides() && o.sizes() == dout.sizes(), "attention_bwd: o/dout layout differs");
+  MP_CHECK(dq.strides() == q.strides() && dk.strides() == q.strides() && dv.strides() == q.strides(),
+           "attention_bwd: gradient buffers must share q's layout");
+  MP_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)a.B * a.H * a.S, "attention_bwd: bad lse");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  auto delta = at::empty({a.B, a.H, a.S}, q.options().dtype(at::kFloat));
+  a.o = o.data_ptr(); a.dout = dout.data_ptr();
+  a.sb_o = o.stride(0); a.ld_o = o.stride(1); a.sh_o = o.stride(2);
+  a.dq = dq.data_ptr(); a.dk = dk.data_ptr(); a.dv = dv.data_ptr();
+  a.lse = ptr<float>(lse); a.delta = ptr<float>(delta);
+  a.scale = (float)scale; a.p = (float)p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset; a.causal = causal;
+  attention_bwd(a, cur_stream(q));
+}
+
 // ------------------------------------------------------------------ optimizer
 Tensor py_sumsq(Tensor g) {
   check_cuda(g, "g");
@@ -494,14 +580,20 @@ PYBIND11_MODULE(_C, m) {
   });
   // kernels
   m.def("layernorm_fwd", &py_layernorm_fwd);
-  m.def("layernorm_bwd", &py_layernorm_bwd);
+  m.def("layernorm_bwd", &py_layernorm_bwd, py::arg("dy"), py::arg("z"), py::arg("mean"), py::arg("rstd"),
+        py::arg("gamma"), py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("acc_gamma") = py::none(),
+        py::arg("acc_beta") = py::none());
   m.def("bias_act_fwd", &py_bias_act_fwd);
-  m.def("bias_act_bwd", &py_bias_act_bwd);
+  m.def("bias_act_bwd", &py_bias_act_bwd, py::arg("dy"), py::arg("saved"), py::arg("bias"), py::arg("act"),
+        py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dbias"), py::arg("dbias_acc") = py::none());
   m.def("column_sum", &py_column_sum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cross_entropy_fwd", &py_ce_fwd);
   m.def("cross_entropy_bwd", &py_ce_bwd);
   m.def("embedding_fwd", &py_embed_fwd);
   m.def("embedding_bwd", &py_embed_bwd);
+  m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });
+  m.def("attention_fwd", &py_attention_fwd);
+  m.def("attention_bwd", &py_attention_bwd);
   m.def("gemm_supported", &py_gemm_supported);
   m.def("linear_fwd", &py_linear_fwd);
   m.def("linear_dgrad", &py_linear_dgrad);

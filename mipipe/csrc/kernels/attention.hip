@@ -1,0 +1,554 @@
+// Flash attention for gfx950: forward, and backward as two kernels (dK/dV and
+// dQ) plus a delta pre-pass.
+//
+// Layout: Q, K, V are read in place from the packed QKV projection output
+// [B, S, 3, H, D] (token stride 3*H*D) and O / dO are [B, S, H, D]; the
+// backward writes dQ, dK, dV straight into the packed dQKV buffer, so no
+// transpose or concatenation ever touches HBM.
+//
+// Tiling: a workgroup = 4 waves = 64 query rows (forward, dQ) or 64 keys
+// (dK/dV), 16 rows per wave on v_mfma_f32_16x16x32_bf16.  The streamed
+// operand tiles (64 x D) are staged into LDS row-major with an XOR chunk
+// swizzle that serves both the 16-byte row reads (ds_read_b128, B operand of
+// Q.K^T / dO.V^T) and the transposing reads (ds_read_b64_tr_b16, B operand of
+// P.V / dS.K / P^T.dO / dS^T.Q) from ONE image (T10 'one image for row reads
+// and transposed reads').  Softmax probabilities take one LDS round trip per
+// tile to move from the accumulator layout to the A-operand layout.
+//
+// Online softmax in fp32 with exp2; causal tiles above the diagonal are
+// skipped entirely; attention dropout uses Philox keyed by (batch*head,
+// query/4, key) -- word (query & 3) -- so forward, dQ and dK/dV regenerate the
+// same mask without storing it.
+#include "common.h"
+#include "kernels.h"
+
+namespace mipipe {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kRows = 64;      // rows per workgroup tile and per streamed tile
+constexpr int kThreads = 256;  // 4 waves
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+struct Img {
+  static constexpr int kRowBytes = 2 * D;
+  static constexpr int kChunks = D / 8;          // 16-byte chunks per row
+  static constexpr int kMask = kChunks >= 16 ? 15 : kChunks - 1;
+  static constexpr int kBytes = kRows * kRowBytes;
+  __device__ static __forceinline__ int f(int r) { return ((((r & 3) << 2) | ((r >> 2) & 3))) & kMask; }
+  __device__ static __forceinline__ int off(int r, int c16) { return r * kRowBytes + ((c16 ^ f(r)) << 4); }
+};
+
+// Stage a 64 x D tile (rows t0.., row stride `ld` elements) into LDS.
+template <int D>
+__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ base, int64_t ld, char* img, int tid) {
+  constexpr int kPer = kRows * Img<D>::kChunks / kThreads;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int id = tid + u * kThreads;
+    const int r = id / Img<D>::kChunks, c = id % Img<D>::kChunks;
+    const uint4 v = *reinterpret_cast<const uint4*>(base + (int64_t)r * ld + c * 8);
+    *reinterpret_cast<uint4*>(img + Img<D>::off(r, c)) = v;
+  }
+}
+
+// B-operand fragment where B[k = d][n = row]: the n index is the image row
+// (16 rows from rb), k = 32 s + 8 (lane >> 4) + j is the column  -> row read.
+template <int D>
+__device__ __forceinline__ bf16x8 frag_rows(const char* img, int rb, int s, int lane) {
+  const int r = rb + (lane & 15);
+  const int c = 4 * s + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(img + Img<D>::off(r, c));
+}
+
+// B-operand fragment where B[k = row][n = d]: k = 32 s + 8 g + j over image
+// rows, n = db + (lane & 15) over columns -> two transposing reads.
+template <int D>
+__device__ __forceinline__ bf16x8 frag_cols(const char* img, int db, int s, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 32 * s + 8 * g + q;
+  const int c8 = (db >> 2) + p;
+  const int o0 = Img<D>::off(r0, c8 >> 1) + 8 * (c8 & 1);
+  const int o1 = Img<D>::off(r0 + 4, c8 >> 1) + 8 * (c8 & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// A-operand fragment straight from global memory: row (lane & 15) of a
+// 16-row slab, k = 32 s + 8 (lane >> 4) + j.
+__device__ __forceinline__ bf16x8 frag_global(const bf16_t* __restrict__ rowp, int s, int lane) {
+  return *reinterpret_cast<const bf16x8*>(rowp + 32 * s + 8 * (lane >> 4));
+}
+
+// Per-wave scratch [16][64] bf16 for accumulator -> A-operand relayout.
+// Row stride 136 bytes (64 + 4 elements) keeps both the scattered 2-byte
+// writes and the 16-byte fragment reads spread over the banks.
+constexpr int kScrStride = 68;  // elements
+__device__ __forceinline__ void scratch_write(bf16_t* scr, const float (&v)[4][4], int lane) {
+  const int rq = 4 * (lane >> 4), c = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[(rq + r) * kScrStride + 16 * j + c] = f2bf(v[j][r]);
+}
+__device__ __forceinline__ bf16x8 scratch_frag(const bf16_t* scr, int s, int lane) {
+  const bf16_t* p = scr + (lane & 15) * kScrStride + 32 * s + 8 * (lane >> 4);
+  // 136-byte rows are 8-byte but not 16-byte aligned: two 8-byte reads.
+  const uint2 a = *reinterpret_cast<const uint2*>(p);
+  const uint2 b = *reinterpret_cast<const uint2*>(p + 4);
+  const uint4 v = make_uint4(a.x, a.y, b.x, b.y);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ uint4 attn_mask_words(const AttnArgs& a, int bh, int q4, int key) {
+  const uint64_t sub = ((uint64_t)bh * (uint64_t)(a.S >> 2) + (uint64_t)q4) * (uint64_t)a.S + (uint64_t)key;
+  return Philox(a.seed, sub, a.offset).next4();
+}
+
+__device__ __forceinline__ float row_reduce_max16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float row_reduce_sum16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------ forward
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + Img<D>::kBytes;
+  bf16_t* scr_all = reinterpret_cast<bf16_t*>(smem + 2 * Img<D>::kBytes);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qt = blockIdx.x;          // query tile
+  const int bh = blockIdx.y;          // batch * head
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qt * kRows;
+  bf16_t* scr = scr_all + wave * 16 * kScrStride;
+
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+
+  // Q fragments of this wave's 16 rows (A operand), kept in registers.
+  constexpr int NS = D / 32;
+  bf16x8 qf[NS];
+  const bf16_t* qrow = Q + (int64_t)(q0 + wave * 16 + (lane & 15)) * a.ld_qkv;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) qf[s] = frag_global(qrow, s, lane);
+
+  constexpr int ND = D / 16;
+  f32x4 o[ND];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  const int qrow0 = q0 + wave * 16 + 4 * (lane >> 4);  // this lane's rows qrow0 .. +3
+  const int ntiles = CAUSAL ? qt + 1 : a.S / kRows;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * kRows;
+    __syncthreads();
+    stage_tile<D>(K + (int64_t)k0 * a.ld_qkv, a.ld_qkv, kimg, tid);
+    stage_tile<D>(V + (int64_t)k0 * a.ld_qkv, a.ld_qkv, vimg, tid);
+    __syncthreads();
+
+    f32x4 sacc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], frag_rows<D>(kimg, 16 * j, s, lane), sacc[j], 0, 0, 0);
+
+    // online softmax (log2 domain)
+    float sv[4][4];
+    float tmax[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = k0 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = sacc[j][r] * sl2;
+        if (CAUSAL && key > qrow0 + r) x = -INFINITY;
+        sv[j][r] = x;
+        tmax[r] = fmaxf(tmax[r], x);
+      }
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float mx = row_reduce_max16(tmax[r]);
+      const float mn = fmaxf(m[r], mx);
+      alpha[r] = m[r] == -INFINITY ? 0.f : exp2f(m[r] - mn);
+      m[r] = mn;
+    }
+    float psum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      if (a.p > 0.f) {
+        const uint4 mw = attn_mask_words(a, bh, qrow0 >> 2, k0 + 16 * j + (lane & 15));
+        w[0] = mw.x; w[1] = mw.y; w[2] = mw.z; w[3] = mw.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pr = m[r] == -INFINITY ? 0.f : exp2f(sv[j][r] - m[r]);
+        psum[r] += pr;
+        sv[j][r] = (a.p > 0.f) ? (w[r] >= a.threshold ? pr * pscale : 0.f) : pr;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) l[r] = l[r] * alpha[r] + row_reduce_sum16(psum[r]);
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[t2][r] *= alpha[r];
+
+    scratch_write(scr, sv, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's scratch writes done
+    const bf16x8 p0 = scratch_frag(scr, 0, lane);
+    const bf16x8 p1 = scratch_frag(scr, 1, lane);
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2) {
+      o[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(p0, frag_cols<D>(vimg, 16 * t2, 0, lane), o[t2], 0, 0, 0);
+      o[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(p1, frag_cols<D>(vimg, 16 * t2, 1, lane), o[t2], 0, 0, 0);
+    }
+  }
+
+  // epilogue: O / l (bf16) and lse (natural log) per row
+  bf16_t* O = reinterpret_cast<bf16_t*>(a.o) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+  float inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) inv[r] = l[r] > 0.f ? 1.f / l[r] : 0.f;
+#pragma unroll
+  for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      O[(int64_t)(qrow0 + r) * a.ld_o + 16 * t2 + (lane & 15)] = f2bf(o[t2][r] * inv[r]);
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      a.lse[(int64_t)bh * a.S + qrow0 + r] = (m[r] + log2f(l[r] > 0.f ? l[r] : 1.f)) / kLog2e;
+  }
+}
+
+// ------------------------------------------------------------------ delta = rowsum(dO * O)
+__global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a, int D) {
+  // one wave per (b, s, h) row
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t total = (int64_t)a.B * a.S * a.H;
+  if (row >= total) return;
+  const int h = (int)(row % a.H);
+  const int64_t bs = row / a.H;  // b * S + s
+  const int64_t ob = (bs / a.S) * a.sb_o + (bs % a.S) * a.ld_o + (int64_t)h * a.sh_o;
+  const bf16_t* o = reinterpret_cast<const bf16_t*>(a.o) + ob;
+  const bf16_t* d = reinterpret_cast<const bf16_t*>(a.dout) + ob;
+  float acc = 0.f;
+  for (int c = lane * 4; c < D; c += 256) {
+    const u16x4 ov = *reinterpret_cast<const u16x4*>(o + c);
+    const u16x4 dv = *reinterpret_cast<const u16x4*>(d + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc += bf2f(ov[i]) * bf2f(dv[i]);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const int b = (int)(bs / a.S), s = (int)(bs % a.S);
+    a.delta[((int64_t)b * a.H + h) * a.S + s] = acc;
+  }
+}
+
+// ------------------------------------------------------------------ dQ
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_dq_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + Img<D>::kBytes;
+  bf16_t* scr_all = reinterpret_cast<bf16_t*>(smem + 2 * Img<D>::kBytes);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qt = blockIdx.x, bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qt * kRows;
+  bf16_t* scr = scr_all + wave * 16 * kScrStride;
+  const int64_t boff = (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + boff;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + boff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + boff;
+  const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+
+  constexpr int NS = D / 32, ND = D / 16;
+  bf16x8 qf[NS], df[NS];
+  const int myrow = q0 + wave * 16 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    qf[s] = frag_global(Q + (int64_t)myrow * a.ld_qkv, s, lane);
+    df[s] = frag_global(dO + (int64_t)myrow * a.ld_o, s, lane);
+  }
+  const int qrow0 = q0 + wave * 16 + 4 * (lane >> 4);
+  float lse2[4], dl[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    lse2[r] = a.lse[(int64_t)bh * a.S + qrow0 + r] * kLog2e;
+    dl[r] = a.delta[(int64_t)bh * a.S + qrow0 + r];
+  }
+  f32x4 dq[ND];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  const int ntiles = CAUSAL ? qt + 1 : a.S / kRows;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * kRows;
+    __syncthreads();
+    stage_tile<D>(K + (int64_t)k0 * a.ld_qkv, a.ld_qkv, kimg, tid);
+    stage_tile<D>(V + (int64_t)k0 * a.ld_qkv, a.ld_qkv, vimg, tid);
+    __syncthreads();
+    f32x4 sacc[4], pacc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sacc[j] = pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], frag_rows<D>(kimg, 16 * j, s, lane), sacc[j], 0, 0, 0);
+        pacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[s], frag_rows<D>(vimg, 16 * j, s, lane), pacc[j], 0, 0, 0);
+      }
+    float ds[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = k0 + 16 * j + (lane & 15);
+      uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      if (a.p > 0.f) {
+        const uint4 mw = attn_mask_words(a, bh, qrow0 >> 2, key);
+        w[0] = mw.x; w[1] = mw.y; w[2] = mw.z; w[3] = mw.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pr = exp2f(sacc[j][r] * sl2 - lse2[r]);
+        if (CAUSAL && key > qrow0 + r) pr = 0.f;
+        float dp = pacc[j][r];
+        if (a.p > 0.f) dp = w[r] >= a.threshold ? dp * pscale : 0.f;
+        ds[j][r] = pr * (dp - dl[r]);
+      }
+    }
+    scratch_write(scr, ds, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const bf16x8 s0 = scratch_frag(scr, 0, lane);
+    const bf16x8 s1 = scratch_frag(scr, 1, lane);
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2) {
+      dq[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(s0, frag_cols<D>(kimg, 16 * t2, 0, lane), dq[t2], 0, 0, 0);
+      dq[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(s1, frag_cols<D>(kimg, 16 * t2, 1, lane), dq[t2], 0, 0, 0);
+    }
+  }
+  bf16_t* dQ = reinterpret_cast<bf16_t*>(a.dq) + boff;
+#pragma unroll
+  for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      dQ[(int64_t)(qrow0 + r) * a.ld_qkv + 16 * t2 + (lane & 15)] = f2bf(dq[t2][r] * a.scale);
+}
+
+// ------------------------------------------------------------------ dK, dV
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, D >= 128 ? 1 : 2) attn_dkdv_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* qimg = smem;
+  char* dimg = smem + Img<D>::kBytes;
+  bf16_t* scr_all = reinterpret_cast<bf16_t*>(smem + 2 * Img<D>::kBytes);
+  float* stats = reinterpret_cast<float*>(smem + 2 * Img<D>::kBytes + 4 * 16 * kScrStride * 2);  // lse2[64], delta[64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kt = blockIdx.x, bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int k0 = kt * kRows;
+  bf16_t* scr = scr_all + wave * 16 * kScrStride;
+  const int64_t boff = (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + boff;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + boff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + boff;
+  const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+
+  constexpr int NS = D / 32, ND = D / 16;
+  bf16x8 kf[NS], vf[NS];
+  const int mykey = k0 + wave * 16 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    kf[s] = frag_global(K + (int64_t)mykey * a.ld_qkv, s, lane);
+    vf[s] = frag_global(V + (int64_t)mykey * a.ld_qkv, s, lane);
+  }
+  const int key0 = k0 + wave * 16 + 4 * (lane >> 4);  // this lane's keys key0 .. +3 (rows of S^T)
+  f32x4 dk[ND], dv[ND];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) dk[t] = dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  const int first = CAUSAL ? kt : 0;
+  const int nq = a.S / kRows;
+
+  for (int t = first; t < nq; ++t) {
+    const int q0 = t * kRows;
+    __syncthreads();
+    stage_tile<D>(Q + (int64_t)q0 * a.ld_qkv, a.ld_qkv, qimg, tid);
+    stage_tile<D>(dO + (int64_t)q0 * a.ld_o, a.ld_o, dimg, tid);
+    if (tid < 64) {
+      stats[tid] = a.lse[(int64_t)bh * a.S + q0 + tid] * kLog2e;
+      stats[64 + tid] = a.delta[(int64_t)bh * a.S + q0 + tid];
+    }
+    __syncthreads();
+    f32x4 sacc[4], pacc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sacc[j] = pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], frag_rows<D>(qimg, 16 * j, s, lane), sacc[j], 0, 0, 0);
+        pacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s], frag_rows<D>(dimg, 16 * j, s, lane), pacc[j], 0, 0, 0);
+      }
+    // S^T[key][q]: lane holds keys key0 + r, query q = q0 + 16 j + (lane & 15)
+    float pd[4][4], ds[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ql = 16 * j + (lane & 15);
+      const int q = q0 + ql;
+      const float l2 = stats[ql], dl = stats[64 + ql];
+      uint32_t w = 0xFFFFFFFFu;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = key0 + r;
+        float pr = exp2f(sacc[j][r] * sl2 - l2);
+        if (CAUSAL && key > q) pr = 0.f;
+        float dp = pacc[j][r];
+        float pdrop = pr;
+        if (a.p > 0.f) {
+          const uint4 mw = attn_mask_words(a, bh, q >> 2, key);
+          const uint32_t ws[4] = {mw.x, mw.y, mw.z, mw.w};
+          w = ws[q & 3];
+          const bool keep = w >= a.threshold;
+          pdrop = keep ? pr * pscale : 0.f;
+          dp = keep ? dp * pscale : 0.f;
+        }
+        pd[j][r] = pdrop;
+        ds[j][r] = pr * (dp - dl);
+      }
+    }
+    scratch_write(scr, pd, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    bf16x8 f0 = scratch_frag(scr, 0, lane);
+    bf16x8 f1 = scratch_frag(scr, 1, lane);
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2) {
+      dv[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0, frag_cols<D>(dimg, 16 * t2, 0, lane), dv[t2], 0, 0, 0);
+      dv[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1, frag_cols<D>(dimg, 16 * t2, 1, lane), dv[t2], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    scratch_write(scr, ds, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    f0 = scratch_frag(scr, 0, lane);
+    f1 = scratch_frag(scr, 1, lane);
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2) {
+      dk[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0, frag_cols<D>(qimg, 16 * t2, 0, lane), dk[t2], 0, 0, 0);
+      dk[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1, frag_cols<D>(qimg, 16 * t2, 1, lane), dk[t2], 0, 0, 0);
+    }
+  }
+  bf16_t* dK = reinterpret_cast<bf16_t*>(a.dk) + boff;
+  bf16_t* dV = reinterpret_cast<bf16_t*>(a.dv) + boff;
+#pragma unroll
+  for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t o = (int64_t)(key0 + r) * a.ld_qkv + 16 * t2 + (lane & 15);
+      dK[o] = f2bf(dk[t2][r] * a.scale);
+      dV[o] = f2bf(dv[t2][r]);
+    }
+}
+
+template <int D>
+size_t fwd_smem() { return 2 * Img<D>::kBytes + 4 * 16 * kScrStride * 2; }
+template <int D>
+size_t dkdv_smem() { return fwd_smem<D>() + 128 * sizeof(float); }
+
+template <typename Kern>
+void set_smem(Kern k, size_t bytes) {
+  hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <int D, bool CAUSAL>
+void run_fwd(const AttnArgs& a, hipStream_t s) {
+  const size_t sm = fwd_smem<D>();
+  static bool once = false;
+  if (!once) { set_smem(attn_fwd_kernel<D, CAUSAL>, sm); once = true; }
+  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL>), dim3(a.S / kRows, a.B * a.H), dim3(kThreads), sm, s, a);
+}
+
+template <int D, bool CAUSAL>
+void run_bwd(const AttnArgs& a, hipStream_t s) {
+  const size_t sm = fwd_smem<D>(), sm2 = dkdv_smem<D>();
+  static bool once = false;
+  if (!once) {
+    set_smem(attn_dq_kernel<D, CAUSAL>, sm);
+    set_smem(attn_dkdv_kernel<D, CAUSAL>, sm2);
+    once = true;
+  }
+  const int64_t rows = (int64_t)a.B * a.S * a.H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, D);
+  hipLaunchKernelGGL((attn_dkdv_kernel<D, CAUSAL>), dim3(a.S / kRows, a.B * a.H), dim3(kThreads), sm2, s, a);
+  hipLaunchKernelGGL((attn_dq_kernel<D, CAUSAL>), dim3(a.S / kRows, a.B * a.H), dim3(kThreads), sm, s, a);
+}
+
+}  // namespace
+
+bool attention_supported(int S, int D) { return S > 0 && S % kRows == 0 && (D == 64 || D == 128 || D == 256); }
+
+void attention_fwd(const AttnArgs& ai, hipStream_t s) {
+  AttnArgs a = ai;
+  a.threshold = dropout_threshold(a.p);
+  if (a.causal) {
+    if (a.D == 64) run_fwd<64, true>(a, s);
+    else if (a.D == 128) run_fwd<128, true>(a, s);
+    else run_fwd<256, true>(a, s);
+  } else {
+    if (a.D == 64) run_fwd<64, false>(a, s);
+    else if (a.D == 128) run_fwd<128, false>(a, s);
+    else run_fwd<256, false>(a, s);
+  }
+}
+
+void attention_bwd(const AttnArgs& ai, hipStream_t s) {
+  AttnArgs a = ai;
+  a.threshold = dropout_threshold(a.p);
+  if (a.causal) {
+    if (a.D == 64) run_bwd<64, true>(a, s);
+    else if (a.D == 128) run_bwd<128, true>(a, s);
+    else run_bwd<256, true>(a, s);
+  } else {
+    if (a.D == 64) run_bwd<64, false>(a, s);
+    else if (a.D == 128) run_bwd<128, false>(a, s);
+    else run_bwd<256, false>(a, s);
+  }
+}
+
+}  // namespace mipipe

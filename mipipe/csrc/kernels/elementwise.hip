@@ -124,16 +124,6 @@ __global__ void __launch_bounds__(256) colsum_part_scalar_kernel(const T* __rest
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ part, int nparts, int cols,
-                                                           T* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float a = accumulate ? Io<T>::load(out + c) : 0.f;
-  for (int r = 0; r < nparts; ++r) a += part[(size_t)r * cols + c];
-  Io<T>::store(out + c, a);
-}
-
 int64_t grid_for(int64_t nvec) {
   int64_t g = (nvec + 255) / 256;
   return g < 2048 ? (g < 1 ? 1 : g) : 2048;
@@ -174,7 +164,8 @@ int colsum_parts(int64_t rows) {
 }
 
 template <typename T>
-void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, T* out, bool accumulate, hipStream_t s) {
+void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, void* out, bool out_f32, bool accumulate,
+                hipStream_t s) {
   if (rows == 0 || cols == 0) return;
   const int rows_per = (int)((rows + nparts - 1) / nparts);
   if (cols % 8 == 0) {
@@ -185,15 +176,14 @@ void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, T* 
     dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);
     hipLaunchKernelGGL((colsum_part_scalar_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
   }
-  hipLaunchKernelGGL((colsum_final_kernel<T>), dim3((cols + 255) / 256), dim3(256), 0, s, part, nparts, cols, out,
-                     accumulate ? 1 : 0);
+  reduce_parts(part, nullptr, nparts, cols, out, nullptr, out_f32, accumulate, s);
 }
 
 template void bias_act_dropout_fwd<float>(const float*, const float*, float*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
 template void bias_act_dropout_fwd<bf16_t>(const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
 template void bias_act_dropout_bwd<float>(const float*, const float*, const float*, float*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
 template void bias_act_dropout_bwd<bf16_t>(const bf16_t*, const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
-template void column_sum<float>(const float*, int64_t, int, float*, int, float*, bool, hipStream_t);
-template void column_sum<bf16_t>(const bf16_t*, int64_t, int, float*, int, bf16_t*, bool, hipStream_t);
+template void column_sum<float>(const float*, int64_t, int, float*, int, void*, bool, bool, hipStream_t);
+template void column_sum<bf16_t>(const bf16_t*, int64_t, int, float*, int, void*, bool, bool, hipStream_t);
 
 }  // namespace mipipe

@@ -40,12 +40,18 @@ struct LnBwdArgs {
   T* dx = nullptr;           // grad of the dropout branch (nullptr if p == 0)
   float* dgamma_part = nullptr;  // [nparts, cols] workspace
   float* dbeta_part = nullptr;
-  T* dgamma = nullptr;
-  T* dbeta = nullptr;
+  void* dgamma = nullptr;        // T (store) or fp32 (main_grad, may accumulate)
+  void* dbeta = nullptr;
+  bool out_f32 = false;
+  bool accumulate = false;
   int rows = 0, cols = 0, nparts = 0;
   float p = 0.f;
   uint64_t seed = 0, offset = 0;
 };
+
+// out[c] (=|+=) sum over nparts partial rows; out is fp32 (out_f32) or bf16.
+void reduce_parts(const float* part_a, const float* part_b, int nparts, int cols, void* out_a, void* out_b,
+                  bool out_f32, bool accumulate, hipStream_t s);
 
 int ln_max_vec(int cols);
 int ln_bwd_parts(int rows);
@@ -63,7 +69,8 @@ void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int
                           uint64_t seed, uint64_t offset, hipStream_t s);
 int colsum_parts(int64_t rows);
 template <typename T>
-void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, T* out, bool accumulate, hipStream_t s);
+void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, void* out, bool out_f32, bool accumulate,
+                hipStream_t s);
 
 // ------------------------------------------------------------------ GEMM
 enum GemmEpilogue : int { kEpiStoreBf16 = 0, kEpiAccumF32 = 1, kEpiStoreF32 = 2 };
@@ -86,6 +93,31 @@ struct GemmArgs {
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
+
+// ------------------------------------------------------------------ attention
+struct AttnArgs {
+  const void* q = nullptr;  // bf16, element (b, s, h, d) at b*S*ld_qkv + s*ld_qkv + h*D + d
+  const void* k = nullptr;
+  const void* v = nullptr;
+  void* o = nullptr;        // bf16 [B, S, H, D], token stride ld_o
+  const void* dout = nullptr;
+  void* dq = nullptr;       // same layout as q/k/v (packed dQKV)
+  void* dk = nullptr;
+  void* dv = nullptr;
+  float* lse = nullptr;     // [B, H, S]
+  float* delta = nullptr;   // [B, H, S]
+  int64_t ld_qkv = 0, ld_o = 0;      // token strides (elements)
+  int64_t sb_qkv = 0, sh_qkv = 0;    // batch / head strides of q, k, v (and dq, dk, dv)
+  int64_t sb_o = 0, sh_o = 0;        // batch / head strides of o and dout
+  int B = 0, H = 0, S = 0, D = 0;
+  float scale = 1.f, p = 0.f;
+  uint32_t threshold = 0;
+  uint64_t seed = 0, offset = 0;
+  bool causal = false;
+};
+bool attention_supported(int S, int D);
+void attention_fwd(const AttnArgs& a, hipStream_t s);
+void attention_bwd(const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ loss
 template <typename T>

@@ -174,21 +174,6 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) reduce_cols_kernel(const float* __restrict__ part_a,
-                                                          const float* __restrict__ part_b, int nparts, int cols,
-                                                          T* __restrict__ out_a, T* __restrict__ out_b) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float a = 0.f, b = 0.f;
-  for (int r = 0; r < nparts; ++r) {
-    a += part_a[(size_t)r * cols + c];
-    b += part_b[(size_t)r * cols + c];
-  }
-  Io<T>::store(out_a + c, a);
-  Io<T>::store(out_b + c, b);
-}
-
 template <typename T, int MAXV>
 void launch_fwd(const LnArgs<T>& a, hipStream_t s) {
   hipLaunchKernelGGL((ln_fwd_kernel<T, MAXV>), dim3(a.rows), dim3(kThreads), 0, s, a.x, a.res, a.gamma, a.beta,
@@ -200,8 +185,7 @@ void launch_bwd(const LnBwdArgs<T>& a, hipStream_t s) {
   hipLaunchKernelGGL((ln_bwd_kernel<T, MAXV>), dim3(a.nparts), dim3(kThreads), 0, s, a.dy, a.z, a.mean, a.rstd,
                      a.gamma, a.dz, a.dx, a.dgamma_part, a.dbeta_part, a.rows, a.cols, a.p,
                      dropout_threshold(a.p), a.seed, a.offset);
-  hipLaunchKernelGGL((reduce_cols_kernel<T>), dim3((a.cols + 255) / 256), dim3(256), 0, s, a.dgamma_part,
-                     a.dbeta_part, a.nparts, a.cols, a.dgamma, a.dbeta);
+  reduce_parts(a.dgamma_part, a.dbeta_part, a.nparts, a.cols, a.dgamma, a.dbeta, a.out_f32, a.accumulate, s);
 }
 
 }  // namespace
@@ -215,7 +199,7 @@ int ln_max_vec(int cols) {
   return -1;
 }
 
-int ln_bwd_parts(int rows) { return rows < 512 ? rows : 512; }
+int ln_bwd_parts(int rows) { return rows < 256 ? rows : 256; }
 
 template <typename T>
 void layernorm_fwd(const LnArgs<T>& a, hipStream_t s) {

@@ -75,10 +75,11 @@ class AttentionCore(nn.Module):
         if self.norm_first:
             x = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
         qkv = ops.linear(x, self.in_proj_weight, self.in_proj_bias)
-        # [B, S, 3, H, D] -> 3 x [B, H, S, D]
-        qkv = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
-        o = ops.attention(qkv[0], qkv[1], qkv[2], causal=self.causal, dropout_p=self.dropout, training=self.training)
-        return o.transpose(1, 2).reshape(B, S, E)
+        # The projection output viewed as [B, S, 3, H, D] feeds the kernel in
+        # place; its output [B, S, H, D] is already [B, S, E] -- no transposes.
+        o = ops.attention_packed(qkv.view(B, S, 3, H, D), causal=self.causal, dropout_p=self.dropout,
+                                 training=self.training)
+        return o.reshape(B, S, E)
 
     def flops_per_token(self, seq_len: int) -> float:
         e = self.d_model

@@ -7,7 +7,7 @@ a missing extension raises (``mipipe._native_loader.kernels``).
 """
 from .layernorm import add_dropout_layer_norm, layer_norm_reference
 from .linear import linear
-from .attention import attention, attention_reference
+from .attention import attention, attention_packed, attention_reference
 from .activation import bias_act_dropout
 from .loss import cross_entropy
 from .embedding import embed_scale_posenc_dropout
@@ -17,6 +17,7 @@ __all__ = [
     "layer_norm_reference",
     "linear",
     "attention",
+    "attention_packed",
     "attention_reference",
     "bias_act_dropout",
     "cross_entropy",

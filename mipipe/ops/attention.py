@@ -1,8 +1,18 @@
-"""Scaled dot-product attention (kernel: csrc/kernels/attention.hip).
+"""Scaled dot-product attention on the HIP flash-attention kernels
+(csrc/kernels/attention.hip).
 
-Layout: ``q, k, v`` are ``[B, H, S, D]`` (any strides with unit stride on D
-are made contiguous).  Supports causal masking and attention-probability
-dropout whose mask is regenerated from the Philox (seed, offset) in backward.
+Two entry points:
+
+* :func:`attention_packed` -- ``qkv [B, S, 3, H, D]`` (the QKV projection output
+  viewed in place) -> ``o [B, S, H, D]``.  No transposes: the kernels read Q, K
+  and V with strides and the backward writes one packed ``dqkv`` gradient.
+* :func:`attention` -- the usual ``q, k, v [B, H, S, D]`` API (views are
+  permuted, not copied).
+
+Causal masking and attention dropout are supported; the dropout mask is
+regenerated from Philox (seed, offset) in backward, so checkpoint recompute
+replays it exactly.  Supported on the GPU path: ``S % 64 == 0`` and
+``D in {64, 128, 256}``; the CPU path is eager math.
 """
 from __future__ import annotations
 
@@ -15,11 +25,11 @@ from torch import Tensor
 
 from ._util import native_or_none
 
-__all__ = ["attention", "attention_reference"]
+__all__ = ["attention", "attention_packed", "attention_reference"]
 
 
 def attention_reference(q: Tensor, k: Tensor, v: Tensor, causal: bool, p: float, scale: Optional[float] = None) -> Tensor:
-    """Eager fp32 math (CPU path and test oracle)."""
+    """Eager fp32 math on ``[B, H, S, D]`` (CPU path and test oracle)."""
     d = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(d)
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
@@ -33,11 +43,37 @@ def attention_reference(q: Tensor, k: Tensor, v: Tensor, causal: bool, p: float,
     return torch.matmul(pr, v.float()).to(q.dtype)
 
 
-class _FlashAttention(torch.autograd.Function):
+class _AttentionPacked(torch.autograd.Function):
+    """``qkv [B, S, 3, H, D]`` (contiguous) in, ``o [B, S, H, D]`` out; the
+    backward produces the packed ``dqkv`` in one buffer."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, p, scale):  # type: ignore[override]
+        kern = native_or_none(qkv)
+        q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
+        o, lse, seed, offset = kern.attention_fwd(q, k, v, causal, p, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
+        return o
+
+    @staticmethod
+    def backward(ctx, do):  # type: ignore[override]
+        qkv, o, lse = ctx.saved_tensors
+        kern = native_or_none(do)
+        if do.stride() != o.stride():
+            do = do.contiguous()
+        dqkv = torch.empty_like(qkv)
+        kern.attention_bwd(do, qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2), o, lse, ctx.causal, ctx.p,
+                           ctx.scale, ctx.seed, ctx.offset, dqkv.select(2, 0), dqkv.select(2, 1), dqkv.select(2, 2))
+        return dqkv, None, None, None
+
+
+class _Attention(torch.autograd.Function):
+    """Separate q, k, v as [B, S, H, D] views sharing one layout."""
+
     @staticmethod
     def forward(ctx, q, k, v, causal, p, scale):  # type: ignore[override]
         kern = native_or_none(q)
-        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         o, lse, seed, offset = kern.attention_fwd(q, k, v, causal, p, scale)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
@@ -47,22 +83,63 @@ class _FlashAttention(torch.autograd.Function):
     def backward(ctx, do):  # type: ignore[override]
         q, k, v, o, lse = ctx.saved_tensors
         kern = native_or_none(do)
-        dq, dk, dv = kern.attention_bwd(
-            do.contiguous(), q, k, v, o, lse, ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset
-        )
+        if do.stride() != o.stride():
+            do = do.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        kern.attention_bwd(do, q, k, v, o, lse, ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, dq, dk, dv)
         return dq, dk, dv, None, None, None
+
+
+_noted = set()
+
+
+def _note_math_path(S: int, D: int, dtype) -> None:
+    """fp32 models and shapes outside the kernel's tiling (S % 64, D in
+    {64,128,256}) use the eager math path; say so once per shape."""
+    key = (S, D, dtype)
+    if key not in _noted:
+        _noted.add(key)
+        import warnings
+
+        warnings.warn(f"mipipe attention: S={S} D={D} {dtype} runs the eager math path (HIP kernel: bf16, "
+                      "S % 64 == 0, D in {64, 128, 256})", stacklevel=3)
+
+
+def _gpu_ok(t: Tensor, S: int, D: int) -> bool:
+    return t.dtype == torch.bfloat16 and native_or_none(t).attention_supported(S, D)
+
+
+def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, training: bool = True,
+                     scale: Optional[float] = None) -> Tensor:
+    """``qkv [B, S, 3, H, D]`` -> ``o [B, S, H, D]``."""
+    B, S, three, H, D = qkv.shape
+    assert three == 3
+    p = float(dropout_p) if training else 0.0
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(D)
+    if qkv.is_cuda and _gpu_ok(qkv, S, D):
+        return _AttentionPacked.apply(qkv.contiguous(), bool(causal), p, scale)
+    q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
+    if qkv.is_cuda:
+        _note_math_path(S, D, qkv.dtype)
+    o = attention_reference(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), causal, p, scale)
+    return o.transpose(1, 2)
 
 
 def attention(
     q: Tensor, k: Tensor, v: Tensor, causal: bool = False, dropout_p: float = 0.0, training: bool = True,
     scale: Optional[float] = None,
 ) -> Tensor:
+    """``q, k, v [B, H, S, D]`` -> ``[B, H, S, D]``."""
     p = float(dropout_p) if training else 0.0
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if not q.is_cuda:
         return attention_reference(q, k, v, causal, p, scale)
-    kern = native_or_none(q)
-    if not hasattr(kern, "attention_fwd"):
-        # Bring-up only: the HIP flash kernel is not in this build yet.
-        return F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=causal, scale=scale)
-    return _FlashAttention.apply(q, k, v, bool(causal), p, scale)
+    S, D = q.shape[2], q.shape[3]
+    if not _gpu_ok(q, S, D):
+        _note_math_path(S, D, q.dtype)
+        return attention_reference(q, k, v, causal, p, scale)
+    qs, ks, vs = (t.transpose(1, 2) for t in (q, k, v))
+    if not (qs.stride() == ks.stride() == vs.stride()) or qs.stride(3) != 1:
+        qs, ks, vs = (t.contiguous() for t in (qs, ks, vs))
+    o = _Attention.apply(qs, ks, vs, bool(causal), p, scale)
+    return o.transpose(1, 2)

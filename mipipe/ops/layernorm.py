@@ -45,18 +45,18 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
     def backward(ctx, dy):  # type: ignore[override]
         z, mean, rstd, weight = ctx.saved_tensors
         k = native_or_none(dy)
-        dz, dx, dgamma, dbeta = k.layernorm_bwd(dy.contiguous(), z, mean, rstd, weight, ctx.p, ctx.seed, ctx.offset)
+        mg = getattr(weight, "main_grad", None)
+        mb = ctx.bias_main_grad
+        if mg is not None and mb is not None:
+            # dgamma/dbeta accumulate straight into the fp32 main_grad buffers
+            dz, dx, dgamma, dbeta = k.layernorm_bwd(dy.contiguous(), z, mean, rstd, weight, ctx.p, ctx.seed,
+                                                    ctx.offset, mg, mb)
+        else:
+            dz, dx, dgamma, dbeta = k.layernorm_bwd(dy.contiguous(), z, mean, rstd, weight, ctx.p, ctx.seed,
+                                                    ctx.offset)
         if dx is None:
             dx = dz
         dres = dz if ctx.has_residual else None
-        mg = getattr(weight, "main_grad", None)
-        if mg is not None:
-            mg.add_(dgamma)
-            dgamma = None
-        mb = getattr(ctx, "bias_main_grad", None)
-        if mb is not None:
-            mb.add_(dbeta)
-            dbeta = None
         return dx, dres, dgamma, dbeta, None, None
 
 

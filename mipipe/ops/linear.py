@@ -68,15 +68,20 @@ class _Linear(torch.autograd.Function):
         k = native_or_none(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
+        main_b = getattr(bias, "main_grad", None) if need_db else None
         act, p = ctx.act, ctx.p
         if act != 0 or p > 0.0:
             # GEMM-saved GELU pre-activation already includes the bias.
             bias_for_bwd = None if ctx.fused_tile else bias
             dpre, db = k.bias_act_bwd(d2, saved if saved is not None else d2, bias_for_bwd, act, p,
-                                      ctx.seed, ctx.offset, need_db)
+                                      ctx.seed, ctx.offset, need_db, main_b)
         else:
             dpre = d2
-            db = k.column_sum(d2) if need_db else None
+            db = None
+            if main_b is not None:
+                k.column_sum(d2, main_b, True)  # fp32 main_grad += colsum(dy)
+            elif need_db:
+                db = k.column_sum(d2)
 
         dx = None
         if ctx.needs_input_grad[0]:
@@ -95,11 +100,6 @@ class _Linear(torch.autograd.Function):
                 main.add_(torch.matmul(dpre.t(), x2).float())
             else:
                 dw = torch.matmul(dpre.t(), x2)
-        if db is not None:
-            main_b = getattr(bias, "main_grad", None)
-            if main_b is not None:
-                main_b.add_(db)
-                db = None
         return dx, dw, db, None, None
 
 

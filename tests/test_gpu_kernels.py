@@ -379,3 +379,113 @@ def test_linear_dropout_mask_and_main_grad(k):
     keep2 = (y2 != 0).float()
     expect2 = expect + ((g.to(torch.bfloat16).float() * keep2 / (1 - p)).t() @ x.float())
     assert torch.allclose(w.main_grad, expect2, atol=3e-1, rtol=3e-2)
+
+
+# ------------------------------------------------------------------ attention
+def _philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """numpy Philox4x32-10 (the kernels' RNG), vectorised over counters."""
+    import numpy as np
+
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    mask = np.uint64(0xFFFFFFFF)
+    c0, c1, c2, c3 = (np.asarray(x, dtype=np.uint64) for x in (c0, c1, c2, c3))
+    k0, k1 = np.uint64(k0), np.uint64(k1)
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & mask, lo1, (hi0 ^ c3 ^ k1) & mask, lo0
+        k0 = (k0 + np.uint64(0x9E3779B9)) & mask
+        k1 = (k1 + np.uint64(0xBB67AE85)) & mask
+    return c0, c1, c2, c3
+
+
+def _attn_keep_mask(B, H, S, p, seed, offset):
+    import numpy as np
+
+    bh, q, key = np.meshgrid(np.arange(B * H), np.arange(S), np.arange(S), indexing="ij")
+    sub = (bh.astype(np.uint64) * np.uint64(S // 4) + (q // 4).astype(np.uint64)) * np.uint64(S) + key.astype(np.uint64)
+    seed = seed & 0xFFFFFFFFFFFFFFFF
+    offset = offset & 0xFFFFFFFFFFFFFFFF
+    m32 = np.uint64(0xFFFFFFFF)
+    words = _philox4x32_10(sub & m32, sub >> np.uint64(32), np.uint64(offset) & m32, np.uint64(offset) >> np.uint64(32),
+                           seed & 0xFFFFFFFF, seed >> 32)
+    w = np.choose((q & 3), words)
+    thr = min(int(p * 4294967296.0), 0xFFFFFFFF)
+    return torch.from_numpy((w >= thr).reshape(B, H, S, S))
+
+
+def _ref_attention_masked(q, k, v, causal, keep, p, scale):
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    if causal:
+        S = s.shape[-1]
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    pr = torch.softmax(s, dim=-1)
+    if keep is not None:
+        pr = pr * keep.to(pr.device).float() / (1 - p)
+    return torch.matmul(pr, v.float())
+
+
+@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("p", [0.0, 0.25])
+def test_attention_packed(k, D, causal, p):
+    from mipipe.ops import attention_packed
+
+    torch.manual_seed(4)
+    B, S, H = 2, 128, 2
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16).requires_grad_()
+    scale = 1.0 / math.sqrt(D)
+    if p > 0:
+        q, kk, v = (qkv.detach().select(2, i) for i in range(3))
+        o, lse, seed, offset = k.attention_fwd(q, kk, v, causal, p, scale)
+        keep = _attn_keep_mask(B, H, S, p, seed, offset)
+        assert abs(keep.float().mean().item() - (1 - p)) < 0.02
+    else:
+        keep = None
+    torch.manual_seed(11)
+    o = attention_packed(qkv, causal, p, True)  # [B, S, H, D]
+    if p > 0:
+        # the op drew its own seed: rebuild the mask from the generator state it used
+        torch.manual_seed(11)
+        _, _, seed2, offset2 = k.attention_fwd(*(qkv.detach().select(2, i) for i in range(3)), causal, p, scale)
+        keep = _attn_keep_mask(B, H, S, p, seed2, offset2)
+    qf = qkv.detach().float().requires_grad_()
+    qh, kh, vh = (qf.select(2, i).transpose(1, 2) for i in range(3))
+    ref = _ref_attention_masked(qh, kh, vh, causal, keep, p, scale).transpose(1, 2)
+    err = (o.float() - ref).abs().max().item()
+    assert err < 3e-2, err
+    g = torch.randn_like(ref)
+    o.backward(g.to(torch.bfloat16))
+    ref.backward(g)
+    gerr = (qkv.grad.float() - qf.grad).abs().max().item()
+    gscale = qf.grad.abs().max().item()
+    assert gerr < 3e-2 * max(1.0, gscale), (gerr, gscale)
+
+
+def test_attention_bhsd_api(k):
+    from mipipe.ops import attention, attention_reference
+
+    torch.manual_seed(5)
+    q, kk, v = (torch.randn(2, 4, 192, 64, device=DEV).to(torch.bfloat16) for _ in range(3))
+    o = attention(q, kk, v, causal=True)
+    ref = attention_reference(q, kk, v, True, 0.0)
+    assert (o.float() - ref.float()).abs().max().item() < 3e-2
+
+
+def test_transformer_layer_bf16_kernels_vs_torch(k):
+    """The bf16 hot path (MFMA GEMMs, flash attention, fused LN) vs nn.TransformerEncoderLayer in fp32."""
+    from torch import nn
+
+    from mipipe.models import TransformerEncoderLayer
+
+    torch.manual_seed(0)
+    E, H, F_, B, S = 512, 4, 1024, 2, 128
+    ref = nn.TransformerEncoderLayer(E, H, F_, dropout=0.0, batch_first=True).to(DEV)
+    ours = TransformerEncoderLayer(E, H, F_, dropout=0.0, device=DEV).load_from_torch(ref).to(torch.bfloat16)
+    x = torch.randn(B, S, E, device=DEV)
+    y = ours(x.to(torch.bfloat16).requires_grad_())
+    yr = ref(x)
+    err = (y.float() - yr).abs().max().item()
+    assert err < 0.1, err
