@@ -158,9 +158,11 @@ void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int
 }
 
 int colsum_parts(int64_t rows) {
-  // ~64 rows per part keeps stage 1 latency-friendly and stage 2 short.
-  int64_t parts = (rows + 63) / 64;
-  return (int)(parts < 1 ? 1 : (parts > 256 ? 256 : parts));
+  // ~16 rows per part: enough workgroups in stage 1 to stream at HBM rate
+  // (4096 rows x 4096 cols -> 256 parts x 2 column blocks); stage 2 reads the
+  // 4 MiB of partials with 64 coalesced workgroups.
+  int64_t parts = (rows + 15) / 16;
+  return (int)(parts < 1 ? 1 : (parts > 512 ? 512 : parts));
 }
 
 template <typename T>

@@ -247,7 +247,7 @@ constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int kThreads = 512;
 constexpr int kTileBytes = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int kBufBytes = 2 * kTileBytes;    // A + B
-constexpr int kSmemBytes = 2 * kBufBytes;    // 128 KiB
+constexpr int kSmemBytes = 128 * 260 * 4;    // 130 KiB: 2 x 64 KiB operand buffers, reused by the epilogue
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -339,46 +339,100 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     }
   }
 
+  // ---- epilogue ----
+  // 1) element-wise epilogue in registers (accumulator layout);
+  // 2) the block's 256 x 256 result is written out through LDS in two halves
+  //    (waves wm = 0, then wm = 1): each wave spills its 128 x 64 tile into a
+  //    [128][260] fp32 image (the 4-float row pad makes the scattered 4-byte
+  //    writes conflict-free), then all 512 threads stream whole 1 KiB rows
+  //    back with 16-byte accesses -- fp32 read-modify-write for the weight
+  //    gradient, 16-byte bf16 stores otherwise.
   const int quad = lane >> 4, col_in = lane & 15;
   const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
+  if (EPI == kEpiStoreBf16) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
+    for (int i = 0; i < 8; ++i) {
+      const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn * 64 + 16 * j + col_in;
-      const f32x4 v = acc[i][j];
-      if (EPI == kEpiAccumF32) {
-        float* C = reinterpret_cast<float*>(g.C);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) C[(int64_t)(row0 + r) * g.ldc + col] += v[r];
-      } else if (EPI == kEpiStoreF32) {
-        float* C = reinterpret_cast<float*>(g.C);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) C[(int64_t)(row0 + r) * g.ldc + col] = v[r];
-      } else {
-        bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + 16 * j + col_in;
         const float b = g.bias != nullptr ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
-        float pre[4], out[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pre[r] = v[r] + b;
-          out[r] = ACT == kActRelu ? fmaxf(pre[r], 0.f) : (ACT == kActGelu ? gelu_f(pre[r]) : pre[r]);
-        }
+        uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         if (g.p > 0.f) {
           const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
           const uint4 w = Philox(g.seed, sub, g.offset).next4();
-          const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) out[r] = ws[r] >= g.threshold ? out[r] * pscale : 0.f;
+          ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          C[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out[r]);
-          if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre[r]);
+          const float pre = acc[i][j][r] + b;
+          float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
+          if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
+          reinterpret_cast<bf16_t*>(g.C)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out);
+          if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre);
         }
       }
     }
+    return;  // direct 2-byte stores measured faster than staging for bf16 (profiles/gemm_ablation.txt)
+  }
+  if (EPI == kEpiStoreF32) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          reinterpret_cast<float*>(g.C)[(int64_t)(m0 + wm * 128 + 16 * i + 4 * quad + r) * g.ldc + n0 + wn * 64 +
+                                        16 * j + col_in] = acc[i][j][r];
+    return;
+  }
+
+  constexpr int kStride = 260;  // floats per staged row (256 + 4 pad)
+  float* stg = reinterpret_cast<float*>(smem);
+  __syncthreads();  // every wave is done reading the operand buffers
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(16 * i + 4 * quad + r) * kStride + wn * 64 + 16 * j + col_in] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int rbase = m0 + pass * 128;
+    if (EPI == kEpiStoreBf16) {
+      bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // 128 rows x 32 chunks of 8 columns
+        const int idx = tid + u * kThreads;
+        const int row = idx >> 5, c8 = idx & 31;
+        const float4 lo = *reinterpret_cast<const float4*>(stg + row * kStride + 8 * c8);
+        const float4 hi = *reinterpret_cast<const float4*>(stg + row * kStride + 8 * c8 + 4);
+        bf16x8 o;
+        o[0] = (__bf16)lo.x; o[1] = (__bf16)lo.y; o[2] = (__bf16)lo.z; o[3] = (__bf16)lo.w;
+        o[4] = (__bf16)hi.x; o[5] = (__bf16)hi.y; o[6] = (__bf16)hi.z; o[7] = (__bf16)hi.w;
+        *reinterpret_cast<bf16x8*>(C + (int64_t)(rbase + row) * g.ldc + n0 + 8 * c8) = o;
+      }
+    } else {
+      float* C = reinterpret_cast<float*>(g.C);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {  // 128 rows x 64 chunks of 4 columns
+        const int idx = tid + u * kThreads;
+        const int row = idx >> 6, c4 = idx & 63;
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * kStride + 4 * c4);
+        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(rbase + row) * g.ldc + n0 + 4 * c4);
+        if (EPI == kEpiAccumF32) {
+          const float4 o = *dst;
+          *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        } else {
+          *dst = v;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 

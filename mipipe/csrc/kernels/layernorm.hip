@@ -199,7 +199,7 @@ int ln_max_vec(int cols) {
   return -1;
 }
 
-int ln_bwd_parts(int rows) { return rows < 256 ? rows : 256; }
+int ln_bwd_parts(int rows) { return rows < 512 ? rows : 512; }
 
 template <typename T>
 void layernorm_fwd(const LnArgs<T>& a, hipStream_t s) {
