@@ -1,4 +1,5 @@
-"""Utilities: model partitioning helpers, timing and memory reporting."""
+"""Utilities: model partitioning, LM data pipeline, profiling/memory instrumentation."""
 from .partition import partition_model
+from . import data, profiling
 
-__all__ = ["partition_model"]
+__all__ = ["partition_model", "data", "profiling"]
