@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="enc12_d4096")
-    ap.add_argument("--micro-batch", type=int, default=32, help="sequences per micro-batch")
+    ap.add_argument("--micro-batch", type=int, default=None,
+                    help="sequences per micro-batch (default 32 for enc12_d4096 / ref_main, 8 for gpt2_xl)")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
     ap.add_argument("--checkpoint", default="never", choices=["never", "except_last", "always"])
@@ -73,7 +74,7 @@ def main() -> int:
     S, E, V = cfg.seq_len, cfg.d_model, cfg.vocab
     pp = world
     m = args.chunks or 4 * pp
-    mb = args.micro_batch
+    mb = args.micro_batch or {"gpt2_xl": 8, "tiny": 8}.get(cfg.name, 32)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
     plan = plan_stages(cfg, pp)
@@ -162,7 +163,8 @@ def main() -> int:
     total_params = sum(int(x) for x in _allsum([n_params_local], device, world))
     if rank == 0:
         out = {
-            "metric": "tokens/sec for 12-layer Transformer at PP=N (pipeline-parallel training)",
+            "metric": ("tokens/sec for 12-layer Transformer at PP=N (pipeline-parallel training)"
+                       if cfg.name == "enc12_d4096" else f"tokens/sec for {cfg.name} at PP=N (pipeline-parallel training)"),
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -175,7 +177,7 @@ def main() -> int:
             "dtype": args.dtype,
             "data": "synthetic (random tokens, random-init weights)",
             "config": {
-                "model": f"{cfg.name}: {cfg.num_layers}x TransformerEncoderLayer(d_model={E}, nhead={cfg.nhead}, "
+                "model": f"{cfg.name}: {cfg.num_layers}x {'causal decoder' if cfg.causal else 'TransformerEncoder'}Layer(d_model={E}, nhead={cfg.nhead}, "
                          f"dim_feedforward={cfg.dim_feedforward}, dropout={cfg.dropout}, {cfg.activation}, "
                          f"{'pre' if cfg.norm_first else 'post'}-norm) + embedding/decoder V={V}",
                 "params": total_params,

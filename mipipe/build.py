@@ -63,7 +63,9 @@ def _sources() -> List[Tuple[str, str]]:
 def _flags(kind: str) -> List[str]:
     common = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1"]
     if kind == "kernel":
-        return common + ["-O3", "-ffp-contract=fast", "-munsafe-fp-atomics"]
+        # Fully unrolled epilogues keep MFMA accumulators in registers (an
+        # unroll refused for size spills them to scratch).
+        return common + ["-O3", "-ffp-contract=fast", "-munsafe-fp-atomics", "-mllvm", "-pragma-unroll-threshold=1000000"]
     if kind == "runtime":
         return common + ["-O2", f"-I{ROCM}/include"]
     tinc, _ = _torch_paths()

@@ -130,7 +130,7 @@ __device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, i
 }
 
 template <bool A_KC, bool B_KC, int EPI, int ACT>
-__global__ void __launch_bounds__(kThreads, 2) gemm_kernel(GemmArgs g) {
+__global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -254,9 +254,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 // I-contiguous image with 512-byte rows (256 i values).
 __device__ __forceinline__ int ic_off(int r, int c8) { return r * 512 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
 
+// Edge tiles: i indices past `lim` (M for A, N for B) are clamped onto the last
+// valid row / 8-column chunk, so every DMA reads mapped memory; the garbage
+// they produce lands only in accumulator rows/columns the epilogue masks off.
 template <bool KC>
-__device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t ld, int i0, int k0, char* tile,
-                                      int wave, int lane) {
+__device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t ld, int i0, int k0, int lim,
+                                      char* tile, int wave, int lane) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int inst = wave * 4 + u;  // 32 x 1 KiB pieces per tile
@@ -264,11 +267,13 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t l
     if (KC) {
       const int row = 8 * inst + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
-      src = base + (int64_t)(i0 + row) * ld + k0 + 8 * c;
+      const int gi = min(i0 + row, lim - 1);
+      src = base + (int64_t)gi * ld + k0 + 8 * c;
     } else {
       const int row = 2 * inst + (lane >> 5);
       const int c16 = (lane & 31) ^ (ic_rk(row) << 1);
-      src = base + (int64_t)(k0 + row) * ld + i0 + 8 * c16;
+      const int gi = min(i0 + 8 * c16, lim - 8);
+      src = base + (int64_t)(k0 + row) * ld + gi;
     }
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(tile + inst * 1024), 16, 0, 0);
   }
@@ -290,7 +295,27 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane
   }
 }
 
-template <bool A_KC, bool B_KC, int EPI, int ACT>
+// Ping-pong main loop (PP = true).  The two wave groups (wm = 0: waves 0-3,
+// wm = 1: waves 4-7; each SIMD hosts one wave of each) run one barrier
+// interval apart, so in every interval one wave per SIMD issues its 16-MFMA
+// cluster while its partner issues the LDS fragment reads (and LDS-DMA
+// staging) for its next cluster -- the LDS latency of one group hides behind
+// the other's MFMAs instead of stalling both (guide: 256^2 8-phase template,
+// T5 s_setprio).  A K-tile is 4 phases, one per 64x32 quadrant of the wave's
+// 128x64 tile, in the order (0,0) (0,1) (1,1) (1,0): A fragments are read in
+// phases 0 and 2, B in phases 0 and 1 and kept, phase 3 reads nothing.
+// Buffer hand-off (intervals counted from group 0's first phase of tile u,
+// group 1 one behind):
+//   * tile u+1 is DMA'd into the other buffer in phases 0/1 (A/B) of tile u:
+//     that buffer (tile u-1) was last read in tile u-1's phase 2, retired by
+//     the lgkmcnt(0) of phase 2's MFMA interval, behind >= 1 barrier;
+//   * each wave drains its own DMA (vmcnt(0)) before the barrier that ends
+//     the last interval of tile u -- group 0 after its phase-3 MFMAs, group 1
+//     in its phase-3 load interval -- so every wave's reads of tile u+1 start
+//     after a barrier all DMAs of the tile have landed behind.
+int g_gemm_sched = 1;  // 1: ping-pong (default), 0: one barrier per K-tile
+
+template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP>
 __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -299,7 +324,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
 
   int tm, tn;
-  tile_coords(g.M / BM, g.N / BN, tm, tn);
+  tile_coords((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const bf16_t* A = reinterpret_cast<const bf16_t*>(g.A);
   const bf16_t* B = reinterpret_cast<const bf16_t*>(g.B);
@@ -311,9 +336,62 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BK;
-  stage<A_KC>(A, g.lda, m0, 0, smem, wave, lane);
-  stage<B_KC>(B, g.ldb, n0, 0, smem + kTileBytes, wave, lane);
+  stage<A_KC>(A, g.lda, m0, 0, g.M, smem, wave, lane);
+  stage<B_KC>(B, g.ldb, n0, 0, g.N, smem + kTileBytes, wave, lane);
 
+  if constexpr (PP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
+    bf16x8 af[4][2], bf[2][2][2];
+    for (int u = 0; u < nk; ++u) {
+      const char* cur = smem + (u & 1) * kBufBytes;
+      char* nxt = smem + ((u + 1) & 1) * kBufBytes;
+      const bool more = u + 1 < nk;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int qm = ph >= 2 ? 1 : 0;
+        const int qn = (ph == 1 || ph == 2) ? 1 : 0;
+        // ---- load interval: this cluster's fragments, then staging DMA ----
+        if (ph == 0 || ph == 2) {
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC>(cur, wm * 128 + qm * 64 + 16 * ii, s, lane);
+        }
+        if (ph == 0 || ph == 1) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              bf[qn][jj][s] = frag<B_KC>(cur + kTileBytes, wn * 64 + qn * 32 + 16 * jj, s, lane);
+        }
+        if (ph == 0 && more) stage<A_KC>(A, g.lda, m0, (u + 1) * BK, g.M, nxt, wave, lane);
+        if (ph == 1 && more) stage<B_KC>(B, g.ldb, n0, (u + 1) * BK, g.N, nxt + kTileBytes, wave, lane);
+        if (ph == 3 && wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- MFMA interval ----
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              acc[qm * 4 + ii][qn * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  af[ii][s], bf[qn][jj][s], acc[qm * 4 + ii][qn * 2 + jj], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (ph == 3 && wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // equalise the barrier count
+  } else {
   for (int kt = 0; kt < nk; ++kt) {
     // Tile kt has landed (every wave drained its own DMA) and every wave is
     // done reading the buffer the next prefetch overwrites.
@@ -321,8 +399,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     __syncthreads();
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * kBufBytes;
-      stage<A_KC>(A, g.lda, m0, (kt + 1) * BK, nxt, wave, lane);
-      stage<B_KC>(B, g.ldb, n0, (kt + 1) * BK, nxt + kTileBytes, wave, lane);
+      stage<A_KC>(A, g.lda, m0, (kt + 1) * BK, g.M, nxt, wave, lane);
+      stage<B_KC>(B, g.ldb, n0, (kt + 1) * BK, g.N, nxt + kTileBytes, wave, lane);
     }
     const char* cur = smem + (kt & 1) * kBufBytes;
 #pragma unroll
@@ -337,6 +415,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
     }
+  }
   }
 
   // ---- epilogue ----
@@ -355,8 +434,11 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        // Predicated (never continue/break: the accumulator array must stay
+        // fully unrolled in registers -- an early exit spills it to scratch).
         const int col = n0 + wn * 64 + 16 * j + col_in;
-        const float b = g.bias != nullptr ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
+        const bool col_ok = col < g.N;
+        const float b = (g.bias != nullptr && col_ok) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
         uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         if (g.p > 0.f) {
           const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
@@ -368,8 +450,10 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
           const float pre = acc[i][j][r] + b;
           float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
           if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
-          reinterpret_cast<bf16_t*>(g.C)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out);
-          if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre);
+          if (col_ok && row0 + r < g.M) {
+            reinterpret_cast<bf16_t*>(g.C)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out);
+            if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre);
+          }
         }
       }
     }
@@ -381,9 +465,10 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          reinterpret_cast<float*>(g.C)[(int64_t)(m0 + wm * 128 + 16 * i + 4 * quad + r) * g.ldc + n0 + wn * 64 +
-                                        16 * j + col_in] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 128 + 16 * i + 4 * quad + r, col = n0 + wn * 64 + 16 * j + col_in;
+          if (row < g.M && col < g.N) reinterpret_cast<float*>(g.C)[(int64_t)row * g.ldc + col] = acc[i][j][r];
+        }
     return;
   }
 
@@ -409,6 +494,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       for (int u = 0; u < 8; ++u) {  // 128 rows x 32 chunks of 8 columns
         const int idx = tid + u * kThreads;
         const int row = idx >> 5, c8 = idx & 31;
+        if (rbase + row >= g.M || n0 + 8 * c8 >= g.N) continue;
         const float4 lo = *reinterpret_cast<const float4*>(stg + row * kStride + 8 * c8);
         const float4 hi = *reinterpret_cast<const float4*>(stg + row * kStride + 8 * c8 + 4);
         bf16x8 o;
@@ -422,6 +508,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       for (int u = 0; u < 16; ++u) {  // 128 rows x 64 chunks of 4 columns
         const int idx = tid + u * kThreads;
         const int row = idx >> 6, c4 = idx & 63;
+        if (rbase + row >= g.M || n0 + 4 * c4 >= g.N) continue;
         const float4 v = *reinterpret_cast<const float4*>(stg + row * kStride + 4 * c4);
         float4* dst = reinterpret_cast<float4*>(C + (int64_t)(rbase + row) * g.ldc + n0 + 4 * c4);
         if (EPI == kEpiAccumF32) {
@@ -438,22 +525,31 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 
 }  // namespace big
 
-bool use_big(const GemmArgs& g) {
-  return g.M % big::BM == 0 && g.N % big::BN == 0 && (g.M / big::BM) * (g.N / big::BN) >= 128;
-}
+int big_tiles(const GemmArgs& g) { return ((g.M + big::BM - 1) / big::BM) * ((g.N + big::BN - 1) / big::BN); }
+
+// The 256x256 kernel handles every shape (edge tiles masked); the 128x128 one
+// only exact multiples of 128, where it is kept for grids too small to fill
+// the 256 CUs with 256x256 tiles.
+bool use_big(const GemmArgs& g) { return g.M % BM != 0 || g.N % BN != 0 || big_tiles(g) >= 128; }
 
 template <bool A_KC, bool B_KC, int EPI, int ACT>
 void launch(const GemmArgs& g, hipStream_t s) {
   if (use_big(g)) {
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
       attr_set = true;
     }
-    const int blocks = (g.M / big::BM) * (g.N / big::BN);
-    hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT>), dim3(blocks), dim3(big::kThreads),
-                       big::kSmemBytes, s, g);
+    const int blocks = big_tiles(g);
+    if (big::g_gemm_sched == 1)
+      hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, true>), dim3(blocks), dim3(big::kThreads),
+                         big::kSmemBytes, s, g);
+    else
+      hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, false>), dim3(blocks), dim3(big::kThreads),
+                         big::kSmemBytes, s, g);
     return;
   }
   const int blocks = (g.M / BM) * (g.N / BN);
@@ -471,8 +567,13 @@ void launch_act(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+void gemm_set_schedule(int mode) { big::g_gemm_sched = mode; }
+int gemm_get_schedule() { return big::g_gemm_sched; }
+
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
-  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0;
+  // 16-byte operand chunks along M/N (I-contiguous layouts) and whole 64-deep K tiles.
+  return M >= 8 && N >= 8 && K > 0 && M % 8 == 0 && N % 8 == 0 && K % BK == 0 && M < (1LL << 30) &&
+         N < (1LL << 30);
 }
 
 void gemm_bf16(const GemmArgs& gi, hipStream_t s) {

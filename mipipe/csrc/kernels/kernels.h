@@ -92,6 +92,9 @@ struct GemmArgs {
   uint64_t seed = 0, offset = 0;
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
+// Main-loop schedule of the 256x256 GEMM: 1 = ping-pong wave groups (default), 0 = one barrier per K-tile.
+void gemm_set_schedule(int mode);
+int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
 
 // ------------------------------------------------------------------ attention

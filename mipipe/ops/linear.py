@@ -29,10 +29,14 @@ __all__ = ["linear"]
 
 
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
+    """All three GEMMs of the layer (fwd [T,N,K], dgrad [T,K,N], wgrad [N,K,T]) fit the tile kernel."""
+    t, (n, kk) = x2.shape[0], weight.shape
     return (
         x2.dtype == torch.bfloat16
         and weight.dtype == torch.bfloat16
-        and k.gemm_supported(x2.shape[0], weight.shape[0], weight.shape[1])
+        and k.gemm_supported(t, n, kk)
+        and k.gemm_supported(t, kk, n)
+        and k.gemm_supported(n, kk, t)
     )
 
 

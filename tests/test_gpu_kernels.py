@@ -321,7 +321,9 @@ def test_engine_one_gpu_step(k):
 
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (512, 256, 1024), (2048, 4096, 256), (4096, 2048, 128)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (512, 256, 1024), (2048, 4096, 256), (4096, 2048, 128),
+                                   # edge tiles (GPT-2-XL widths 1600 / 4800, odd multiples of 8)
+                                   (200, 136, 64), (1000, 1000, 128), (4096, 4800, 1600), (4800, 1600, 1024)])
 def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
     torch.manual_seed(1)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -355,6 +357,35 @@ def test_linear_op_matches_reference(k):
         assert torch.allclose(x.grad.float(), xf.grad, atol=6e-2, rtol=5e-2), act
         assert torch.allclose(w.grad.float(), wf.grad, atol=2e-1, rtol=5e-2), act
         assert torch.allclose(b.grad.float(), bf.grad, atol=2e-1, rtol=5e-2), act
+
+
+@pytest.mark.parametrize("T,K,N", [(2048, 1600, 4800), (1024, 6400, 1600), (520, 264, 136)])
+def test_linear_edge_shapes_main_grad(k, T, K, N):
+    """Non-multiple-of-256 widths (GPT-2-XL) go through the masked edge tiles in all three GEMMs."""
+    from mipipe.ops import linear
+
+    torch.manual_seed(4)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=DEV).to(torch.bfloat16).requires_grad_()
+    w.main_grad = torch.zeros(N, K, device=DEV)
+    b.main_grad = torch.zeros(N, device=DEV)
+    y = linear(x, w, b, "gelu", 0.0, True)
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    ref = F.gelu(xf @ wf.t() + bf)
+    g = torch.randn_like(ref)
+    y.backward(g.to(torch.bfloat16))
+    ref.backward(g)
+
+    def rel(a, b):  # error relative to the tensor's scale (sums over up to 6400 bf16 products)
+        return ((a.float() - b).abs().max() / b.abs().max()).item()
+
+    assert rel(y, ref) < 2e-2
+    assert rel(x.grad, xf.grad) < 2e-2
+    assert rel(w.main_grad, wf.grad) < 2e-2
+    assert rel(b.main_grad, bf.grad) < 2e-2
+    # masked edge tiles must not write past N / M: check the last rows/cols explicitly
+    assert rel(w.main_grad[-8:, -8:], wf.grad[-8:, -8:]) < 5e-2
 
 
 def test_linear_dropout_mask_and_main_grad(k):

@@ -44,6 +44,11 @@ dy = torch.randn(K, M, device="cuda").to(torch.bfloat16)   # [T=K, M]
 xx = torch.randn(K, N, device="cuda").to(torch.bfloat16)   # [T=K, N]
 cases["IC,IC f32-accumulate (wgrad)"] = lambda: k.linear_wgrad(dy, xx, c)
 cases["hipBLASLt bf16"] = lambda: torch.matmul(a, b.t())
+scheds = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [k.gemm_get_schedule()]
 for name, fn in cases.items():
-    t = timeit(fn)
-    print(f"{name:34s} {t * 1e3:8.1f} us  {fl / t / 1e9:7.0f} TF/s")
+    for sc in scheds:
+        k.gemm_set_schedule(sc)
+        t = timeit(fn)
+        print(f"{name:34s} sched={sc} {t * 1e3:8.1f} us  {fl / t / 1e9:7.0f} TF/s")
+        if name.startswith("hipBLASLt"):
+            break
