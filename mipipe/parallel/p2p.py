@@ -6,6 +6,11 @@ joins them (every GPU pair has its own link, so stage placement order does not
 matter).  Receives are posted ahead of use so transfers overlap compute; a
 received tensor is made usable on the current compute stream by
 ``Work.wait()`` (a stream wait, not a host block).
+
+With the ``gloo`` backend (CPU tests, or several ranks sharing one GPU, which
+RCCL refuses) device tensors are staged through host memory: the send copies
+to a host buffer, the receive lands in one and ``wait()`` copies it to the
+device tensor.  That path is for testing the engine, not for speed.
 """
 from __future__ import annotations
 
@@ -18,6 +23,23 @@ from torch import Tensor
 __all__ = ["P2P", "exchange_shape"]
 
 
+class _HostStagedWork:
+    """Work handle of a host-staged transfer; ``wait()`` completes the device copy."""
+
+    def __init__(self, work: dist.Work, host: Tensor, dst: Optional[Tensor] = None) -> None:
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self) -> bool:
+        self.work.wait()
+        if self.dst is not None:
+            self.dst.copy_(self.host)
+            self.dst = None
+        return True
+
+    def is_completed(self) -> bool:
+        return self.work.is_completed()
+
+
 class P2P:
     """Sends/receives tensors to/from neighbour ranks of a process group."""
 
@@ -25,24 +47,35 @@ class P2P:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.host_staged = dist.get_backend(group) == "gloo"
 
     def global_rank(self, group_rank: int) -> int:
         if self.group is None:
             return group_rank
         return dist.get_global_rank(self.group, group_rank)
 
-    def isend(self, t: Tensor, dst: int) -> dist.Work:
+    def _meta_device(self, device: torch.device) -> torch.device:
+        return torch.device("cpu") if self.host_staged else device
+
+    def isend(self, t: Tensor, dst: int):
+        if self.host_staged and t.device.type != "cpu":
+            host = t.detach().to("cpu")
+            return _HostStagedWork(dist.isend(host, self.global_rank(dst), group=self.group), host)
         return dist.isend(t.contiguous(), self.global_rank(dst), group=self.group)
 
-    def irecv(self, t: Tensor, src: int) -> dist.Work:
+    def irecv(self, t: Tensor, src: int):
+        if self.host_staged and t.device.type != "cpu":
+            host = torch.empty(t.shape, dtype=t.dtype)
+            return _HostStagedWork(dist.irecv(host, self.global_rank(src), group=self.group), host, t)
         return dist.irecv(t, self.global_rank(src), group=self.group)
 
     def send_obj_shape(self, shape: Sequence[int], dtype_code: int, dst: int, device: torch.device) -> None:
-        meta = torch.tensor([len(shape), dtype_code, *shape] + [0] * (8 - len(shape)), dtype=torch.int64, device=device)
+        meta = torch.tensor([len(shape), dtype_code, *shape] + [0] * (8 - len(shape)), dtype=torch.int64,
+                            device=self._meta_device(device))
         dist.send(meta, self.global_rank(dst), group=self.group)
 
     def recv_obj_shape(self, src: int, device: torch.device) -> Tuple[List[int], int]:
-        meta = torch.empty(10, dtype=torch.int64, device=device)
+        meta = torch.empty(10, dtype=torch.int64, device=self._meta_device(device))
         dist.recv(meta, self.global_rank(src), group=self.group)
         m = meta.tolist()
         n = m[0]

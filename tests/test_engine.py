@@ -112,11 +112,19 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, checkpoint, q):
+def _gpu_cfg():
+    # HIP-kernel-sized: head dim 64, S % 64 == 0, every GEMM dim a multiple of 8.
+    return dataclasses.replace(CONFIGS["tiny"], dropout=0.0, num_layers=2, d_model=256, nhead=4,
+                               dim_feedforward=512, vocab=512, seq_len=64)
+
+
+def _worker(rank, world, port, checkpoint, q, gpu=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = _tiny()
+        cfg = _gpu_cfg() if gpu else _tiny()
+        device = torch.device("cuda", 0) if gpu else torch.device("cpu")
+        dtype = torch.bfloat16 if gpu else torch.float32
         m, mb = 4, 2
         torch.manual_seed(0)
         full = torch.nn.Sequential(*build_lm_blocks(cfg))
@@ -124,17 +132,20 @@ def _worker(rank, world, port, checkpoint, q):
         units = pipeline_units(list(full.children()))
         plan = plan_stages(cfg, world)
         stage = torch.nn.Sequential(*merge_units([units[i] for i in plan.slice(rank)])).train()
+        stage = stage.to(device, dtype)
         opt = FlatAdam(stage.parameters(), lr=1e-3, max_grad_norm=0.5)
         eng = PipelineEngine(stage, chunks=m, checkpoint=checkpoint,
                              act_shape=stage_input_shape(cfg, plan, rank, mb),
-                             act_dtype=torch.float32, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
-                             device=torch.device("cpu"))
+                             act_dtype=dtype, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
+                             device=device)
         inputs, targets = _data(cfg, m, mb)
+        inputs = [x.to(device) for x in inputs]
+        targets = [t.to(device) for t in targets]
         opt.zero_grad()
         st = eng.step(inputs if rank == 0 else None, targets if rank == world - 1 else None)
         opt.fold_grads()
-        grads = {names[id(p)]: p.main_grad.clone() for p in stage.parameters()}
-        sq = opt.grad_sumsq()
+        grads = {names[id(p)]: p.main_grad.float().cpu().clone() for p in stage.parameters()}
+        sq = opt.grad_sumsq().cpu()
         dist.all_reduce(sq)
         q.put((rank, None if st.loss is None else float(st.loss), grads, float(sq)))
     finally:
@@ -169,3 +180,46 @@ def test_engine_two_ranks_gloo(checkpoint):
     assert seen == set(ref_params)
     ref_sq = sum(float(p.grad.double().pow(2).sum()) for p in ref.parameters())
     assert abs(total_sq - ref_sq) / ref_sq < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("checkpoint", ["never", "always"])
+def test_engine_two_ranks_share_gpu(checkpoint):
+    """Two pipeline ranks on one MI355X (gloo, host-staged boundaries): the HIP
+    kernels of both stages and the multi-rank schedule against the single-rank
+    engine on the whole model (same bf16 kernels, same initial weights)."""
+    cfg = _gpu_cfg()
+    m, mb = 4, 2
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    full = torch.nn.Sequential(*build_lm_blocks(cfg)).train().to(dev, torch.bfloat16)
+    opt = FlatAdam(full.parameters(), lr=1e-3, max_grad_norm=0.5)
+    eng = PipelineEngine(full, chunks=m, checkpoint="never", act_shape=(mb, cfg.seq_len), act_dtype=torch.bfloat16,
+                         loss_fn=_loss_fn(cfg), device=dev)
+    inputs, targets = _data(cfg, m, mb)
+    opt.zero_grad()
+    st = eng.step([x.to(dev) for x in inputs], [t.to(dev) for t in targets])
+    ref_loss = float(st.loss)
+    ref_sq = float(opt.grad_sumsq())
+    ref = {n: p.main_grad.float().cpu() for n, p in full.named_parameters()}
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = set()
+    for rank, loss, grads, sq in results:
+        if loss is not None:
+            assert abs(loss - ref_loss) < 2e-3 * abs(ref_loss)
+        for name, g in grads.items():
+            scale = ref[name].abs().max().item() + 1e-6
+            assert (g - ref[name]).abs().max().item() < 2e-2 * scale, name
+            seen.add(name)
+        assert abs(sq - ref_sq) / ref_sq < 1e-2
+    assert seen == set(ref)
