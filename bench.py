@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--clip", type=float, default=0.5)
     ap.add_argument("--no-bubble", action="store_true", help="skip the extra instrumented step")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = gloo + fp32 plumbing check of the multi-rank path (tests only)")
+    ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
+                    help="model chunks per rank (looping placement); 'auto' = shortest simulated step")
     return ap.parse_args()
 
 
@@ -56,17 +60,28 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=device)
+    else:
+        device = torch.device("cpu")
+        args.dtype = "fp32"
+        if world > 1:
+            dist.init_process_group("gloo")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     import mipipe  # noqa: F401
     from mipipe import ops
     from mipipe.models import CONFIGS
     from mipipe.optim import FlatAdam
     from mipipe.parallel import PipelineEngine, plan_stages
-    from mipipe.parallel.stage import build_stage, stage_input_shape
+    from mipipe.parallel.stage import build_stage, choose_virtual, simulate_step, stage_input_shape
 
     cfg = CONFIGS[args.config]
     if args.seq_len:
@@ -77,23 +92,28 @@ def main() -> int:
     mb = args.micro_batch or {"gpt2_xl": 8, "tiny": 8}.get(cfg.name, 32)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
-    plan = plan_stages(cfg, pp)
+    if args.virtual == "auto":
+        virtual, plan = choose_virtual(cfg, pp, m)
+    else:
+        virtual = int(args.virtual)
+        plan = plan_stages(cfg, pp, virtual, m)
     torch.manual_seed(1234 + rank)
-    # Build only this rank's units (analytic plan; nothing else is instantiated).
-    stage = build_stage(cfg, plan, rank, device=device, dtype=dtype)
-    stage.train()
-    n_params_local = sum(p.numel() for p in stage.parameters())
+    # Build only this rank's chunks (analytic plan; nothing else is instantiated).
+    stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype).train() for vs in plan.vstages(rank)]
+    params = [p for st_ in stages for p in st_.parameters()]
+    n_params_local = sum(p.numel() for p in params)
 
-    opt = FlatAdam(stage.parameters(), lr=args.lr, max_grad_norm=args.clip)
+    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip)
 
     is_last = rank == world - 1
 
     def loss_fn(y, t):
         return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
 
-    engine = PipelineEngine(stage, chunks=m, checkpoint=args.checkpoint,
-                            act_shape=stage_input_shape(cfg, plan, rank, mb), act_dtype=dtype,
-                            loss_fn=loss_fn if is_last else None, device=device)
+    engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
+                            act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
+                            act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device)
+    sim_t, sim_busy = simulate_step([plan.stage_cost(g) for g in range(pp * virtual)], pp, virtual, m)
 
     g = torch.Generator(device="cpu").manual_seed(0)
     tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)
@@ -111,17 +131,17 @@ def main() -> int:
 
     for _ in range(args.warmup):
         st = train_step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = train_step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     ms = elapsed / max(args.steps, 1) * 1e3
     ms_t = torch.tensor([ms], device=device)
@@ -135,13 +155,13 @@ def main() -> int:
 
     # Bubble: one extra instrumented step, per-stage GPU busy time vs step time.
     bubble = None
-    if not args.no_bubble:
+    if not args.no_bubble and on_gpu:
         engine.measure = True
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             dist.barrier()
         st = train_step()
-        torch.cuda.synchronize()
+        sync()
         busy = torch.tensor([st.busy_ms, st.step_ms], device=device)
         if world > 1:
             gathered = [torch.zeros_like(busy) for _ in range(world)]
@@ -186,13 +206,15 @@ def main() -> int:
                 "micro_batch": mb,
                 "chunks": m,
                 "checkpoint": args.checkpoint,
-                "schedule": "gpipe",
+                "schedule": "gpipe" if virtual == 1 else f"gpipe-looping(v={virtual})",
+                "virtual_chunks_per_rank": virtual,
                 "parallelism": f"pp{world}",
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
             },
             "bubble_pct": None if bubble is None else round(bubble, 2),
-            "bubble_theory_pct": round(100.0 * (pp - 1) / (m + pp - 1), 2),
+            "bubble_theory_pct": round(100.0 * (pp - 1) / (virtual * m + pp - 1), 2),
+            "bubble_sim_pct": round(100.0 * (1 - sum(sim_busy) / len(sim_busy) / sim_t), 2),
             "loss": loss_val,
             "baseline_note": "vs_baseline divides by the reference's ~3.5k tokens/s (BASELINE.md, 2 GPUs, fp32, "
                              "16x d2048 model, checkpoint='never'); see BASELINE.md",

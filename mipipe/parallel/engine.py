@@ -2,33 +2,44 @@
 
 This is the scale-out form of :class:`mipipe.Pipe` (SURVEY §5.8 (b), §7.2 step
 5): instead of one process driving every GPU from worker threads with peer
-copies, each GPU is one process (``torchrun --nproc-per-node N``) that owns a
-contiguous slice of the model, and activations / gradients move between
-neighbouring ranks with RCCL send/recv over xGMI.  It keeps the reference's
-semantics:
+copies, each GPU is one process (``torchrun --nproc-per-node N``) that owns
+slices of the model, and activations / gradients move between neighbouring
+ranks with RCCL send/recv over xGMI.  It keeps the reference's semantics:
 
 * micro-batching of the mini-batch on dim 0 into ``chunks`` micro-batches;
-* the GPipe fill-drain schedule: all forwards (clock cycles ``i + j = k``), then
-  all backwards in reverse micro-batch order -- exactly the order the
-  reference's fork/join phonies force (``/root/reference/pipeline.py:128-132``);
+* synchronous fill-drain: every forward of the step, then every backward in
+  reverse micro-batch order -- the order the reference's fork/join phonies
+  force (``/root/reference/pipeline.py:128-132``) -- and one optimizer step on
+  the summed gradients (identical to the unpartitioned model);
 * ``checkpoint`` in {``always``, ``except_last``, ``never``}: checkpointed
   micro-batches run forward under ``no_grad`` keeping only the stage input and
   the RNG state, and are recomputed (bit-identical dropout) right before their
   backward (``/root/reference/pipe.py:255-260,354``);
 * eval mode never checkpoints (``pipeline.py:153-155``).
 
-Optionally ``schedule="1f1b"`` (PipeDream-flush): same bubble, activation
-memory bounded by the number of stages instead of ``chunks``.
+Looping placement (``virtual`` > 1 model chunks per rank): rank ``r`` of ``n``
+owns virtual stages ``r, r+n, r+2n, ...``; a micro-batch flows
+0 -> 1 -> ... -> n-1 -> 0 -> ... and each rank runs its chunks breadth-first
+(all micro-batches of chunk 0, then chunk 1, ...; backward in reverse).  The
+step is still a synchronous GPipe step -- same gradients -- but the fill and
+drain shrink from (n-1) stage-times to (n-1) CHUNK-times:
+bubble = (n-1) / (v*m + n-1) instead of (n-1) / (m + n-1).  MI355X keeps every
+chunk's activations resident (288 GB of HBM), so the extra in-flight
+activations cost nothing, and the extra boundary messages ride idle xGMI links.
 
-Overlap: all receives of a phase are posted before the first compute so each
-transfer lands while the previous micro-batch computes; sends are asynchronous.
-Per-stage busy time is measured with HIP events to report the pipeline bubble.
+Optionally ``schedule="1f1b"`` (PipeDream-flush, ``virtual == 1``): same
+bubble, activation memory bounded by the number of stages instead of chunks.
+
+Transport: :class:`~mipipe.parallel.p2p.Channels` -- one communicator per link
+direction; all receives of a phase are posted before the first compute, in the
+order the peer sends, so each transfer lands while earlier micro-batches
+compute.  Per-stage busy time is measured with HIP events (bubble %).
 """
 from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import torch
 import torch.distributed as dist
@@ -36,7 +47,7 @@ from torch import Tensor, nn
 
 from ..checkpoint import enable_checkpointing, enable_recomputing
 from ..pipeline import checkpoint_stop_for
-from .p2p import P2P
+from .p2p import Channels
 
 __all__ = ["PipelineEngine", "StepStats", "schedule_actions"]
 
@@ -44,27 +55,36 @@ __all__ = ["PipelineEngine", "StepStats", "schedule_actions"]
 @dataclass
 class StepStats:
     loss: Optional[Tensor] = None
-    busy_ms: float = 0.0          # GPU time of this stage's compute (events)
+    busy_ms: float = 0.0          # GPU time of this rank's compute (events)
     step_ms: float = 0.0          # wall time of the step on this rank
     forward_ms: List[float] = field(default_factory=list)
     backward_ms: List[float] = field(default_factory=list)
 
 
-def schedule_actions(kind: str, m: int, n: int, j: int) -> List[Tuple[str, int]]:
-    """Ordered (F|B, micro-batch) actions of stage ``j`` of ``n`` for ``m`` micro-batches."""
+def schedule_actions(kind: str, m: int, n: int, j: int, virtual: int = 1) -> List[Tuple[str, int, int]]:
+    """Ordered (F|B, chunk, micro-batch) actions of rank ``j`` of ``n``.
+
+    ``gpipe``: breadth-first over the rank's ``virtual`` chunks (forward chunk
+    0..v-1, each over micro-batches 0..m-1; backward in exact reverse).  With
+    ``virtual == 1`` the chunk index is always 0 and callers may ignore it.
+    """
     if kind == "gpipe":
-        return [("F", i) for i in range(m)] + [("B", i) for i in reversed(range(m))]
+        fw = [("F", c, i) for c in range(virtual) for i in range(m)]
+        bw = [("B", c, i) for c in reversed(range(virtual)) for i in reversed(range(m))]
+        return fw + bw
     if kind == "1f1b":
+        if virtual != 1:
+            raise ValueError("1f1b supports one chunk per rank")
         warm = min(n - j - 1, m)
-        acts: List[Tuple[str, int]] = [("F", i) for i in range(warm)]
+        acts: List[Tuple[str, int, int]] = [("F", 0, i) for i in range(warm)]
         f, b = warm, 0
         while f < m:
-            acts.append(("F", f))
+            acts.append(("F", 0, f))
             f += 1
-            acts.append(("B", b))
+            acts.append(("B", 0, b))
             b += 1
         while b < m:
-            acts.append(("B", b))
+            acts.append(("B", 0, b))
             b += 1
         return acts
     raise ValueError(f"unknown schedule {kind!r}")
@@ -79,63 +99,92 @@ class _RNGState:
 
 
 class PipelineEngine:
-    """Runs one training (or eval) step of a pipeline stage.
+    """Runs one training (or eval) step of this rank's pipeline stage(s).
 
     Args:
-        module: this rank's stage (single tensor in, single tensor out).
+        module: this rank's stage, or a list of its ``virtual`` chunks in
+            virtual-stage order (chunk ``c`` is virtual stage ``c*n + rank``).
         chunks: micro-batches per mini-batch.
         checkpoint: ``always`` / ``except_last`` / ``never``.
-        act_shape: shape of the activation this stage RECEIVES per micro-batch
-            (gradient buffers take the shape of this stage's outputs).
+        act_shape: shape of the activation each chunk RECEIVES per micro-batch
+            (one shape, or one per chunk); gradient buffers take the shape of
+            the chunk's outputs.
         act_dtype: its dtype.
-        loss_fn: ``loss_fn(output, target) -> scalar`` on the last stage.
-        group: process group of the pipeline (default: WORLD).
-        schedule: ``gpipe`` (reference order) or ``1f1b``.
+        loss_fn: ``loss_fn(output, target) -> scalar`` on the last virtual stage.
+        group: process group of the pipeline (default: WORLD), or a ready
+            :class:`Channels`.
+        schedule: ``gpipe`` (reference order; looping when virtual > 1) or ``1f1b``.
     """
 
     def __init__(
         self,
-        module: nn.Module,
+        module: Union[nn.Module, Sequence[nn.Module]],
         *,
         chunks: int,
         checkpoint: str = "never",
-        act_shape: Sequence[int],
+        act_shape: Union[Sequence[int], Sequence[Sequence[int]]],
         act_dtype: torch.dtype,
         loss_fn: Optional[Callable[[Tensor, Tensor], Tensor]] = None,
-        group: Optional[dist.ProcessGroup] = None,
+        group: Union[None, dist.ProcessGroup, Channels] = None,
         device: Optional[torch.device] = None,
         schedule: str = "gpipe",
         measure: bool = False,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
             raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
-        self.module = module
+        mods = list(module) if isinstance(module, (list, tuple, nn.ModuleList)) else [module]
+        self.modules: List[nn.Module] = mods
+        self.virtual = len(mods)
+        self.module = mods[0] if self.virtual == 1 else nn.ModuleList(mods)
         self.chunks = int(chunks)
         self.checkpoint = checkpoint
-        self.act_shape = tuple(act_shape)
+        shapes = list(act_shape)
+        if shapes and isinstance(shapes[0], (list, tuple, torch.Size)):
+            self.act_shapes = [tuple(s) for s in shapes]
+        else:
+            self.act_shapes = [tuple(shapes)] * self.virtual
+        if len(self.act_shapes) != self.virtual:
+            raise ValueError("act_shape needs one shape per chunk")
+        self.act_shape = self.act_shapes[0]
         self.act_dtype = act_dtype
         self.loss_fn = loss_fn
         self.schedule = schedule
         self.measure = measure
-        if dist.is_available() and dist.is_initialized():
-            self.p2p: Optional[P2P] = P2P(group)
-            self.rank, self.world = self.p2p.rank, self.p2p.world
+        if schedule == "1f1b" and self.virtual > 1:
+            raise ValueError("1f1b supports one chunk per rank")
+        if isinstance(group, Channels):
+            self.chan: Optional[Channels] = group
+        elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+            self.chan = Channels(ranks, wrap=self.virtual > 1)
+            self.chan.warmup(device or next(mods[0].parameters()).device)
         else:
-            self.p2p = None
+            self.chan = None
+        if self.chan is not None:
+            self.rank, self.world = self.chan.rank, self.chan.world
+        else:
             self.rank, self.world = 0, 1
-        if schedule != "gpipe" and self.world > 1:
-            # 1F1B interleaves activation sends with gradient receives on the same
-            # link; without grouped send/recv that deadlocks on RCCL rendezvous.
-            raise NotImplementedError("multi-rank schedule '1f1b' is not supported yet; use 'gpipe'")
-        self.device = device or next(module.parameters()).device
+            if self.virtual > 1:
+                raise ValueError("several chunks per rank need a multi-rank pipeline")
+        self.device = device or next(mods[0].parameters()).device
+        n, v = self.world, self.virtual
+        self.vstage = [c * n + self.rank for c in range(v)]
+        self.nvirtual = n * v
+        # kept for callers: rank-level first/last of the whole pipeline
         self.is_first = self.rank == 0
-        self.is_last = self.rank == self.world - 1
+        self.is_last = self.rank == n - 1
 
     # ------------------------------------------------------------------ helpers
-    def _new_act(self, like: Optional[Tensor] = None) -> Tensor:
+    def _first(self, c: int) -> bool:
+        return self.vstage[c] == 0
+
+    def _last(self, c: int) -> bool:
+        return self.vstage[c] == self.nvirtual - 1
+
+    def _new_act(self, c: int, like: Optional[Tensor] = None) -> Tensor:
         if like is not None:
             return torch.empty(like.shape, dtype=like.dtype, device=self.device)
-        return torch.empty(self.act_shape, dtype=self.act_dtype, device=self.device)
+        return torch.empty(self.act_shapes[c], dtype=self.act_dtype, device=self.device)
 
     def _timer(self):
         if not self.measure or self.device.type != "cuda":
@@ -146,122 +195,131 @@ class PipelineEngine:
     def step(self, inputs: Optional[Sequence[Tensor]] = None, targets: Optional[Sequence[Tensor]] = None) -> StepStats:
         """Forward + backward of one mini-batch given as per-micro-batch lists.
 
-        ``inputs`` (first stage) and ``targets`` (last stage) have ``chunks``
-        entries.  Gradients accumulate into the parameters (or their
-        ``main_grad``); the caller runs the optimizer.  Returns the mean loss on
-        the last stage.
+        ``inputs`` (rank owning virtual stage 0) and ``targets`` (rank owning
+        the last virtual stage) have ``chunks`` entries.  Gradients accumulate
+        into the parameters (or their ``main_grad``); the caller runs the
+        optimizer.  Returns the mean loss on the last stage.
         """
-        m, n, j = self.chunks, self.world, self.rank
-        training = self.module.training and torch.is_grad_enabled()
-        stop = checkpoint_stop_for(self.checkpoint, m) if self.module.training else 0
+        m, v = self.chunks, self.virtual
+        training = self.modules[0].training and torch.is_grad_enabled()
+        stop = checkpoint_stop_for(self.checkpoint, m) if self.modules[0].training else 0
         stats = StepStats()
         t0 = time.perf_counter()
+        chan = self.chan
 
-        # Post every activation receive of the forward phase up front.
-        recv_x: List[Optional[Tensor]] = [None] * m
-        recv_w: List[Optional[dist.Work]] = [None] * m
-        if not self.is_first:
-            for i in range(m):
-                recv_x[i] = self._new_act()
-                recv_w[i] = self.p2p.irecv(recv_x[i], j - 1)
+        # Post every activation receive of the forward phase up front, in the
+        # order the upstream rank sends them (chunk-major, micro-batch minor).
+        recv_x = [[None] * m for _ in range(v)]
+        recv_w = [[None] * m for _ in range(v)]
+        for c in range(v):
+            if not self._first(c):
+                for i in range(m):
+                    recv_x[c][i] = self._new_act(c)
+                    recv_w[c][i] = chan.recv_act(recv_x[c][i])
 
-        stage_in: List[Optional[Tensor]] = [None] * m
-        stage_out: List[Optional[Tensor]] = [None] * m
-        rng: List[Optional[_RNGState]] = [None] * m
+        stage_in = [[None] * m for _ in range(v)]
+        stage_out = [[None] * m for _ in range(v)]
+        out_meta = [[None] * m for _ in range(v)]
+        rng = [[None] * m for _ in range(v)]
+        grad_w = [[None] * m for _ in range(v)]
+        grad_buf = [[None] * m for _ in range(v)]
         losses: List[Tensor] = []
-        sends: List[dist.Work] = []
-        grad_w: List[Optional[dist.Work]] = [None] * m
-        grad_buf: List[Optional[Tensor]] = [None] * m
+        sends = []
         events = []
 
-        def forward(i: int) -> None:
-            if self.is_first:
+        def forward(c: int, i: int) -> None:
+            mod = self.modules[c]
+            last = self._last(c)
+            if self._first(c):
                 x = inputs[i]
             else:
-                recv_w[i].wait()
-                x = recv_x[i]
-                recv_x[i] = None
+                recv_w[c][i].wait()
+                x = recv_x[c][i]
+                recv_x[c][i] = recv_w[c][i] = None
                 if training:
                     x.requires_grad_(True)
             tm = self._timer()
             if tm:
                 tm[0].record()
             if training and i < stop:
-                rng[i] = _RNGState(self.device)
+                rng[c][i] = _RNGState(self.device)
                 with torch.no_grad(), enable_checkpointing():
-                    y = self.module(x)
+                    y = mod(x)
             else:
-                y = self.module(x)
-            if self.is_last and self.loss_fn is not None:
+                y = mod(x)
+            if last and self.loss_fn is not None:
                 loss = self.loss_fn(y, targets[i])
                 losses.append(loss.detach())
                 y = loss / m  # backward seeds from the scaled loss
             if tm:
                 tm[1].record()
                 events.append(("F", tm))
-            stage_in[i] = x
-            stage_out[i] = y if (training and i >= stop) else None
-            out_meta[i] = torch.empty(y.shape, dtype=y.dtype, device="meta")
-            if not self.is_last:
-                sends.append(self.p2p.isend(y.detach(), j + 1))
+            stage_in[c][i] = x
+            stage_out[c][i] = y if (training and i >= stop) else None
+            out_meta[c][i] = torch.empty(y.shape, dtype=y.dtype, device="meta")
+            if not last:
+                sends.append(chan.send_act(y.detach()))
 
-        out_meta: List[Optional[Tensor]] = [None] * m
+        def post_grad_recv(c: int, i: int) -> None:
+            if not self._last(c) and grad_w[c][i] is None:
+                grad_buf[c][i] = self._new_act(c, out_meta[c][i])
+                grad_w[c][i] = chan.recv_grad(grad_buf[c][i])
 
-        def post_grad_recv(i: int) -> None:
-            if not self.is_last and grad_w[i] is None:
-                grad_buf[i] = self._new_act(out_meta[i])
-                grad_w[i] = self.p2p.irecv(grad_buf[i], j + 1)
-
-        def backward(i: int) -> None:
-            x = stage_in[i]
+        def backward(c: int, i: int) -> None:
+            mod = self.modules[c]
+            last = self._last(c)
+            x = stage_in[c][i]
             tm = self._timer()
-            if not self.is_last:
-                grad_w[i].wait()
+            if not last:
+                grad_w[c][i].wait()
             if tm:
                 tm[0].record()
-            if stage_out[i] is None:
+            if stage_out[c][i] is None:
                 # Recompute with the RNG state of the original forward.
-                st = rng[i]
+                st = rng[c][i]
                 devices = [self.device] if self.device.type == "cuda" else []
                 with torch.random.fork_rng(devices=devices):
                     torch.set_rng_state(st.cpu)
                     if st.dev is not None:
                         torch.cuda.set_rng_state(st.dev, self.device)
                     with torch.enable_grad(), enable_recomputing():
-                        y = self.module(x)
-                        if self.is_last and self.loss_fn is not None:
+                        y = mod(x)
+                        if last and self.loss_fn is not None:
                             y = self.loss_fn(y, targets[i]) / m
             else:
-                y = stage_out[i]
-            if self.is_last:
+                y = stage_out[c][i]
+            if last:
                 y.backward()
             else:
-                torch.autograd.backward(y, grad_buf[i])
+                torch.autograd.backward(y, grad_buf[c][i])
             if tm:
                 tm[1].record()
                 events.append(("B", tm))
-            stage_out[i] = None
-            grad_buf[i] = None
-            if not self.is_first:
-                sends.append(self.p2p.isend(x.grad, j - 1))
-            stage_in[i] = None
-            rng[i] = None
+            stage_out[c][i] = grad_buf[c][i] = grad_w[c][i] = None
+            if not self._first(c):
+                sends.append(chan.send_grad(x.grad))
+            stage_in[c][i] = rng[c][i] = None
 
-        actions = schedule_actions(self.schedule, m, n, j) if training else [("F", i) for i in range(m)]
+        if training:
+            actions = schedule_actions(self.schedule, m, self.world, self.rank, v)
+        else:
+            actions = [("F", c, i) for c in range(v) for i in range(m)]
         started_backward = False
-        for kind, i in actions:
+        for kind, c, i in actions:
             if kind == "F":
                 with torch.set_grad_enabled(training):
-                    forward(i)
+                    forward(c, i)
             else:
                 if not started_backward:
                     started_backward = True
-                    # Post all gradient receives of the drain phase at once.
                     if self.schedule == "gpipe":
-                        for k in reversed(range(m)):
-                            post_grad_recv(k)
-                post_grad_recv(i)
-                backward(i)
+                        # Post all gradient receives of the drain phase at once,
+                        # in the downstream rank's send order (reverse).
+                        for cc in reversed(range(v)):
+                            for k in reversed(range(m)):
+                                post_grad_recv(cc, k)
+                post_grad_recv(c, i)
+                backward(c, i)
 
         for w in sends:
             w.wait()

@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
-__all__ = ["P2P", "exchange_shape"]
+__all__ = ["P2P", "Channels", "exchange_shape"]
 
 
 class _HostStagedWork:
@@ -80,6 +80,92 @@ class P2P:
         m = meta.tolist()
         n = m[0]
         return m[2 : 2 + n], m[1]
+
+
+class Channels:
+    """One process group per DIRECTION of every pipeline link.
+
+    RCCL (like NCCL) gives each rank pair one communicator and one stream, and
+    runs that stream's sends and receives in issue order.  With activations
+    flowing one way and gradients the other -- and, for looping placements,
+    activations flowing back from the last rank to the first -- sharing that
+    stream would couple the two directions (a pre-posted receive would hold
+    back a send queued behind it).  A 2-rank group per direction gives every
+    direction its own communicator and stream, so the only ordering rule left
+    is per channel: the receiver posts in the order the sender sends.
+
+    For pipeline rank ``r`` of ``n``: ``act_out`` (r -> r+1), ``act_in``
+    (r-1 -> r), ``grad_out`` (r -> r-1), ``grad_in`` (r+1 -> r); indices mod n,
+    the wrap-around links (n-1 -> 0 for activations, 0 -> n-1 for gradients)
+    only exist when ``wrap`` (looping placement).  Every process of the default
+    group must construct Channels for every pipeline, in the same order
+    (``dist.new_group`` is collective).
+    """
+
+    def __init__(self, ranks: Sequence[int], wrap: bool = False) -> None:
+        self.ranks = list(ranks)  # global ranks of the pipeline, in stage order
+        n = len(self.ranks)
+        me = dist.get_rank()
+        self.rank = self.ranks.index(me) if me in self.ranks else -1
+        self.world = n
+        self.host_staged = dist.get_backend() == "gloo"
+        fwd, bwd = {}, {}
+        links = range(n) if wrap and n > 1 else range(n - 1)
+        for r in links:
+            a, b = self.ranks[r], self.ranks[(r + 1) % n]
+            fwd[r] = (dist.new_group([a, b]) if n > 1 else None, a, b)  # activations a -> b
+        for r in links:
+            a, b = self.ranks[r], self.ranks[(r + 1) % n]
+            bwd[r] = (dist.new_group([a, b]) if n > 1 else None, b, a)  # gradients b -> a
+        self._fwd, self._bwd = fwd, bwd
+
+    def warmup(self, device: torch.device) -> None:
+        """Creates every channel's communicator up front.
+
+        RCCL builds a pair's communicator lazily, host-blocking, on the first
+        send/recv.  A looping pipeline pre-posts rank 0's receive from rank
+        n-1 before rank 0 has computed anything, so a lazy init there would
+        wait on a send that can never happen.  Here every link does one tiny
+        blocking exchange, links visited in the same global order on every
+        rank (a chain of pairwise rendezvous: always deadlock-free)."""
+        dev = torch.device("cpu") if self.host_staged else device
+        me = dist.get_rank()
+        for table in (self._fwd, self._bwd):
+            for r in sorted(table):
+                group, src, dst = table[r]
+                if me == src:
+                    dist.send(torch.zeros(1, device=dev), dst, group=group)
+                elif me == dst:
+                    dist.recv(torch.zeros(1, device=dev), src, group=group)
+
+    def _link(self, table, r):
+        return table.get(r % self.world) if self.world > 1 else None
+
+    def _send(self, link, t: Tensor):
+        group, _, dst = link
+        if self.host_staged and t.device.type != "cpu":
+            host = t.detach().to("cpu")
+            return _HostStagedWork(dist.isend(host, dst, group=group), host)
+        return dist.isend(t.detach().contiguous(), dst, group=group)
+
+    def _recv(self, link, t: Tensor):
+        group, src, _ = link
+        if self.host_staged and t.device.type != "cpu":
+            host = torch.empty(t.shape, dtype=t.dtype)
+            return _HostStagedWork(dist.irecv(host, src, group=group), host, t)
+        return dist.irecv(t, src, group=group)
+
+    def send_act(self, t: Tensor):
+        return self._send(self._link(self._fwd, self.rank), t)
+
+    def recv_act(self, t: Tensor):
+        return self._recv(self._link(self._fwd, self.rank - 1), t)
+
+    def send_grad(self, t: Tensor):
+        return self._send(self._link(self._bwd, self.rank - 1), t)
+
+    def recv_grad(self, t: Tensor):
+        return self._recv(self._link(self._bwd, self.rank), t)
 
 
 _DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32]

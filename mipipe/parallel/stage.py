@@ -10,7 +10,7 @@ attention and MLP halves of a layer.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Tuple
+from typing import List, Sequence, Tuple
 
 import torch
 from torch import nn
@@ -19,24 +19,38 @@ from ..balance import balance_cost
 from ..models.lm import LMConfig, build_lm_blocks
 from ..models.transformer import merge_units, pipeline_units
 
-__all__ = ["StagePlan", "plan_stages", "block_costs", "stage_input_shape", "build_stage"]
+__all__ = ["StagePlan", "plan_stages", "block_costs", "stage_input_shape", "build_stage", "simulate_step", "choose_virtual"]
 
 
 @dataclass
 class StagePlan:
+    """Units per VIRTUAL stage (``len(balance) == ranks * virtual``); rank ``r``
+    owns virtual stages ``r, r + ranks, ...`` (looping placement)."""
+
     balance: List[int]
     costs: List[float]
+    virtual: int = 1
 
-    def slice(self, rank: int) -> range:
-        start = sum(self.balance[:rank])
-        return range(start, start + self.balance[rank])
+    @property
+    def ranks(self) -> int:
+        return len(self.balance) // self.virtual
 
-    def stage_cost(self, rank: int) -> float:
-        return sum(self.costs[i] for i in self.slice(rank))
+    def slice(self, vstage: int) -> range:
+        start = sum(self.balance[:vstage])
+        return range(start, start + self.balance[vstage])
+
+    def vstages(self, rank: int) -> List[int]:
+        return [c * self.ranks + rank for c in range(self.virtual)]
+
+    def stage_cost(self, vstage: int) -> float:
+        return sum(self.costs[i] for i in self.slice(vstage))
+
+    def rank_cost(self, rank: int) -> float:
+        return sum(self.stage_cost(s) for s in self.vstages(rank))
 
     def imbalance(self) -> float:
-        """max stage cost / mean stage cost (1.0 = perfect)."""
-        per = [self.stage_cost(r) for r in range(len(self.balance))]
+        """max rank cost / mean rank cost (1.0 = perfect)."""
+        per = [self.rank_cost(r) for r in range(self.ranks)]
         return max(per) / (sum(per) / len(per))
 
 
@@ -60,9 +74,151 @@ def block_costs(cfg: LMConfig) -> List[float]:
     return costs
 
 
-def plan_stages(cfg: LMConfig, stages: int) -> StagePlan:
+def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
+    """Contiguous split into ranks*virtual groups minimising the largest RANK
+    total (sum of its virtual stages), then the largest group: start from the
+    per-group min-max split and move single boundaries while that improves."""
+    groups = ranks * virtual
+    bal = balance_cost(costs, groups)
+
+    def score(b: List[int]) -> Tuple[float, float]:
+        gc, pos = [], 0
+        for k in b:
+            gc.append(sum(costs[pos:pos + k]))
+            pos += k
+        per_rank = [sum(gc[c * ranks + r] for c in range(virtual)) for r in range(ranks)]
+        return max(per_rank), max(gc)
+
+    def descend(b: List[int]) -> Tuple[Tuple[float, float], List[int]]:
+        best = score(b)
+        improved = True
+        while improved:  # coordinate descent: each boundary over its whole feasible range
+            improved = False
+            for g in range(groups - 1):
+                pair = b[g] + b[g + 1]
+                for left in range(1, pair):
+                    if left == b[g]:
+                        continue
+                    t = list(b)
+                    t[g], t[g + 1] = left, pair - left
+                    sc = score(t)
+                    if sc < best:
+                        b, best, improved = t, sc, True
+        return best, b
+
+    # Deterministic restarts (every rank must derive the same plan): random
+    # kicks of the best split, each followed by coordinate descent.
+    import random
+
+    rnd = random.Random(0)
+    best, bal = descend(bal)
+    for _ in range(200):
+        t = list(bal)
+        for _ in range(3):
+            g = rnd.randrange(groups - 1)
+            d = rnd.choice((-2, -1, 1, 2))
+            if t[g] + d >= 1 and t[g + 1] - d >= 1:
+                t[g] += d
+                t[g + 1] -= d
+        sc, t = descend(t)
+        if sc < best:
+            best, bal = sc, t
+    return bal
+
+
+def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks: int,
+                  bwd_ratio: float = 2.0) -> Tuple[float, List[float]]:
+    """Event simulation of one synchronous step (breadth-first looping order,
+    as :class:`~mipipe.parallel.engine.PipelineEngine` runs it; transfers free).
+
+    ``stage_costs`` are per VIRTUAL stage forward+backward costs.  Returns the
+    makespan and per-rank busy time (bubble = 1 - mean busy / makespan)."""
+    nv = ranks * virtual
+    fwd = [c / (1.0 + bwd_ratio) for c in stage_costs]
+    bwd = [c * bwd_ratio / (1.0 + bwd_ratio) for c in stage_costs]
+    f_done = [[None] * chunks for _ in range(nv)]
+    b_done = [[None] * chunks for _ in range(nv)]
+    order = {r: [("F", c * ranks + r, i) for c in range(virtual) for i in range(chunks)]
+             + [("B", c * ranks + r, i) for c in reversed(range(virtual)) for i in reversed(range(chunks))]
+             for r in range(ranks)}
+    pos = [0] * ranks
+    clock = [0.0] * ranks
+    busy = [0.0] * ranks
+    remaining = sum(len(o) for o in order.values())
+    while remaining:
+        progressed = False
+        for r in range(ranks):
+            while pos[r] < len(order[r]):
+                kind, s, i = order[r][pos[r]]
+                if kind == "F":
+                    dep = 0.0 if s == 0 else f_done[s - 1][i]
+                    dur = fwd[s]
+                else:
+                    dep = f_done[s][i] if s == nv - 1 else b_done[s + 1][i]
+                    dur = bwd[s]
+                if dep is None:
+                    break
+                start = max(clock[r], dep)
+                clock[r] = start + dur
+                busy[r] += dur
+                (f_done if kind == "F" else b_done)[s][i] = clock[r]
+                pos[r] += 1
+                remaining -= 1
+                progressed = True
+        if not progressed:
+            raise RuntimeError("schedule deadlock in simulation")
+    return max(clock), busy
+
+
+def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int, start: List[int]) -> List[int]:
+    """Coordinate descent on the simulated step time (:func:`simulate_step`)."""
+    groups = ranks * virtual
+
+    def score(b: List[int]) -> float:
+        gc, pos = [], 0
+        for k in b:
+            gc.append(sum(costs[pos:pos + k]))
+            pos += k
+        return simulate_step(gc, ranks, virtual, chunks)[0]
+
+    bal, best = list(start), score(start)
+    improved = True
+    while improved:
+        improved = False
+        for g in range(groups - 1):
+            pair = bal[g] + bal[g + 1]
+            for left in range(1, pair):
+                if left == bal[g]:
+                    continue
+                t = list(bal)
+                t[g], t[g + 1] = left, pair - left
+                sc = score(t)
+                if sc < best * (1 - 1e-9):
+                    bal, best, improved = t, sc, True
+    return bal
+
+
+def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0) -> StagePlan:
+    """Plan for ``stages`` ranks with ``virtual`` chunks each (looping placement).
+
+    With ``virtual > 1`` the split starts from the rank-total-balanced one and
+    is refined against the simulated step time for ``chunks`` micro-batches
+    (default 4 x stages): a chunk far larger than its neighbours stalls the
+    micro-batch flow even when rank totals are even."""
     costs = block_costs(cfg)
-    return StagePlan(balance_cost(costs, stages), costs)
+    if stages * virtual > len(costs):
+        raise ValueError(f"{stages} x {virtual} virtual stages exceed the {len(costs)} pipeline units")
+    if virtual == 1:
+        return StagePlan(balance_cost(costs, stages), costs)
+    m = chunks or 4 * stages
+    best = None
+    for start in (balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)):
+        bal = _makespan_refined(costs, stages, virtual, m, start)
+        plan = StagePlan(bal, costs, virtual)
+        t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m)[0]
+        if best is None or t < best[0]:
+            best = (t, plan)
+    return best[1]
 
 
 def unit_is_packed_core(cfg: LMConfig, index: int) -> bool:
@@ -70,23 +226,23 @@ def unit_is_packed_core(cfg: LMConfig, index: int) -> bool:
     return 1 <= index <= 3 * cfg.num_layers and (index - 1) % 3 == 0
 
 
-def stage_input_shape(cfg: LMConfig, plan: StagePlan, rank: int, micro_batch: int) -> Tuple[int, ...]:
-    """Shape of the activation stage ``rank`` receives (``[2, mb, S, E]`` after a
-    packed attention core, else ``[mb, S, E]``)."""
+def stage_input_shape(cfg: LMConfig, plan: StagePlan, vstage: int, micro_batch: int) -> Tuple[int, ...]:
+    """Shape of the activation virtual stage ``vstage`` receives (``[2, mb, S, E]``
+    after a packed attention core, else ``[mb, S, E]``)."""
     base = (micro_batch, cfg.seq_len, cfg.d_model)
-    if rank == 0:
+    if vstage == 0:
         return base
-    prev = plan.slice(rank).start - 1
+    prev = plan.slice(vstage).start - 1
     return (2,) + base if unit_is_packed_core(cfg, prev) else base
 
 
-def build_stage(cfg: LMConfig, plan: StagePlan, rank: int, *, device, dtype) -> nn.Sequential:
-    """Instantiates ONLY this rank's units (on ``device``, in ``dtype``) and
-    merges attention halves that ended up on the same stage."""
+def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -> nn.Sequential:
+    """Instantiates ONLY this virtual stage's units (on ``device``, in ``dtype``)
+    and merges attention halves that ended up on the same stage."""
     with torch.device("meta"):
         proto = pipeline_units(build_lm_blocks(cfg))
     units = []
-    for idx in plan.slice(rank):
+    for idx in plan.slice(vstage):
         u = proto[idx].to_empty(device=device)
         u.reset_parameters()
         units.append(u)
@@ -96,3 +252,16 @@ def build_stage(cfg: LMConfig, plan: StagePlan, rank: int, *, device, dtype) -> 
         if p.dtype.is_floating_point:
             p.data = p.data.to(dtype)
     return stage
+
+
+def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence[int] = (1, 2, 3)) -> Tuple[int, StagePlan]:
+    """Chunks per rank with the shortest simulated step (ties -> fewer chunks)."""
+    best = None
+    for v in candidates:
+        if stages * v > len(block_costs(cfg)) or (v > 1 and stages == 1):
+            continue
+        plan = plan_stages(cfg, stages, v, chunks)
+        t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks)
+        if best is None or t < best[0] * 0.995:
+            best = (t, v, plan)
+    return best[1], best[2]

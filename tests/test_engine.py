@@ -21,16 +21,54 @@ from mipipe.models.transformer import merge_units, pipeline_units
 from mipipe.parallel.stage import block_costs, stage_input_shape
 
 
+def _pairs(acts):
+    return [(k, i) for k, c, i in acts]
+
+
 def test_schedule_actions():
-    assert schedule_actions("gpipe", 3, 2, 0) == [("F", 0), ("F", 1), ("F", 2), ("B", 2), ("B", 1), ("B", 0)]
-    a = schedule_actions("1f1b", 4, 2, 0)
+    assert _pairs(schedule_actions("gpipe", 3, 2, 0)) == [("F", 0), ("F", 1), ("F", 2), ("B", 2), ("B", 1), ("B", 0)]
+    a = _pairs(schedule_actions("1f1b", 4, 2, 0))
     assert a == [("F", 0), ("F", 1), ("B", 0), ("F", 2), ("B", 1), ("F", 3), ("B", 2), ("B", 3)]
-    last = schedule_actions("1f1b", 4, 2, 1)
+    last = _pairs(schedule_actions("1f1b", 4, 2, 1))
     assert last == [("F", 0), ("B", 0), ("F", 1), ("B", 1), ("F", 2), ("B", 2), ("F", 3), ("B", 3)]
     for kind in ("gpipe", "1f1b"):
         for j in range(3):
-            acts = schedule_actions(kind, 5, 3, j)
+            acts = _pairs(schedule_actions(kind, 5, 3, j))
             assert sorted(acts) == sorted([("F", i) for i in range(5)] + [("B", i) for i in range(5)])
+    # looping: breadth-first over chunks, backward in exact reverse
+    lp = schedule_actions("gpipe", 2, 2, 1, virtual=2)
+    assert lp == [("F", 0, 0), ("F", 0, 1), ("F", 1, 0), ("F", 1, 1),
+                  ("B", 1, 1), ("B", 1, 0), ("B", 0, 1), ("B", 0, 0)]
+    with pytest.raises(ValueError):
+        schedule_actions("1f1b", 2, 2, 0, virtual=2)
+
+
+def test_simulated_bubble_matches_gpipe_formula():
+    from mipipe.parallel.stage import simulate_step
+
+    for n, m in ((2, 4), (4, 16), (8, 32)):
+        t, busy = simulate_step([1.0] * n, n, 1, m)
+        bubble = 1 - sum(busy) / len(busy) / t
+        assert abs(bubble - (n - 1) / (m + n - 1)) < 1e-9
+        # looping with v chunks: fill/drain shrink by v
+        v = 2
+        t, busy = simulate_step([0.5] * (n * v), n, v, m)
+        bubble = 1 - sum(busy) / len(busy) / t
+        assert abs(bubble - (n - 1) / (v * m + n - 1)) < 1e-9
+
+
+def test_looping_plans():
+    from mipipe.parallel.stage import choose_virtual
+
+    cfg = CONFIGS["enc12_d4096"]
+    p = plan_stages(cfg, 4, 2)
+    assert len(p.balance) == 8 and p.virtual == 2 and p.ranks == 4
+    assert p.vstages(1) == [1, 5]
+    assert sum(p.balance) == len(block_costs(cfg))
+    v, plan = choose_virtual(cfg, 2, 8)
+    assert v >= 2 and plan.virtual == v  # looping wins at PP=2
+    v1, _ = choose_virtual(cfg, 1, 4)
+    assert v1 == 1
 
 
 def test_plan_stages_balance():
@@ -118,7 +156,7 @@ def _gpu_cfg():
                                dim_feedforward=512, vocab=512, seq_len=64)
 
 
-def _worker(rank, world, port, checkpoint, q, gpu=False):
+def _worker(rank, world, port, checkpoint, q, gpu=False, virtual=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -130,12 +168,13 @@ def _worker(rank, world, port, checkpoint, q, gpu=False):
         full = torch.nn.Sequential(*build_lm_blocks(cfg))
         names = {id(p): n for n, p in full.named_parameters()}
         units = pipeline_units(list(full.children()))
-        plan = plan_stages(cfg, world)
-        stage = torch.nn.Sequential(*merge_units([units[i] for i in plan.slice(rank)])).train()
-        stage = stage.to(device, dtype)
+        plan = plan_stages(cfg, world, virtual)
+        chunks = [torch.nn.Sequential(*merge_units([units[i] for i in plan.slice(s)])).train().to(device, dtype)
+                  for s in plan.vstages(rank)]
+        stage = torch.nn.ModuleList(chunks)
         opt = FlatAdam(stage.parameters(), lr=1e-3, max_grad_norm=0.5)
-        eng = PipelineEngine(stage, chunks=m, checkpoint=checkpoint,
-                             act_shape=stage_input_shape(cfg, plan, rank, mb),
+        eng = PipelineEngine(chunks, chunks=m, checkpoint=checkpoint,
+                             act_shape=[stage_input_shape(cfg, plan, s, mb) for s in plan.vstages(rank)],
                              act_dtype=dtype, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
                              device=device)
         inputs, targets = _data(cfg, m, mb)
@@ -144,7 +183,9 @@ def _worker(rank, world, port, checkpoint, q, gpu=False):
         opt.zero_grad()
         st = eng.step(inputs if rank == 0 else None, targets if rank == world - 1 else None)
         opt.fold_grads()
-        grads = {names[id(p)]: p.main_grad.float().cpu().clone() for p in stage.parameters()}
+        # numpy: pickled by value (a torch tensor would be shared by fd, which
+        # dies with this process)
+        grads = {names[id(p)]: p.main_grad.float().cpu().numpy().copy() for p in stage.parameters()}
         sq = opt.grad_sumsq().cpu()
         dist.all_reduce(sq)
         q.put((rank, None if st.loss is None else float(st.loss), grads, float(sq)))
@@ -152,8 +193,9 @@ def _worker(rank, world, port, checkpoint, q, gpu=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("checkpoint", ["never", "except_last"])
-def test_engine_two_ranks_gloo(checkpoint):
+@pytest.mark.parametrize("checkpoint,world,virtual", [("never", 2, 1), ("except_last", 2, 1), ("never", 2, 2),
+                                                      ("always", 2, 3), ("except_last", 3, 2)])
+def test_engine_multi_rank_gloo(checkpoint, world, virtual):
     cfg = _tiny()
     m, mb = 4, 2
     ref, ref_loss = _reference(cfg, m, mb)
@@ -161,10 +203,10 @@ def test_engine_two_ranks_gloo(checkpoint):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, checkpoint, q, False, virtual)) for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=120) for _ in range(2)]
+    results = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -174,7 +216,7 @@ def test_engine_two_ranks_gloo(checkpoint):
         if loss is not None:
             assert abs(loss - ref_loss) < 1e-5
         for name, g in grads.items():
-            assert torch.allclose(g, ref_params[name].grad, atol=1e-5), name
+            assert torch.allclose(torch.from_numpy(g), ref_params[name].grad, atol=1e-5), name
             seen.add(name)
         total_sq = sq
     assert seen == set(ref_params)
@@ -183,8 +225,8 @@ def test_engine_two_ranks_gloo(checkpoint):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("checkpoint", ["never", "always"])
-def test_engine_two_ranks_share_gpu(checkpoint):
+@pytest.mark.parametrize("checkpoint,virtual", [("never", 1), ("always", 1), ("except_last", 2)])
+def test_engine_two_ranks_share_gpu(checkpoint, virtual):
     """Two pipeline ranks on one MI355X (gloo, host-staged boundaries): the HIP
     kernels of both stages and the multi-rank schedule against the single-rank
     engine on the whole model (same bf16 kernels, same initial weights)."""
@@ -206,7 +248,7 @@ def test_engine_two_ranks_share_gpu(checkpoint):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q, True)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q, True, virtual)) for r in range(2)]
     for p in procs:
         p.start()
     results = [q.get(timeout=300) for _ in range(2)]
@@ -218,6 +260,7 @@ def test_engine_two_ranks_share_gpu(checkpoint):
         if loss is not None:
             assert abs(loss - ref_loss) < 2e-3 * abs(ref_loss)
         for name, g in grads.items():
+            g = torch.from_numpy(g)
             scale = ref[name].abs().max().item() + 1e-6
             assert (g - ref[name]).abs().max().item() < 2e-2 * scale, name
             seen.add(name)
