@@ -113,7 +113,8 @@ def main() -> int:
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
                             act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device)
-    sim_t, sim_busy = simulate_step([plan.stage_cost(g) for g in range(pp * virtual)], pp, virtual, m)
+    sim_t, sim_busy = simulate_step([plan.stage_cost(g) for g in range(pp * virtual)], pp, virtual, m,
+                                    deferred_w=0.5)
 
     g = torch.Generator(device="cpu").manual_seed(0)
     tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)

@@ -437,6 +437,41 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad) {
   gemm_bf16(g, cur_stream(dy));
 }
 
+// Deferred weight gradient over the micro-batches of a step:
+//   main_grad[N, K] += sum_i dy_i^T . x_i
+// as K-segmented GEMMs (up to GemmArgs::kMaxSegs micro-batches per launch),
+// so the fp32 read-modify-write of main_grad happens once per launch instead
+// of once per micro-batch and K is long enough to amortise the tile prologue.
+void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, Tensor main_grad) {
+  MP_CHECK(!dys.empty() && dys.size() == xs.size(), "linear_wgrad_segments: need matching non-empty lists");
+  check_cuda(main_grad, "main_grad");
+  const int64_t T = dys[0].size(0), N = dys[0].size(1), K = xs[0].size(1);
+  MP_CHECK(main_grad.scalar_type() == at::kFloat && main_grad.numel() == N * K, "linear_wgrad_segments: bad main_grad");
+  for (size_t i = 0; i < dys.size(); ++i) {
+    check_bf16_2d(dys[i], "dy");
+    check_bf16_2d(xs[i], "x");
+    MP_CHECK(dys[i].size(0) == T && dys[i].size(1) == N && xs[i].size(0) == T && xs[i].size(1) == K,
+             "linear_wgrad_segments: every micro-batch needs the same [T, N] / [T, K] shapes");
+  }
+  MP_CHECK(T % 64 == 0 && gemm_supported(N, K, T), "linear_wgrad_segments: unsupported shape");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(main_grad.device());
+  const int total = (int)dys.size();
+  for (int first = 0; first < total; first += GemmArgs::kMaxSegs) {
+    const int n = std::min(GemmArgs::kMaxSegs, total - first);
+    GemmArgs g;
+    g.C = main_grad.data_ptr();
+    g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)(T * n);
+    g.a_kc = false; g.b_kc = false; g.epi = kEpiAccumF32;
+    g.seg_k = (int)T;
+    for (int i = 0; i < n; ++i) {
+      g.a_seg[i] = dys[first + i].data_ptr();
+      g.b_seg[i] = xs[first + i].data_ptr();
+    }
+    g.A = g.a_seg[0]; g.B = g.b_seg[0];
+    gemm_bf16(g, cur_stream(main_grad));
+  }
+}
+
 // Generic test entry: C[M,N] (fp32) = A . B with A given [M,K] (a_kc) or [K,M],
 // B given [N,K] (b_kc) or [K,N].
 Tensor py_gemm_f32(Tensor a, Tensor b, bool a_kc, bool b_kc) {
@@ -600,6 +635,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_fwd", &py_linear_fwd);
   m.def("linear_dgrad", &py_linear_dgrad);
   m.def("linear_wgrad", &py_linear_wgrad);
+  m.def("linear_wgrad_segments", &py_linear_wgrad_segments);
   m.def("gemm_f32", &py_gemm_f32);
   m.def("sumsq", &py_sumsq);
   m.def("adam_step", &py_adam);

@@ -279,6 +279,17 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t l
   }
 }
 
+// Operand base and local k of K-tile k0 (K-segmented operands, GemmArgs::seg_k).
+__device__ __forceinline__ const bf16_t* seg_base(const GemmArgs& g, bool is_a, int k0, int& kl) {
+  if (g.seg_k == 0) {
+    kl = k0;
+    return reinterpret_cast<const bf16_t*>(is_a ? g.A : g.B);
+  }
+  const int s = k0 / g.seg_k;
+  kl = k0 - s * g.seg_k;
+  return reinterpret_cast<const bf16_t*>(is_a ? g.a_seg[s] : g.b_seg[s]);
+}
+
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane) {
   if (KC) {
@@ -326,9 +337,6 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   int tm, tn;
   tile_coords((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const bf16_t* A = reinterpret_cast<const bf16_t*>(g.A);
-  const bf16_t* B = reinterpret_cast<const bf16_t*>(g.B);
-
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -336,8 +344,13 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BK;
-  stage<A_KC>(A, g.lda, m0, 0, g.M, smem, wave, lane);
-  stage<B_KC>(B, g.ldb, n0, 0, g.N, smem + kTileBytes, wave, lane);
+  {
+    int kl;
+    const bf16_t* A = seg_base(g, true, 0, kl);
+    stage<A_KC>(A, g.lda, m0, kl, g.M, smem, wave, lane);
+    const bf16_t* B = seg_base(g, false, 0, kl);
+    stage<B_KC>(B, g.ldb, n0, kl, g.N, smem + kTileBytes, wave, lane);
+  }
 
   if constexpr (PP) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -366,8 +379,16 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
             for (int s = 0; s < 2; ++s)
               bf[qn][jj][s] = frag<B_KC>(cur + kTileBytes, wn * 64 + qn * 32 + 16 * jj, s, lane);
         }
-        if (ph == 0 && more) stage<A_KC>(A, g.lda, m0, (u + 1) * BK, g.M, nxt, wave, lane);
-        if (ph == 1 && more) stage<B_KC>(B, g.ldb, n0, (u + 1) * BK, g.N, nxt + kTileBytes, wave, lane);
+        if (ph == 0 && more) {
+          int kl;
+          const bf16_t* A = seg_base(g, true, (u + 1) * BK, kl);
+          stage<A_KC>(A, g.lda, m0, kl, g.M, nxt, wave, lane);
+        }
+        if (ph == 1 && more) {
+          int kl;
+          const bf16_t* B = seg_base(g, false, (u + 1) * BK, kl);
+          stage<B_KC>(B, g.ldb, n0, kl, g.N, nxt + kTileBytes, wave, lane);
+        }
         if (ph == 3 && wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -399,8 +420,11 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     __syncthreads();
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * kBufBytes;
-      stage<A_KC>(A, g.lda, m0, (kt + 1) * BK, g.M, nxt, wave, lane);
-      stage<B_KC>(B, g.ldb, n0, (kt + 1) * BK, g.N, nxt + kTileBytes, wave, lane);
+      int kl;
+      const bf16_t* A = seg_base(g, true, (kt + 1) * BK, kl);
+      stage<A_KC>(A, g.lda, m0, kl, g.M, nxt, wave, lane);
+      const bf16_t* B = seg_base(g, false, (kt + 1) * BK, kl);
+      stage<B_KC>(B, g.ldb, n0, kl, g.N, nxt + kTileBytes, wave, lane);
     }
     const char* cur = smem + (kt & 1) * kBufBytes;
 #pragma unroll
@@ -530,7 +554,9 @@ int big_tiles(const GemmArgs& g) { return ((g.M + big::BM - 1) / big::BM) * ((g.
 // The 256x256 kernel handles every shape (edge tiles masked); the 128x128 one
 // only exact multiples of 128, where it is kept for grids too small to fill
 // the 256 CUs with 256x256 tiles.
-bool use_big(const GemmArgs& g) { return g.M % BM != 0 || g.N % BN != 0 || big_tiles(g) >= 128; }
+bool use_big(const GemmArgs& g) {
+  return g.seg_k > 0 || g.M % BM != 0 || g.N % BN != 0 || big_tiles(g) >= 128;
+}
 
 template <bool A_KC, bool B_KC, int EPI, int ACT>
 void launch(const GemmArgs& g, hipStream_t s) {

@@ -90,6 +90,14 @@ struct GemmArgs {
   float p = 0.f;
   uint32_t threshold = 0;
   uint64_t seed = 0, offset = 0;
+  // K-segmented operands (deferred weight gradients: one GEMM over the
+  // micro-batches of a step without concatenating them).  seg_k > 0: K-rows
+  // [s*seg_k, (s+1)*seg_k) of A / B live at a_seg[s] / b_seg[s] (leading
+  // dimensions lda / ldb); seg_k must be a multiple of 64.
+  static constexpr int kMaxSegs = 16;
+  int seg_k = 0;
+  const void* a_seg[kMaxSegs] = {};
+  const void* b_seg[kMaxSegs] = {};
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 // Main-loop schedule of the 256x256 GEMM: 1 = ping-pong wave groups (default), 0 = one barrier per K-tile.

@@ -6,7 +6,7 @@ CPU tensors (plumbing tests).  GPU tensors never fall back to eager PyTorch:
 a missing extension raises (``mipipe._native_loader.kernels``).
 """
 from .layernorm import add_dropout_layer_norm, layer_norm_reference
-from .linear import linear
+from .linear import deferred_wgrad, flush_wgrad, linear
 from .attention import attention, attention_packed, attention_reference
 from .activation import bias_act_dropout
 from .loss import cross_entropy
@@ -16,6 +16,8 @@ __all__ = [
     "add_dropout_layer_norm",
     "layer_norm_reference",
     "linear",
+    "deferred_wgrad",
+    "flush_wgrad",
     "attention",
     "attention_packed",
     "attention_reference",

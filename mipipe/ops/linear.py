@@ -25,7 +25,7 @@ from torch import Tensor
 from ._util import native_or_none
 from .activation import ACTIVATIONS, bias_act_reference
 
-__all__ = ["linear"]
+__all__ = ["linear", "deferred_wgrad", "flush_wgrad"]
 
 
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
@@ -98,13 +98,71 @@ class _Linear(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             main = getattr(w, "main_grad", None)
-            if main is not None and ctx.fused_tile:
+            if main is not None and ctx.fused_tile and _DEFERRED is not None:
+                _defer(w, dpre, x2)
+            elif main is not None and ctx.fused_tile:
                 k.linear_wgrad(dpre, x2, main)
             elif main is not None:
                 main.add_(torch.matmul(dpre.t(), x2).float())
             else:
                 dw = torch.matmul(dpre.t(), x2)
         return dx, dw, db, None, None
+
+
+# ---------------------------------------------------------------- deferred wgrad
+# Zero-bubble style split of the linear backward: inside ``deferred_wgrad()``
+# the backward computes only dX (and the bias gradient) -- what the upstream
+# pipeline stage waits for -- and queues (dY, X) per weight; ``flush_wgrad()``
+# then runs ONE K-segmented GEMM per weight over all queued micro-batches
+# (``linear_wgrad_segments``).  A pipeline rank thereby sends its input
+# gradients (n-1) weight-gradient times earlier in the drain, and the fp32
+# main_grad read-modify-write happens once per step instead of once per
+# micro-batch.  Module-level (not thread-local): autograd runs backward on its
+# own device threads.
+_DEFERRED: Optional[dict] = None
+
+
+def _defer(w: Tensor, dy: Tensor, x: Tensor) -> None:
+    entry = _DEFERRED.setdefault(id(w), (w, [], []))
+    entry[1].append(dy)
+    entry[2].append(x)
+
+
+def flush_wgrad() -> None:
+    """Runs every queued weight-gradient GEMM (accumulating into main_grad)."""
+    global _DEFERRED
+    if not _DEFERRED:
+        return
+    queue, _DEFERRED = _DEFERRED, {}
+    for w, dys, xs in queue.values():
+        k = native_or_none(dys[0])
+        T = dys[0].shape[0]
+        uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
+        if uniform and T % 64 == 0:
+            k.linear_wgrad_segments(dys, xs, w.main_grad)
+        else:
+            for d, x in zip(dys, xs):
+                k.linear_wgrad(d, x, w.main_grad)
+
+
+class deferred_wgrad:
+    """Context: queue weight gradients of tile-path linears; flush on exit."""
+
+    def __enter__(self):
+        global _DEFERRED
+        if _DEFERRED is not None:
+            raise RuntimeError("deferred_wgrad() does not nest")
+        _DEFERRED = {}
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFERRED
+        try:
+            if exc[0] is None:
+                flush_wgrad()
+        finally:
+            _DEFERRED = None
+        return False
 
 
 def linear(

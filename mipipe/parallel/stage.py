@@ -127,15 +127,20 @@ def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
 
 
 def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks: int,
-                  bwd_ratio: float = 2.0) -> Tuple[float, List[float]]:
+                  bwd_ratio: float = 2.0, deferred_w: float = 0.0) -> Tuple[float, List[float]]:
     """Event simulation of one synchronous step (breadth-first looping order,
     as :class:`~mipipe.parallel.engine.PipelineEngine` runs it; transfers free).
 
-    ``stage_costs`` are per VIRTUAL stage forward+backward costs.  Returns the
-    makespan and per-rank busy time (bubble = 1 - mean busy / makespan)."""
+    ``stage_costs`` are per VIRTUAL stage forward+backward costs; backward is
+    ``bwd_ratio`` x forward, of which the fraction ``deferred_w`` (weight
+    gradients under ``defer_wgrad``) runs after the rank's last backward.
+    Returns the makespan and per-rank busy time (bubble = 1 - mean busy /
+    makespan)."""
     nv = ranks * virtual
     fwd = [c / (1.0 + bwd_ratio) for c in stage_costs]
-    bwd = [c * bwd_ratio / (1.0 + bwd_ratio) for c in stage_costs]
+    bwd_all = [c * bwd_ratio / (1.0 + bwd_ratio) for c in stage_costs]
+    bwd = [b * (1.0 - deferred_w) for b in bwd_all]
+    wgt = [b * deferred_w for b in bwd_all]
     f_done = [[None] * chunks for _ in range(nv)]
     b_done = [[None] * chunks for _ in range(nv)]
     order = {r: [("F", c * ranks + r, i) for c in range(virtual) for i in range(chunks)]
@@ -145,6 +150,10 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
     clock = [0.0] * ranks
     busy = [0.0] * ranks
     remaining = sum(len(o) for o in order.values())
+    # deferred weight gradients: after the rank's last backward, no dependencies
+    for r in range(ranks):
+        order[r] += [("W", c * ranks + r, i) for c in range(virtual) for i in range(chunks)] if deferred_w else []
+    remaining = sum(len(o) for o in order.values())
     while remaining:
         progressed = False
         for r in range(ranks):
@@ -153,6 +162,8 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
                 if kind == "F":
                     dep = 0.0 if s == 0 else f_done[s - 1][i]
                     dur = fwd[s]
+                elif kind == "W":
+                    dep, dur = 0.0, wgt[s]
                 else:
                     dep = f_done[s][i] if s == nv - 1 else b_done[s + 1][i]
                     dur = bwd[s]
@@ -161,13 +172,19 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
                 start = max(clock[r], dep)
                 clock[r] = start + dur
                 busy[r] += dur
-                (f_done if kind == "F" else b_done)[s][i] = clock[r]
+                if kind != "W":
+                    (f_done if kind == "F" else b_done)[s][i] = clock[r]
                 pos[r] += 1
                 remaining -= 1
                 progressed = True
         if not progressed:
             raise RuntimeError("schedule deadlock in simulation")
     return max(clock), busy
+
+
+# Fraction of the backward that is weight-gradient GEMMs (deferred by the
+# engine's ``defer_wgrad``): wgrad FLOPs equal dgrad FLOPs for every linear.
+DEFERRED_W = 0.5
 
 
 def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int, start: List[int]) -> List[int]:
@@ -179,7 +196,7 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
         for k in b:
             gc.append(sum(costs[pos:pos + k]))
             pos += k
-        return simulate_step(gc, ranks, virtual, chunks)[0]
+        return simulate_step(gc, ranks, virtual, chunks, deferred_w=DEFERRED_W)[0]
 
     bal, best = list(start), score(start)
     improved = True
@@ -215,7 +232,8 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0) -
     for start in (balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)):
         bal = _makespan_refined(costs, stages, virtual, m, start)
         plan = StagePlan(bal, costs, virtual)
-        t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m)[0]
+        t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m,
+                          deferred_w=DEFERRED_W)[0]
         if best is None or t < best[0]:
             best = (t, plan)
     return best[1]
@@ -261,7 +279,8 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence
         if stages * v > len(block_costs(cfg)) or (v > 1 and stages == 1):
             continue
         plan = plan_stages(cfg, stages, v, chunks)
-        t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks)
+        t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks,
+                             deferred_w=DEFERRED_W)
         if best is None or t < best[0] * 0.995:
             best = (t, v, plan)
     return best[1], best[2]

@@ -266,3 +266,27 @@ def test_engine_two_ranks_share_gpu(checkpoint, virtual):
             seen.add(name)
         assert abs(sq - ref_sq) / ref_sq < 1e-2
     assert seen == set(ref)
+
+
+@pytest.mark.gpu
+def test_engine_deferred_wgrad_same_gradients():
+    """defer_wgrad (weight GEMMs after the last backward, K-segmented) gives the
+    gradients of the immediate path."""
+    cfg = _gpu_cfg()
+    m, mb = 4, 2
+    dev = torch.device("cuda", 0)
+    inputs, targets = _data(cfg, m, mb)
+    grads = {}
+    for defer in (False, True):
+        torch.manual_seed(0)
+        full = torch.nn.Sequential(*build_lm_blocks(cfg)).train().to(dev, torch.bfloat16)
+        opt = FlatAdam(full.parameters(), lr=1e-3)
+        eng = PipelineEngine(full, chunks=m, checkpoint="except_last", act_shape=(mb, cfg.seq_len),
+                             act_dtype=torch.bfloat16, loss_fn=_loss_fn(cfg), device=dev, defer_wgrad=defer)
+        opt.zero_grad()
+        eng.step([x.to(dev) for x in inputs], [t.to(dev) for t in targets])
+        opt.fold_grads()
+        grads[defer] = {n: p.main_grad.clone() for n, p in full.named_parameters()}
+    for n, g in grads[False].items():
+        scale = g.abs().max().item() + 1e-6
+        assert (grads[True][n] - g).abs().max().item() < 1e-2 * scale, n

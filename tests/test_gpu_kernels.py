@@ -388,6 +388,41 @@ def test_linear_edge_shapes_main_grad(k, T, K, N):
     assert rel(w.main_grad[-8:, -8:], wf.grad[-8:, -8:]) < 5e-2
 
 
+@pytest.mark.parametrize("nseg,T,N,K", [(4, 256, 512, 384), (20, 128, 264, 136), (3, 1024, 1600, 4800)])
+def test_wgrad_segments_matches_sum(k, nseg, T, N, K):
+    """K-segmented weight-gradient GEMM (deferred wgrad) == sum of per-micro-batch dY^T X."""
+    torch.manual_seed(5)
+    dys = [torch.randn(T, N, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    xs = [torch.randn(T, K, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    main = torch.randn(N, K, device=DEV)
+    expect = main.clone()
+    for d, x in zip(dys, xs):
+        expect += d.float().t() @ x.float()
+    k.linear_wgrad_segments(dys, xs, main)
+    err = ((main - expect).abs().max() / expect.abs().max()).item()
+    assert err < 1e-3, err
+
+
+def test_deferred_wgrad_op(k):
+    from mipipe import ops
+
+    torch.manual_seed(6)
+    w = (torch.randn(384, 256, device=DEV) / 16).to(torch.bfloat16).requires_grad_()
+    w.main_grad = torch.zeros(384, 256, device=DEV)
+    xs = [torch.randn(128, 256, device=DEV).to(torch.bfloat16) for _ in range(3)]
+    gs = [torch.randn(128, 384, device=DEV).to(torch.bfloat16) for _ in range(3)]
+    with ops.deferred_wgrad():
+        for x, g in zip(xs, gs):
+            ops.linear(x, w, None, "relu", 0.0, True).backward(g)
+        assert w.main_grad.abs().max().item() == 0.0  # nothing ran yet
+    expect = torch.zeros(384, 256, device=DEV)
+    for x, g in zip(xs, gs):
+        pre = x.float() @ w.detach().float().t()
+        expect += (g.float() * (pre > 0).float()).t() @ x.float()
+    err = ((w.main_grad - expect).abs().max() / expect.abs().max()).item()
+    assert err < 2e-2, err
+
+
 def test_linear_dropout_mask_and_main_grad(k):
     from mipipe.ops import linear
 
