@@ -486,10 +486,244 @@ __global__ void __launch_bounds__(kThreads, D >= 128 ? 1 : 2) attn_dkdv_kernel(A
     }
 }
 
+// ------------------------------------------------------------------ fused backward, S = 128
+// One 512-thread workgroup per (batch, head) computes dQ, dK and dV of the
+// whole 128-token sequence in one pass (the reference's bptt = 128 case):
+//   phase 1  S = Q K^T and dP = dO V^T for all 128 x 128 pairs, streamed over
+//            D in 64-wide chunks (K, V chunks double-buffered in LDS; Q, dO
+//            A-fragments straight from HBM); wave w owns query rows 16w..16w+15.
+//            P = exp(S - lse), dropout replayed from Philox, and
+//            delta_i = sum_j P~_ij dP_ij straight from registers (= rowsum(dO.O),
+//            so no O read and no delta pre-pass);
+//   phase 2  P~ and dS = P (dP~ - delta) go to two 128 x 128 bf16 LDS images;
+//            per 64-wide D chunk K, Q and dO chunks are staged and
+//            dQ = dS K, dK = dS^T Q, dV = P~^T dO come out of 48 MFMAs per wave
+//            (transposed operands via ds_read_b64_tr_b16).
+// vs. the general path (delta + dK/dV + dQ kernels) it reads Q, K, V, dO once
+// and recomputes S / dP once instead of twice.
+namespace shortseq {
+
+constexpr int S = 128;
+constexpr int kThreads = 512;      // 8 waves x 16 query rows
+constexpr int kChunk = 64;         // D chunk
+constexpr int kChunkImg = S * kChunk * 2;   // [128][64] bf16 = 16 KiB
+constexpr int kSqImg = S * S * 2;           // [128][128] bf16 = 32 KiB
+constexpr int kStageBytes = 3 * kChunkImg;  // phase 2: K, Q, dO chunks (48 KiB); phase 1 uses 4 chunk images
+constexpr int kPOff = 4 * kChunkImg;        // 64 KiB
+constexpr int kDsOff = kPOff + kSqImg;      // 96 KiB
+constexpr int kSmem = kDsOff + kSqImg;      // 128 KiB
+
+// [128][64] chunk image: Img<64> addressing (128-byte rows).
+__device__ __forceinline__ int coff(int r, int c16) { return Img<64>::off(r, c16); }
+// [128][128] image: Img<128> addressing (256-byte rows).
+__device__ __forceinline__ int soff(int r, int c16) { return Img<128>::off(r, c16); }
+
+// rows 0..127, columns [d0, d0 + 64) of a row-major matrix -> chunk image.
+// (two named registers, not an array: a loop-carried uint4[2] was kept in scratch)
+__device__ __forceinline__ void load_chunk(const bf16_t* __restrict__ base, int64_t ld, int d0, int tid, uint4& v0,
+                                           uint4& v1) {
+  const int r = tid >> 3, c = tid & 7;  // pieces tid and tid + 512 of 1024: rows r and r + 64
+  v0 = *reinterpret_cast<const uint4*>(base + (int64_t)r * ld + d0 + 8 * c);
+  v1 = *reinterpret_cast<const uint4*>(base + (int64_t)(r + 64) * ld + d0 + 8 * c);
+}
+__device__ __forceinline__ void store_chunk(char* img, int tid, const uint4& v0, const uint4& v1) {
+  const int r = tid >> 3, c = tid & 7;
+  *reinterpret_cast<uint4*>(img + coff(r, c)) = v0;
+  *reinterpret_cast<uint4*>(img + coff(r + 64, c)) = v1;
+}
+
+// B[k = d][n = row] from a chunk image (16 rows from rb, k-step s of 32).
+__device__ __forceinline__ bf16x8 crow(const char* img, int rb, int s, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + coff(rb + (lane & 15), 4 * s + (lane >> 4)));
+}
+// B[k = row][n = d] from a chunk image (rows 32 s.., columns db..db+15).
+__device__ __forceinline__ bf16x8 ccol(const char* img, int db, int s, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 32 * s + 8 * g + q;
+  const int c8 = (db >> 2) + p;
+  const int o0 = coff(r0, c8 >> 1) + 8 * (c8 & 1);
+  const int o1 = coff(r0 + 4, c8 >> 1) + 8 * (c8 & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// A[i = row][k = col] from a [128][128] image (rows rb.., k-step s of 32).
+__device__ __forceinline__ bf16x8 srow(const char* img, int rb, int s, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + soff(rb + (lane & 15), 4 * s + (lane >> 4)));
+}
+// A[i = col][k = row] from a [128][128] image (columns ib.., k-step s of 32 over rows).
+__device__ __forceinline__ bf16x8 scol(const char* img, int ib, int s, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 32 * s + 8 * g + q;
+  const int c8 = (ib >> 2) + p;
+  const int o0 = soff(r0, c8 >> 1) + 8 * (c8 & 1);
+  const int o1 = soff(r0 + 4, c8 >> 1) + 8 * (c8 & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 1) attn_bwd_s128_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t boff = (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + boff;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + boff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + boff;
+  const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+  constexpr int NC = D / kChunk;
+
+  // ---- phase 1: S and dP over D chunks ----
+  f32x4 sacc[8], pacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sacc[j] = pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int myrow = wave * 16 + (lane & 15);
+  const bf16_t* qrow = Q + (int64_t)myrow * a.ld_qkv;
+  const bf16_t* drow = dO + (int64_t)myrow * a.ld_o;
+
+  uint4 k0, k1, v0, v1;
+  load_chunk(K, a.ld_qkv, 0, tid, k0, k1);
+  load_chunk(V, a.ld_qkv, 0, tid, v0, v1);
+  store_chunk(smem, tid, k0, k1);
+  store_chunk(smem + kChunkImg, tid, v0, v1);
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const char* kimg = smem + (c & 1) * 2 * kChunkImg;
+    const char* vimg = kimg + kChunkImg;
+    if (c + 1 < NC) {  // prefetch the next chunk into registers (T14)
+      load_chunk(K, a.ld_qkv, (c + 1) * kChunk, tid, k0, k1);
+      load_chunk(V, a.ld_qkv, (c + 1) * kChunk, tid, v0, v1);
+    }
+    bf16x8 qf[2], df[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      qf[s2] = frag_global(qrow + c * kChunk, s2, lane);
+      df[s2] = frag_global(drow + c * kChunk, s2, lane);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s2], crow(kimg, 16 * j, s2, lane), sacc[j], 0, 0, 0);
+        pacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[s2], crow(vimg, 16 * j, s2, lane), pacc[j], 0, 0, 0);
+      }
+    if (c + 1 < NC) {
+      char* nimg = smem + ((c + 1) & 1) * 2 * kChunkImg;
+      store_chunk(nimg, tid, k0, k1);
+      store_chunk(nimg + kChunkImg, tid, v0, v1);
+    }
+    __syncthreads();
+  }
+
+  // ---- softmax, dropout replay, delta, dS ----
+  const int qrow0 = wave * 16 + 4 * (lane >> 4);  // this lane's rows qrow0 .. +3
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  float lse2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) lse2[r] = a.lse[(int64_t)bh * S + qrow0 + r] * kLog2e;
+  float dsum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int key = 16 * j + (lane & 15);
+    uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (a.p > 0.f) {
+      const uint4 mw = attn_mask_words(a, bh, qrow0 >> 2, key);
+      w[0] = mw.x; w[1] = mw.y; w[2] = mw.z; w[3] = mw.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pr = exp2f(sacc[j][r] * sl2 - lse2[r]);
+      if (CAUSAL && key > qrow0 + r) pr = 0.f;
+      float dp = pacc[j][r];
+      float pd = pr;
+      if (a.p > 0.f) {
+        const bool keep = w[r] >= a.threshold;
+        dp = keep ? dp * pscale : 0.f;
+        pd = keep ? pr * pscale : 0.f;
+      }
+      sacc[j][r] = pr;  // P (undropped)
+      pacc[j][r] = dp;  // dP~
+      dsum[r] += pr * dp;
+      // P~ into its image now (sacc is overwritten by dS below)
+      *reinterpret_cast<bf16_t*>(smem + kPOff + soff(qrow0 + r, key >> 3) + 2 * (key & 7)) = f2bf(pd);
+    }
+  }
+  float delta[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) delta[r] = row_reduce_sum16(dsum[r]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int key = 16 * j + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ds = sacc[j][r] * (pacc[j][r] - delta[r]);
+      *reinterpret_cast<bf16_t*>(smem + kDsOff + soff(qrow0 + r, key >> 3) + 2 * (key & 7)) = f2bf(ds);
+    }
+  }
+
+  // ---- phase 2: dQ = dS K, dK = dS^T Q, dV = P~^T dO per D chunk ----
+  const char* pimg = smem + kPOff;
+  const char* dsimg = smem + kDsOff;
+  char* kimg = smem;
+  char* qimg = smem + kChunkImg;
+  char* dimg = smem + 2 * kChunkImg;
+  bf16_t* dQ = reinterpret_cast<bf16_t*>(a.dq) + boff;
+  bf16_t* dK = reinterpret_cast<bf16_t*>(a.dk) + boff;
+  bf16_t* dV = reinterpret_cast<bf16_t*>(a.dv) + boff;
+  const int r0 = wave * 16;  // output rows (queries for dQ, keys for dK / dV)
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const int d0 = c * kChunk;
+    uint4 a0, a1, b0, b1, e0, e1;
+    load_chunk(K, a.ld_qkv, d0, tid, a0, a1);
+    load_chunk(Q, a.ld_qkv, d0, tid, b0, b1);
+    load_chunk(dO, a.ld_o, d0, tid, e0, e1);
+    __syncthreads();  // previous chunk's readers are done (and phase-1 images for c == 0)
+    store_chunk(kimg, tid, a0, a1);
+    store_chunk(qimg, tid, b0, b1);
+    store_chunk(dimg, tid, e0, e1);
+    __syncthreads();
+    f32x4 dq[4], dk[4], dv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dq[t] = dk[t] = dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 a_dq = srow(dsimg, r0, ks, lane);   // dS[q][key], k = key
+      const bf16x8 a_dk = scol(dsimg, r0, ks, lane);   // dS^T[key][q], k = q
+      const bf16x8 a_dv = scol(pimg, r0, ks, lane);    // P~^T[key][q], k = q
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dq[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_dq, ccol(kimg, 16 * t, ks, lane), dq[t], 0, 0, 0);
+        dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_dk, ccol(qimg, 16 * t, ks, lane), dk[t], 0, 0, 0);
+        dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_dv, ccol(dimg, 16 * t, ks, lane), dv[t], 0, 0, 0);
+      }
+    }
+    const int orow = r0 + 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t o = (int64_t)(orow + r) * a.ld_qkv + d0 + 16 * t + (lane & 15);
+        dQ[o] = f2bf(dq[t][r] * a.scale);
+        dK[o] = f2bf(dk[t][r] * a.scale);
+        dV[o] = f2bf(dv[t][r]);
+      }
+  }
+}
+
+}  // namespace shortseq
+
 template <int D>
 size_t fwd_smem() { return 2 * Img<D>::kBytes + 4 * 16 * kScrStride * 2; }
 template <int D>
 size_t dkdv_smem() { return fwd_smem<D>() + 128 * sizeof(float); }
+
+int g_attn_fused_bwd = 1;  // S == 128: fused single-pass backward (1) or the general kernels (0)
 
 template <typename Kern>
 void set_smem(Kern k, size_t bytes) {
@@ -513,6 +747,16 @@ void run_bwd(const AttnArgs& a, hipStream_t s) {
     set_smem(attn_dkdv_kernel<D, CAUSAL>, sm2);
     once = true;
   }
+  if (a.S == shortseq::S && g_attn_fused_bwd) {
+    static bool once_s = false;
+    if (!once_s) {
+      set_smem(shortseq::attn_bwd_s128_kernel<D, CAUSAL>, shortseq::kSmem);
+      once_s = true;
+    }
+    hipLaunchKernelGGL((shortseq::attn_bwd_s128_kernel<D, CAUSAL>), dim3(a.B * a.H), dim3(shortseq::kThreads),
+                       shortseq::kSmem, s, a);
+    return;
+  }
   const int64_t rows = (int64_t)a.B * a.S * a.H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, D);
   hipLaunchKernelGGL((attn_dkdv_kernel<D, CAUSAL>), dim3(a.S / kRows, a.B * a.H), dim3(kThreads), sm2, s, a);
@@ -520,6 +764,8 @@ void run_bwd(const AttnArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+void attention_set_fused_bwd(int on) { g_attn_fused_bwd = on; }
 
 bool attention_supported(int S, int D) { return S > 0 && S % kRows == 0 && (D == 64 || D == 128 || D == 256); }
 

@@ -127,6 +127,8 @@ struct AttnArgs {
   bool causal = false;
 };
 bool attention_supported(int S, int D);
+// S == 128 backward: fused one-pass kernel (1, default) or delta + dK/dV + dQ kernels (0).
+void attention_set_fused_bwd(int on);
 void attention_fwd(const AttnArgs& a, hipStream_t s);
 void attention_bwd(const AttnArgs& a, hipStream_t s);
 

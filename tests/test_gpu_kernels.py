@@ -496,11 +496,22 @@ def _ref_attention_masked(q, k, v, causal, keep, p, scale):
 @pytest.mark.parametrize("D", [64, 128, 256])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("p", [0.0, 0.25])
-def test_attention_packed(k, D, causal, p):
+@pytest.mark.parametrize("S,fused", [(128, 1), (128, 0), (256, 1)])
+def test_attention_packed(k, D, causal, p, S, fused):
+    """S = 128 runs the fused one-pass backward (fused=1) or the general
+    delta + dK/dV + dQ kernels (fused=0); S = 256 always the general ones."""
+    k.attention_set_fused_bwd(fused)
+    try:
+        _check_attention_packed(k, D, causal, p, S)
+    finally:
+        k.attention_set_fused_bwd(1)
+
+
+def _check_attention_packed(k, D, causal, p, S):
     from mipipe.ops import attention_packed
 
     torch.manual_seed(4)
-    B, S, H = 2, 128, 2
+    B, H = 2, 2
     qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16).requires_grad_()
     scale = 1.0 / math.sqrt(D)
     if p > 0:

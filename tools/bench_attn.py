@@ -1,0 +1,43 @@
+"""Attention kernel timing at the enc12 shape (B=32, S=128, H=16, D=256), fused vs general backward."""
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+from mipipe._native_loader import kernels  # noqa: E402
+
+k = kernels()
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts) * 1e3
+
+
+B, S, H, D = (int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (32, 128, 16, 256)))
+causal = len(sys.argv) > 5 and sys.argv[5] == "causal"
+qkv = torch.randn(B, S, 3, H, D, device="cuda").to(torch.bfloat16)
+q, kk, v = (qkv.select(2, i) for i in range(3))
+scale = D ** -0.5
+o, lse, seed, off = k.attention_fwd(q, kk, v, causal, 0.2, scale)
+dout = torch.randn_like(o)
+dq = torch.empty_like(qkv)
+f = timeit(lambda: k.attention_fwd(q, kk, v, causal, 0.2, scale))
+print(f"B={B} S={S} H={H} D={D} causal={causal}: fwd {f:.1f} us")
+for fused in (0, 1):
+    k.attention_set_fused_bwd(fused)
+    t = timeit(lambda: k.attention_bwd(dout, q, kk, v, o, lse, causal, 0.2, scale, seed, off,
+                                       dq.select(2, 0), dq.select(2, 1), dq.select(2, 2)))
+    print(f"  bwd fused={fused}: {t:.1f} us")
+k.attention_set_fused_bwd(1)
