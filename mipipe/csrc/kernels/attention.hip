@@ -512,6 +512,8 @@ constexpr int kStageBytes = 3 * kChunkImg;  // phase 2: K, Q, dO chunks (48 KiB)
 constexpr int kPOff = 4 * kChunkImg;        // 64 KiB
 constexpr int kDsOff = kPOff + kSqImg;      // 96 KiB
 constexpr int kSmem = kDsOff + kSqImg;      // 128 KiB
+constexpr int kFwdPOff = 2 * kChunkImg;     // forward: 2 chunk buffers + P~ image = 64 KiB (2 workgroups / CU)
+constexpr int kFwdSmem = kFwdPOff + kSqImg;
 
 // [128][64] chunk image: Img<64> addressing (128-byte rows).
 __device__ __forceinline__ int coff(int r, int c16) { return Img<64>::off(r, c16); }
@@ -716,6 +718,133 @@ __global__ void __launch_bounds__(kThreads, 1) attn_bwd_s128_kernel(AttnArgs a) 
   }
 }
 
+// Forward, S = 128: one workgroup per (batch, head); with the whole key range
+// in registers the softmax is exact (no online rescaling): S = Q K^T over D
+// chunks, P = softmax (dropout applied), P~ to a [128][128] LDS image, then
+// O = P~ V per 64-wide D chunk of V.
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 2) attn_fwd_s128_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t boff = (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + boff;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + boff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + boff;
+  constexpr int NC = D / kChunk;
+
+  f32x4 sacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16_t* qrow = Q + (int64_t)(wave * 16 + (lane & 15)) * a.ld_qkv;
+
+  uint4 k0, k1;
+  load_chunk(K, a.ld_qkv, 0, tid, k0, k1);
+  store_chunk(smem, tid, k0, k1);
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const char* kimg = smem + (c & 1) * kChunkImg;
+    if (c + 1 < NC) load_chunk(K, a.ld_qkv, (c + 1) * kChunk, tid, k0, k1);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) qf[s2] = frag_global(qrow + c * kChunk, s2, lane);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s2], crow(kimg, 16 * j, s2, lane), sacc[j], 0, 0, 0);
+    if (c + 1 < NC) store_chunk(smem + ((c + 1) & 1) * kChunkImg, tid, k0, k1);
+    __syncthreads();
+  }
+
+  // exact softmax over the 128 keys (log2 domain), dropout, P~ -> LDS image
+  const int qrow0 = wave * 16 + 4 * (lane >> 4);
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int key = 16 * j + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = sacc[j][r] * sl2;
+      if (CAUSAL && key > qrow0 + r) x = -INFINITY;
+      sacc[j][r] = x;
+      mx[r] = fmaxf(mx[r], x);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mx[r] = row_reduce_max16(mx[r]);
+  float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = exp2f(sacc[j][r] - mx[r]);
+      sacc[j][r] = e;
+      sum[r] += e;
+    }
+  float inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    sum[r] = row_reduce_sum16(sum[r]);
+    inv[r] = 1.f / sum[r];
+  }
+  char* pimg = smem + kFwdPOff;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int key = 16 * j + (lane & 15);
+    uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (a.p > 0.f) {
+      const uint4 mw = attn_mask_words(a, bh, qrow0 >> 2, key);
+      w[0] = mw.x; w[1] = mw.y; w[2] = mw.z; w[3] = mw.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = sacc[j][r] * inv[r];
+      if (a.p > 0.f) pv = w[r] >= a.threshold ? pv * pscale : 0.f;
+      *reinterpret_cast<bf16_t*>(pimg + soff(qrow0 + r, key >> 3) + 2 * (key & 7)) = f2bf(pv);
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.lse[(int64_t)bh * S + qrow0 + r] = (mx[r] + log2f(sum[r])) / kLog2e;
+  }
+
+  // O = P~ V per D chunk (V chunks double-buffered in the phase-1 buffers)
+  bf16_t* O = reinterpret_cast<bf16_t*>(a.o) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+  uint4 v0, v1;
+  load_chunk(V, a.ld_qkv, 0, tid, v0, v1);
+  store_chunk(smem, tid, v0, v1);
+  __syncthreads();  // P~ image and V chunk 0 visible
+  const int r0 = wave * 16;
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const char* vimg = smem + (c & 1) * kChunkImg;
+    if (c + 1 < NC) load_chunk(V, a.ld_qkv, (c + 1) * kChunk, tid, v0, v1);
+    f32x4 o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 ap = srow(pimg, r0, ks, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap, ccol(vimg, 16 * t, ks, lane), o[t], 0, 0, 0);
+    }
+    const int orow = r0 + 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        O[(int64_t)(orow + r) * a.ld_o + c * kChunk + 16 * t + (lane & 15)] = f2bf(o[t][r]);
+    if (c + 1 < NC) store_chunk(smem + ((c + 1) & 1) * kChunkImg, tid, v0, v1);
+    __syncthreads();
+  }
+}
+
 }  // namespace shortseq
 
 template <int D>
@@ -723,7 +852,7 @@ size_t fwd_smem() { return 2 * Img<D>::kBytes + 4 * 16 * kScrStride * 2; }
 template <int D>
 size_t dkdv_smem() { return fwd_smem<D>() + 128 * sizeof(float); }
 
-int g_attn_fused_bwd = 1;  // S == 128: fused single-pass backward (1) or the general kernels (0)
+int g_attn_fused_bwd = 1;  // S == 128: whole-sequence forward/backward kernels (1) or the general ones (0)
 
 template <typename Kern>
 void set_smem(Kern k, size_t bytes) {
@@ -732,6 +861,16 @@ void set_smem(Kern k, size_t bytes) {
 
 template <int D, bool CAUSAL>
 void run_fwd(const AttnArgs& a, hipStream_t s) {
+  if (a.S == shortseq::S && g_attn_fused_bwd) {
+    static bool once_s = false;
+    if (!once_s) {
+      set_smem(shortseq::attn_fwd_s128_kernel<D, CAUSAL>, shortseq::kFwdSmem);
+      once_s = true;
+    }
+    hipLaunchKernelGGL((shortseq::attn_fwd_s128_kernel<D, CAUSAL>), dim3(a.B * a.H), dim3(shortseq::kThreads),
+                       shortseq::kFwdSmem, s, a);
+    return;
+  }
   const size_t sm = fwd_smem<D>();
   static bool once = false;
   if (!once) { set_smem(attn_fwd_kernel<D, CAUSAL>, sm); once = true; }

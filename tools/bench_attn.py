@@ -33,11 +33,11 @@ scale = D ** -0.5
 o, lse, seed, off = k.attention_fwd(q, kk, v, causal, 0.2, scale)
 dout = torch.randn_like(o)
 dq = torch.empty_like(qkv)
-f = timeit(lambda: k.attention_fwd(q, kk, v, causal, 0.2, scale))
-print(f"B={B} S={S} H={H} D={D} causal={causal}: fwd {f:.1f} us")
+print(f"B={B} S={S} H={H} D={D} causal={causal}")
 for fused in (0, 1):
     k.attention_set_fused_bwd(fused)
+    f = timeit(lambda: k.attention_fwd(q, kk, v, causal, 0.2, scale))
     t = timeit(lambda: k.attention_bwd(dout, q, kk, v, o, lse, causal, 0.2, scale, seed, off,
                                        dq.select(2, 0), dq.select(2, 1), dq.select(2, 2)))
-    print(f"  bwd fused={fused}: {t:.1f} us")
+    print(f"  whole-sequence kernels={fused}: fwd {f:.1f} us  bwd {t:.1f} us")
 k.attention_set_fused_bwd(1)
