@@ -254,6 +254,24 @@ typedef __attribute__((address_space(3))) void lds_void;
 // I-contiguous image with 512-byte rows (256 i values).
 __device__ __forceinline__ int ic_off(int r, int c8) { return r * 512 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4), issued from inline
+// asm on purpose: the compiler cannot prove that a DMA into one LDS buffer does
+// not alias the ds_reads of the other, and after a __builtin_amdgcn_global_load_lds
+// it inserts s_waitcnt vmcnt(0) before EVERY following ds_read -- which makes
+// each phase wait for the next tile's DMA to land and serialises staging with
+// compute.  Hidden from the waitcnt pass, the DMA is ordered only by the
+// kernel's own counted waits (vmcnt before the barrier that precedes the read).
+__device__ __forceinline__ void glds16(const void* src, const char* lds_dst) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)lds_dst);
+  asm volatile(
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off"
+      :
+      : "s"(m0), "v"(src)
+      : "memory", "m0");
+}
+
 // Edge tiles: i indices past `lim` (M for A, N for B) are clamped onto the last
 // valid row / 8-column chunk, so every DMA reads mapped memory; the garbage
 // they produce lands only in accumulator rows/columns the epilogue masks off.
@@ -275,7 +293,7 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t l
       const int gi = min(i0 + 8 * c16, lim - 8);
       src = base + (int64_t)(k0 + row) * ld + gi;
     }
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(tile + inst * 1024), 16, 0, 0);
+    glds16(src, tile + inst * 1024);
   }
 }
 
