@@ -355,6 +355,7 @@ void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, doub
   MP_CHECK(dweight.scalar_type() == at::kFloat && dweight.dim() == 2, "embedding_bwd: dweight must be fp32 [V, E]");
   const int64_t E = dweight.size(1), V = dweight.size(0);
   MP_CHECK(dout.numel() == tokens.numel() * E, "embedding_bwd: shape mismatch");
+  MP_CHECK(E % 8 == 0 && E <= 8192, "embedding_bwd: E must be a multiple of 8 and at most 8192");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dout.device());
   auto s = cur_stream(dout);
   dispatch_fb(dout, "embedding_bwd", [&](auto* tag) {

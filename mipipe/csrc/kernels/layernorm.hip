@@ -113,20 +113,44 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(
     if (vi < nvec) Io<T>::load8(gamma + vi * 8, g[k]);
   }
 
+  // Rows are software-pipelined: the next row's z / dy loads are in flight
+  // while this row's reductions and stores run (a block walks rows/grid rows).
+  float zn[MAXV][8], dn[MAXV][8];
+  auto load_row = [&](int row) {
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = threadIdx.x + k * kThreads;
+      if (vi < nvec) {
+        const size_t e = (size_t)row * cols + (size_t)vi * 8;
+        Io<T>::load8(z + e, zn[k]);
+        Io<T>::load8(dy + e, dn[k]);
+      }
+    }
+  };
+  constexpr bool kPrefetch = MAXV <= 2;  // wider rows: the extra row would spill
+  if (kPrefetch && blockIdx.x < rows) load_row(blockIdx.x);
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     const size_t base = (size_t)row * cols;
     const float mean = mean_in[row];
     const float rstd = rstd_in[row];
+    if (!kPrefetch) load_row(row);
+    float zc[MAXV][8], dc[MAXV][8];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        zc[k][i] = zn[k][i];
+        dc[k][i] = dn[k][i];
+      }
+    if (kPrefetch && row + (int)gridDim.x < rows) load_row(row + gridDim.x);
     float xh[MAXV][8], gy[MAXV][8];
     float a = 0.f, b = 0.f;  // sum(g*dy), sum(g*dy*xhat)
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
       const int vi = threadIdx.x + k * kThreads;
       if (vi < nvec) {
-        const size_t e = base + (size_t)vi * 8;
-        float zz[8], d[8];
-        Io<T>::load8(z + e, zz);
-        Io<T>::load8(dy + e, d);
+        const float* zz = zc[k];
+        const float* d = dc[k];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           xh[k][i] = (zz[i] - mean) * rstd;

@@ -36,6 +36,10 @@ __all__ = [
     "PackedAttentionOutput",
     "SelfAttentionBlock",
     "FeedForwardBlock",
+    "FeedForwardIn",
+    "FeedForwardOut",
+    "PackedFeedForwardIn",
+    "PackedFeedForwardOut",
     "TransformerEncoderLayer",
     "transformer_blocks",
     "block_flops",
@@ -184,7 +188,79 @@ class PackedAttentionOutput(nn.Module):
         return self.out.flops_per_token(seq_len)
 
 
+class FeedForwardIn(nn.Module):
+    """First half of the MLP: ``h = drop(act(W1 x + b1))`` (pre-norm: of ``LN2(x)``)."""
+
+    def __init__(self, d_model: int, dim_feedforward: int, dropout: float, activation: str, *, norm_first: bool,
+                 layer_norm_eps: float, device=None, dtype=None) -> None:
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model, self.dim_feedforward = d_model, dim_feedforward
+        self.dropout, self.activation, self.norm_first, self.eps = dropout, activation, norm_first, layer_norm_eps
+        self.linear1_weight = nn.Parameter(torch.empty(dim_feedforward, d_model, **fk))
+        self.linear1_bias = nn.Parameter(torch.empty(dim_feedforward, **fk))
+        if norm_first:
+            self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
+            self.norm_bias = nn.Parameter(torch.empty(d_model, **fk))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        nn.init.kaiming_uniform_(self.linear1_weight, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(self.linear1_weight.shape[1])
+        nn.init.uniform_(self.linear1_bias, -bound, bound)
+        if self.norm_first:
+            nn.init.ones_(self.norm_weight)
+            nn.init.zeros_(self.norm_bias)
+
+    def forward(self, x: Tensor) -> Tensor:
+        p = self.dropout if self.training else 0.0
+        if self.norm_first:
+            x = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
+        return ops.linear(x, self.linear1_weight, self.linear1_bias, self.activation, p, self.training)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return 2 * self.d_model * self.dim_feedforward
+
+
+class FeedForwardOut(nn.Module):
+    """Second half: ``LN2(x + drop(W2 h + b2))`` (pre-norm: ``x + drop(W2 h + b2)``)."""
+
+    def __init__(self, d_model: int, dim_feedforward: int, dropout: float, *, norm_first: bool, layer_norm_eps: float,
+                 device=None, dtype=None) -> None:
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model, self.dim_feedforward = d_model, dim_feedforward
+        self.dropout, self.norm_first, self.eps = dropout, norm_first, layer_norm_eps
+        self.linear2_weight = nn.Parameter(torch.empty(d_model, dim_feedforward, **fk))
+        self.linear2_bias = nn.Parameter(torch.empty(d_model, **fk))
+        if not norm_first:
+            self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
+            self.norm_bias = nn.Parameter(torch.empty(d_model, **fk))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        nn.init.kaiming_uniform_(self.linear2_weight, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(self.linear2_weight.shape[1])
+        nn.init.uniform_(self.linear2_bias, -bound, bound)
+        if not self.norm_first:
+            nn.init.ones_(self.norm_weight)
+            nn.init.zeros_(self.norm_bias)
+
+    def forward(self, x: Tensor, h: Tensor) -> Tensor:
+        p = self.dropout if self.training else 0.0
+        if self.norm_first:
+            return x + ops.linear(h, self.linear2_weight, self.linear2_bias, None, p, self.training)
+        h = ops.linear(h, self.linear2_weight, self.linear2_bias)
+        return ops.add_dropout_layer_norm(h, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return 2 * self.d_model * self.dim_feedforward
+
+
 class FeedForwardBlock(nn.Module):
+    """``LN2(x + drop(W2 drop(act(W1 x))))`` as two halves (:class:`FeedForwardIn`,
+    :class:`FeedForwardOut`) so a pipeline boundary may fall between them."""
+
     def __init__(
         self,
         d_model: int,
@@ -198,41 +274,57 @@ class FeedForwardBlock(nn.Module):
         dtype=None,
     ) -> None:
         super().__init__()
-        fk = {"device": device, "dtype": dtype}
         self.d_model, self.dim_feedforward = d_model, dim_feedforward
-        self.dropout = dropout
-        self.activation = activation
         self.norm_first = norm_first
-        self.eps = layer_norm_eps
-        self.linear1_weight = nn.Parameter(torch.empty(dim_feedforward, d_model, **fk))
-        self.linear1_bias = nn.Parameter(torch.empty(dim_feedforward, **fk))
-        self.linear2_weight = nn.Parameter(torch.empty(d_model, dim_feedforward, **fk))
-        self.linear2_bias = nn.Parameter(torch.empty(d_model, **fk))
-        self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
-        self.norm_bias = nn.Parameter(torch.empty(d_model, **fk))
-        self.reset_parameters()
+        self.fc_in = FeedForwardIn(d_model, dim_feedforward, dropout, activation, norm_first=norm_first,
+                                   layer_norm_eps=layer_norm_eps, device=device, dtype=dtype)
+        self.fc_out = FeedForwardOut(d_model, dim_feedforward, dropout, norm_first=norm_first,
+                                     layer_norm_eps=layer_norm_eps, device=device, dtype=dtype)
 
     def reset_parameters(self) -> None:
-        for w, b in ((self.linear1_weight, self.linear1_bias), (self.linear2_weight, self.linear2_bias)):
-            nn.init.kaiming_uniform_(w, a=math.sqrt(5))
-            bound = 1.0 / math.sqrt(w.shape[1])
-            nn.init.uniform_(b, -bound, bound)
-        nn.init.ones_(self.norm_weight)
-        nn.init.zeros_(self.norm_bias)
+        self.fc_in.reset_parameters()
+        self.fc_out.reset_parameters()
 
     def forward(self, x: Tensor) -> Tensor:
-        p = self.dropout if self.training else 0.0
-        if self.norm_first:
-            h = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
-            h = ops.linear(h, self.linear1_weight, self.linear1_bias, self.activation, p, self.training)
-            h = ops.linear(h, self.linear2_weight, self.linear2_bias, None, p, self.training)
-            return x + h
-        h = ops.linear(x, self.linear1_weight, self.linear1_bias, self.activation, p, self.training)
-        h = ops.linear(h, self.linear2_weight, self.linear2_bias)
-        return ops.add_dropout_layer_norm(h, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
+        return self.fc_out(x, self.fc_in(x))
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2 * 2 * self.d_model * self.dim_feedforward
+
+
+class PackedFeedForwardIn(nn.Module):
+    """Pipeline unit: ``x -> cat(x, h)`` on the feature dim (``[.., E + F]``)."""
+
+    def __init__(self, fc_in: FeedForwardIn) -> None:
+        super().__init__()
+        self.fc_in = fc_in
+
+    def reset_parameters(self) -> None:
+        self.fc_in.reset_parameters()
+
+    def forward(self, x: Tensor) -> Tensor:
+        return torch.cat((x, self.fc_in(x)), dim=-1)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return self.fc_in.flops_per_token(seq_len)
+
+
+class PackedFeedForwardOut(nn.Module):
+    """Pipeline unit: ``cat(x, h) -> fc_out(x, h)``."""
+
+    def __init__(self, fc_out: FeedForwardOut) -> None:
+        super().__init__()
+        self.fc_out = fc_out
+
+    def reset_parameters(self) -> None:
+        self.fc_out.reset_parameters()
+
+    def forward(self, packed: Tensor) -> Tensor:
+        e = self.fc_out.d_model
+        return self.fc_out(packed[..., :e].contiguous(), packed[..., e:].contiguous())
+
+    def flops_per_token(self, seq_len: int) -> float:
+        return self.fc_out.flops_per_token(seq_len)
 
 
 class TransformerEncoderLayer(nn.Sequential):
@@ -269,12 +361,13 @@ class TransformerEncoderLayer(nn.Sequential):
         norm1 = attn.core if attn.core.norm_first else attn.out
         norm1.norm_weight.copy_(layer.norm1.weight)
         norm1.norm_bias.copy_(layer.norm1.bias)
-        ff.linear1_weight.copy_(layer.linear1.weight)
-        ff.linear1_bias.copy_(layer.linear1.bias)
-        ff.linear2_weight.copy_(layer.linear2.weight)
-        ff.linear2_bias.copy_(layer.linear2.bias)
-        ff.norm_weight.copy_(layer.norm2.weight)
-        ff.norm_bias.copy_(layer.norm2.bias)
+        ff.fc_in.linear1_weight.copy_(layer.linear1.weight)
+        ff.fc_in.linear1_bias.copy_(layer.linear1.bias)
+        ff.fc_out.linear2_weight.copy_(layer.linear2.weight)
+        ff.fc_out.linear2_bias.copy_(layer.linear2.bias)
+        norm2 = ff.fc_in if ff.norm_first else ff.fc_out
+        norm2.norm_weight.copy_(layer.norm2.weight)
+        norm2.norm_bias.copy_(layer.norm2.bias)
         return self
 
 
@@ -301,12 +394,15 @@ def transformer_blocks(
 
 
 def pipeline_units(blocks: List[nn.Module]) -> List[nn.Module]:
-    """Expands every :class:`SelfAttentionBlock` into its two packed halves so a
-    pipeline stage boundary may fall inside it (see :func:`merge_units`)."""
+    """Expands every :class:`SelfAttentionBlock` and :class:`FeedForwardBlock`
+    into its two packed halves so a pipeline stage boundary may fall inside it
+    (see :func:`merge_units`): 4 units per layer."""
     units: List[nn.Module] = []
     for b in blocks:
         if isinstance(b, SelfAttentionBlock):
             units += [PackedAttentionCore(b.core), PackedAttentionOutput(b.out)]
+        elif isinstance(b, FeedForwardBlock):
+            units += [PackedFeedForwardIn(b.fc_in), PackedFeedForwardOut(b.fc_out)]
         else:
             units.append(b)
     return units
@@ -320,12 +416,22 @@ def merge_units(units: List[nn.Module]) -> List[nn.Module]:
     i = 0
     while i < len(units):
         u = units[i]
-        if (isinstance(u, PackedAttentionCore) and i + 1 < len(units)
-                and isinstance(units[i + 1], PackedAttentionOutput)):
+        nxt = units[i + 1] if i + 1 < len(units) else None
+        if isinstance(u, PackedAttentionCore) and isinstance(nxt, PackedAttentionOutput):
             blk = SelfAttentionBlock.__new__(SelfAttentionBlock)
             nn.Module.__init__(blk)
             blk.core = u.core
-            blk.out = units[i + 1].out
+            blk.out = nxt.out
+            out.append(blk)
+            i += 2
+            continue
+        if isinstance(u, PackedFeedForwardIn) and isinstance(nxt, PackedFeedForwardOut):
+            blk = FeedForwardBlock.__new__(FeedForwardBlock)
+            nn.Module.__init__(blk)
+            blk.d_model, blk.dim_feedforward = u.fc_in.d_model, u.fc_in.dim_feedforward
+            blk.norm_first = u.fc_in.norm_first
+            blk.fc_in = u.fc_in
+            blk.fc_out = nxt.fc_out
             out.append(blk)
             i += 2
             continue

@@ -56,18 +56,19 @@ class StagePlan:
 
 def block_costs(cfg: LMConfig) -> List[float]:
     """Training FLOPs per token of the pipeline units
-    ``[Encoder, (attn core, attn out, mlp) x L, (final norm), Decoder]``
+    ``[Encoder, (attn core, attn out, mlp in, mlp out) x L, (final norm), Decoder]``
     (see ``mipipe.models.transformer.pipeline_units``)."""
     e, f, s, v = cfg.d_model, cfg.dim_feedforward, cfg.seq_len, cfg.vocab
     causal = 0.5 if cfg.causal else 1.0
     core = 3.0 * (2 * 3 * e * e + 4 * s * e * causal) + 3.0 * 10 * e
     out = 3.0 * (2 * e * e) + 3.0 * 10 * e  # + LN/dropout traffic
-    mlp = 3.0 * (2 * 2 * e * f) + 3.0 * 20 * e
+    mlp_in = 3.0 * (2 * e * f) + 3.0 * 5 * f
+    mlp_out = 3.0 * (2 * e * f) + 3.0 * 10 * e
     enc = 3.0 * 40 * e  # gather + scatter-add traffic, expressed in FLOP-equivalents
     dec = 3.0 * (2 * e * v) + 3.0 * 4 * v  # GEMM + cross-entropy passes
     costs = [enc]
     for _ in range(cfg.num_layers):
-        costs += [core, out, mlp]
+        costs += [core, out, mlp_in, mlp_out]
     if cfg.norm_first:
         costs.append(3.0 * 10 * e)
     costs.append(dec)
@@ -239,19 +240,36 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0) -
     return best[1]
 
 
+UNITS_PER_LAYER = 4  # attention core, attention output, mlp in, mlp out
+
+
+def unit_kind(cfg: LMConfig, index: int) -> str:
+    """``enc`` / ``core`` / ``out`` / ``mlp_in`` / ``mlp_out`` / ``norm`` / ``dec``."""
+    if index == 0:
+        return "enc"
+    if index <= UNITS_PER_LAYER * cfg.num_layers:
+        return ("core", "out", "mlp_in", "mlp_out")[(index - 1) % UNITS_PER_LAYER]
+    return "norm" if (cfg.norm_first and index == UNITS_PER_LAYER * cfg.num_layers + 1) else "dec"
+
+
 def unit_is_packed_core(cfg: LMConfig, index: int) -> bool:
     """True if pipeline unit ``index`` is an attention core (packed output)."""
-    return 1 <= index <= 3 * cfg.num_layers and (index - 1) % 3 == 0
+    return unit_kind(cfg, index) == "core"
 
 
 def stage_input_shape(cfg: LMConfig, plan: StagePlan, vstage: int, micro_batch: int) -> Tuple[int, ...]:
-    """Shape of the activation virtual stage ``vstage`` receives (``[2, mb, S, E]``
-    after a packed attention core, else ``[mb, S, E]``)."""
+    """Shape of the activation virtual stage ``vstage`` receives: ``[2, mb, S, E]``
+    after a packed attention core, ``[mb, S, E + F]`` after a packed MLP input
+    half, else ``[mb, S, E]``."""
     base = (micro_batch, cfg.seq_len, cfg.d_model)
     if vstage == 0:
         return base
-    prev = plan.slice(vstage).start - 1
-    return (2,) + base if unit_is_packed_core(cfg, prev) else base
+    kind = unit_kind(cfg, plan.slice(vstage).start - 1)
+    if kind == "core":
+        return (2,) + base
+    if kind == "mlp_in":
+        return (micro_batch, cfg.seq_len, cfg.d_model + cfg.dim_feedforward)
+    return base
 
 
 def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -> nn.Sequential:
