@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-bubble", action="store_true", help="skip the extra instrumented step")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = gloo + fp32 plumbing check of the multi-rank path (tests only)")
+    ap.add_argument("--split-decoder", default="auto", choices=["auto", "on", "off"],
+                    help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
                     help="model chunks per rank (looping placement); 'auto' = shortest simulated step")
     return ap.parse_args()
@@ -92,11 +94,12 @@ def main() -> int:
     mb = args.micro_batch or {"gpt2_xl": 8, "tiny": 8}.get(cfg.name, 32)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
+    splits = {"auto": (False, True), "on": (True,), "off": (False,)}[args.split_decoder]
     if args.virtual == "auto":
-        virtual, plan = choose_virtual(cfg, pp, m)
+        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits)
     else:
         virtual = int(args.virtual)
-        plan = plan_stages(cfg, pp, virtual, m)
+        plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1)
     torch.manual_seed(1234 + rank)
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype).train() for vs in plan.vstages(rank)]
@@ -119,7 +122,8 @@ def main() -> int:
     g = torch.Generator(device="cpu").manual_seed(0)
     tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)
     inputs = [tokens[i, :, :S].to(device) for i in range(m)] if rank == 0 else None
-    targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(m)] if is_last else None
+    # every rank gets the targets: the vocabulary-split decoder's head stage needs them too
+    targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(m)]
 
     def train_step():
         opt.zero_grad()
@@ -209,6 +213,7 @@ def main() -> int:
                 "checkpoint": args.checkpoint,
                 "schedule": "gpipe" if virtual == 1 else f"gpipe-looping(v={virtual})",
                 "virtual_chunks_per_rank": virtual,
+                "vocab_split_decoder": plan.split_decoder,
                 "parallelism": f"pp{world}",
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),

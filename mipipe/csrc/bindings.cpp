@@ -307,18 +307,35 @@ std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignor
   return {loss, lse};
 }
 
-Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor scale, int64_t ignore_index) {
+// out (optional): [N, >= V] destination with unit column stride (e.g. a
+// zero-padded vocabulary buffer); row_scale (optional): per-row scale, see loss.hip.
+Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, std::optional<Tensor> scale, int64_t ignore_index,
+                 std::optional<Tensor> row_scale, std::optional<Tensor> out) {
   check_rows(logits, "logits");
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0) && lse.numel() == logits.size(0),
            "cross_entropy_bwd: shape mismatch");
-  MP_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && scale.is_cuda(), "cross_entropy_bwd: bad scale");
+  MP_CHECK(scale.has_value() != row_scale.has_value(), "cross_entropy_bwd: give exactly one of scale / row_scale");
+  if (scale)
+    MP_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->is_cuda(), "cross_entropy_bwd: bad scale");
+  if (row_scale)
+    MP_CHECK(row_scale->scalar_type() == at::kFloat && row_scale->numel() == logits.size(0) && row_scale->is_cuda() &&
+                 row_scale->is_contiguous(), "cross_entropy_bwd: bad row_scale");
   at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
-  auto d = at::empty({logits.size(0), logits.size(1)}, logits.options());
+  Tensor d;
+  if (out) {
+    MP_CHECK(out->dim() == 2 && out->size(0) == logits.size(0) && out->size(1) >= logits.size(1) &&
+                 out->stride(1) == 1 && out->scalar_type() == logits.scalar_type() && out->is_cuda(),
+             "cross_entropy_bwd: bad out");
+    d = *out;
+  } else {
+    d = at::empty({logits.size(0), logits.size(1)}, logits.options());
+  }
   auto s = cur_stream(logits);
   dispatch_fb(logits, "cross_entropy_bwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    cross_entropy_bwd<T>(cptr<T>(logits), cptr<int64_t>(target), cptr<float>(lse), cptr<float>(scale),
-                         logits.size(0), logits.size(1), logits.stride(0), ignore_index, ptr<T>(d), s);
+    cross_entropy_bwd<T>(cptr<T>(logits), cptr<int64_t>(target), cptr<float>(lse),
+                         scale ? cptr<float>(*scale) : nullptr, row_scale ? cptr<float>(*row_scale) : nullptr,
+                         logits.size(0), logits.size(1), logits.stride(0), d.stride(0), ignore_index, ptr<T>(d), s);
   });
   return d;
 }
@@ -624,7 +641,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dbias"), py::arg("dbias_acc") = py::none());
   m.def("column_sum", &py_column_sum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cross_entropy_fwd", &py_ce_fwd);
-  m.def("cross_entropy_bwd", &py_ce_bwd);
+  m.def("cross_entropy_bwd", &py_ce_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("scale"),
+        py::arg("ignore_index"), py::arg("row_scale") = py::none(), py::arg("out") = py::none());
   m.def("embedding_fwd", &py_embed_fwd);
   m.def("embedding_bwd", &py_embed_bwd);
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });

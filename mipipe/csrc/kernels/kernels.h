@@ -137,8 +137,9 @@ template <typename T>
 void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
                        int64_t ignore_index, float* loss, float* lse, hipStream_t s);
 template <typename T>
-void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale, int64_t rows,
-                       int64_t V, int64_t ld, int64_t ignore_index, T* dlogits, hipStream_t s);
+void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale,
+                       const float* row_scale, int64_t rows, int64_t V, int64_t ld, int64_t ld_out,
+                       int64_t ignore_index, T* dlogits, hipStream_t s);
 
 // ------------------------------------------------------------------ embedding
 template <typename T>

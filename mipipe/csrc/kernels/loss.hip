@@ -64,17 +64,20 @@ __global__ void __launch_bounds__(kT) ce_fwd_kernel(const T* __restrict__ logits
   }
 }
 
+// row_scale (optional): per-row dL/dloss_row; then a target outside [0, V)
+// means "no one-hot term in this vocabulary slice" (the row still gets its
+// softmax term) -- the vocabulary-split decoder's backward.
 template <typename T>
 __global__ void __launch_bounds__(kT) ce_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
                                                     const float* __restrict__ lse_in, const float* __restrict__ scale_p,
-                                                    int64_t V, int64_t ld, int64_t ignore_index,
-                                                    T* __restrict__ dlogits) {
+                                                    const float* __restrict__ row_scale, int64_t V, int64_t ld,
+                                                    int64_t ld_out, int64_t ignore_index, T* __restrict__ dlogits) {
   const int64_t row = blockIdx.x;
   const T* x = logits + row * ld;
-  T* d = dlogits + row * V;
+  T* d = dlogits + row * ld_out;
   const int64_t t = target[row];
   const bool valid = !(t == ignore_index || t < 0 || t >= V);
-  const float scale = valid ? *scale_p : 0.f;
+  const float scale = row_scale != nullptr ? row_scale[row] : (valid ? *scale_p : 0.f);
   const float lse = lse_in[row];
   for (int64_t c = threadIdx.x; c < V; c += kT) {
     const float pr = __expf(Io<T>::load(x + c) - lse);
@@ -94,16 +97,17 @@ void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int
 }
 
 template <typename T>
-void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale, int64_t rows,
-                       int64_t V, int64_t ld, int64_t ignore_index, T* dlogits, hipStream_t s) {
+void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale,
+                       const float* row_scale, int64_t rows, int64_t V, int64_t ld, int64_t ld_out,
+                       int64_t ignore_index, T* dlogits, hipStream_t s) {
   if (rows == 0) return;
-  hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, lse, scale, V, ld,
-                     ignore_index, dlogits);
+  hipLaunchKernelGGL((ce_bwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, lse, scale, row_scale,
+                     V, ld, ld_out, ignore_index, dlogits);
 }
 
 template void cross_entropy_fwd<float>(const float*, const int64_t*, int64_t, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
 template void cross_entropy_fwd<bf16_t>(const bf16_t*, const int64_t*, int64_t, int64_t, int64_t, int64_t, float*, float*, hipStream_t);
-template void cross_entropy_bwd<float>(const float*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, int64_t, float*, hipStream_t);
-template void cross_entropy_bwd<bf16_t>(const bf16_t*, const int64_t*, const float*, const float*, int64_t, int64_t, int64_t, int64_t, bf16_t*, hipStream_t);
+template void cross_entropy_bwd<float>(const float*, const int64_t*, const float*, const float*, const float*, int64_t, int64_t, int64_t, int64_t, int64_t, float*, hipStream_t);
+template void cross_entropy_bwd<bf16_t>(const bf16_t*, const int64_t*, const float*, const float*, const float*, int64_t, int64_t, int64_t, int64_t, int64_t, bf16_t*, hipStream_t);
 
 }  // namespace mipipe

@@ -7,7 +7,9 @@ from .transformer import (
     block_flops,
     transformer_blocks,
 )
-from .lm import CONFIGS, Decoder, Encoder, FinalNorm, LMConfig, build_lm_blocks, sinusoidal_positions
+from .lm import (CONFIGS, Decoder, Encoder, FinalNorm, LMConfig, TargetSequential, build_lm_blocks,
+                 lm_pipeline_units, sinusoidal_positions)
+from .vocab_split import DecoderHead, DecoderTail, split_decoder
 
 __all__ = [
     "SelfAttentionBlock",
@@ -21,5 +23,10 @@ __all__ = [
     "LMConfig",
     "CONFIGS",
     "build_lm_blocks",
+    "lm_pipeline_units",
+    "TargetSequential",
+    "DecoderHead",
+    "DecoderTail",
+    "split_decoder",
     "sinusoidal_positions",
 ]

@@ -191,3 +191,34 @@ def build_lm_blocks(cfg: LMConfig, *, device=None, dtype=None) -> List[nn.Module
         blocks.append(FinalNorm(cfg.d_model, device=device, dtype=dtype))
     blocks.append(Decoder(cfg.vocab, cfg.d_model, device=device, dtype=dtype))
     return blocks
+
+
+class TargetSequential(nn.Sequential):
+    """``nn.Sequential`` that also hands the micro-batch targets to the children
+    that want them (``wants_target``: the vocabulary-split decoder units)."""
+
+    @property
+    def wants_target(self) -> bool:
+        return any(getattr(m, "wants_target", False) for m in self)
+
+    @property
+    def fused_loss(self) -> bool:
+        return len(self) > 0 and getattr(self[-1], "fused_loss", False)
+
+    def forward(self, x, target=None):  # type: ignore[override]
+        for m in self:
+            x = m(x, target) if getattr(m, "wants_target", False) else m(x)
+        return x
+
+
+def lm_pipeline_units(blocks: List[nn.Module], *, split_decoder: bool = False) -> List[nn.Module]:
+    """:func:`~mipipe.models.transformer.pipeline_units` of an LM, optionally with
+    the decoder cut along the vocabulary (:mod:`mipipe.models.vocab_split`)."""
+    from .transformer import pipeline_units
+    from .vocab_split import split_decoder as _split
+
+    units = pipeline_units(blocks)
+    if split_decoder and isinstance(units[-1], Decoder):
+        head, tail = _split(units[-1])
+        units = units[:-1] + [head, tail]
+    return units

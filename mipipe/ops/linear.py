@@ -25,7 +25,7 @@ from torch import Tensor
 from ._util import native_or_none
 from .activation import ACTIVATIONS, bias_act_reference
 
-__all__ = ["linear", "deferred_wgrad", "flush_wgrad"]
+__all__ = ["linear", "deferred_wgrad", "flush_wgrad", "accumulate_wgrad"]
 
 
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
@@ -126,6 +126,27 @@ def _defer(w: Tensor, dy: Tensor, x: Tensor) -> None:
     entry = _DEFERRED.setdefault(id(w), (w, [], []))
     entry[1].append(dy)
     entry[2].append(x)
+
+
+def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
+    """Weight gradient ``dy^T x`` of ``w`` (2-D operands) for ops with their own
+    backward: into ``w.main_grad`` (deferred inside :func:`deferred_wgrad`) when
+    it exists, else returned for autograd."""
+    main = getattr(w, "main_grad", None)
+    k = native_or_none(dy) if dy.is_cuda else None
+    tile = (k is not None and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and k.gemm_supported(w.shape[0], w.shape[1], dy.shape[0]))
+    if main is not None and tile:
+        if _DEFERRED is not None:
+            _defer(w, dy.contiguous(), x.contiguous())
+        else:
+            k.linear_wgrad(dy.contiguous(), x.contiguous(), main)
+        return None
+    g = torch.matmul(dy.t(), x)
+    if main is not None:
+        main.add_(g.float())
+        return None
+    return g.to(w.dtype)
 
 
 def flush_wgrad() -> None:

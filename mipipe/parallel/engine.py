@@ -194,6 +194,21 @@ class PipelineEngine:
             return torch.empty(like.shape, dtype=like.dtype, device=self.device)
         return torch.empty(self.act_shapes[c], dtype=self.act_dtype, device=self.device)
 
+    @staticmethod
+    def _run(mod: nn.Module, x: Tensor, targets, i: int) -> Tensor:
+        """Chunk forward; chunks that want the targets (vocabulary-split decoder) get them."""
+        if getattr(mod, "wants_target", False):
+            if targets is None:
+                raise ValueError("this stage needs the targets (vocabulary-split decoder): pass targets on every rank")
+            return mod(x, targets[i])
+        return mod(x)
+
+    def _loss(self, mod: nn.Module, y: Tensor, targets, i: int) -> Tensor:
+        """Loss of the last virtual stage: computed by the chunk itself (``fused_loss``) or by ``loss_fn``."""
+        if getattr(mod, "fused_loss", False):
+            return y
+        return self.loss_fn(y, targets[i])
+
     def _timer(self):
         if not self.measure or self.device.type != "cuda":
             return None
@@ -204,7 +219,8 @@ class PipelineEngine:
         """Forward + backward of one mini-batch given as per-micro-batch lists.
 
         ``inputs`` (rank owning virtual stage 0) and ``targets`` (rank owning
-        the last virtual stage) have ``chunks`` entries.  Gradients accumulate
+        the last virtual stage, and every rank whose chunks want targets) have
+        ``chunks`` entries.  Gradients accumulate
         into the parameters (or their ``main_grad``); the caller runs the
         optimizer.  Returns the mean loss on the last stage.
         """
@@ -252,11 +268,11 @@ class PipelineEngine:
             if training and i < stop:
                 rng[c][i] = _RNGState(self.device)
                 with torch.no_grad(), enable_checkpointing():
-                    y = mod(x)
+                    y = self._run(mod, x, targets, i)
             else:
-                y = mod(x)
-            if last and self.loss_fn is not None:
-                loss = self.loss_fn(y, targets[i])
+                y = self._run(mod, x, targets, i)
+            if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
+                loss = self._loss(mod, y, targets, i)
                 losses.append(loss.detach())
                 y = loss / m  # backward seeds from the scaled loss
             if tm:
@@ -291,9 +307,9 @@ class PipelineEngine:
                     if st.dev is not None:
                         torch.cuda.set_rng_state(st.dev, self.device)
                     with torch.enable_grad(), enable_recomputing():
-                        y = mod(x)
-                        if last and self.loss_fn is not None:
-                            y = self.loss_fn(y, targets[i]) / m
+                        y = self._run(mod, x, targets, i)
+                        if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
+                            y = self._loss(mod, y, targets, i) / m
             else:
                 y = stage_out[c][i]
             if last:

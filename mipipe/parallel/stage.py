@@ -16,8 +16,9 @@ import torch
 from torch import nn
 
 from ..balance import balance_cost
-from ..models.lm import LMConfig, build_lm_blocks
-from ..models.transformer import merge_units, pipeline_units
+from ..models.lm import LMConfig, TargetSequential, build_lm_blocks, lm_pipeline_units
+from ..models.transformer import merge_units
+from ..models.vocab_split import STAT_SLOTS, split_point
 
 __all__ = ["StagePlan", "plan_stages", "block_costs", "stage_input_shape", "build_stage", "simulate_step", "choose_virtual"]
 
@@ -30,6 +31,7 @@ class StagePlan:
     balance: List[int]
     costs: List[float]
     virtual: int = 1
+    split_decoder: bool = False  # decoder cut along the vocabulary into two units
 
     @property
     def ranks(self) -> int:
@@ -54,7 +56,7 @@ class StagePlan:
         return max(per) / (sum(per) / len(per))
 
 
-def block_costs(cfg: LMConfig) -> List[float]:
+def block_costs(cfg: LMConfig, split_decoder: bool = False) -> List[float]:
     """Training FLOPs per token of the pipeline units
     ``[Encoder, (attn core, attn out, mlp in, mlp out) x L, (final norm), Decoder]``
     (see ``mipipe.models.transformer.pipeline_units``)."""
@@ -71,7 +73,11 @@ def block_costs(cfg: LMConfig) -> List[float]:
         costs += [core, out, mlp_in, mlp_out]
     if cfg.norm_first:
         costs.append(3.0 * 10 * e)
-    costs.append(dec)
+    if split_decoder:
+        va = split_point(v)
+        costs += [dec * va / v, dec * (v - va) / v]
+    else:
+        costs.append(dec)
     return costs
 
 
@@ -216,23 +222,23 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
     return bal
 
 
-def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0) -> StagePlan:
+def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, split_decoder: bool = False) -> StagePlan:
     """Plan for ``stages`` ranks with ``virtual`` chunks each (looping placement).
 
     With ``virtual > 1`` the split starts from the rank-total-balanced one and
     is refined against the simulated step time for ``chunks`` micro-batches
     (default 4 x stages): a chunk far larger than its neighbours stalls the
     micro-batch flow even when rank totals are even."""
-    costs = block_costs(cfg)
+    costs = block_costs(cfg, split_decoder)
     if stages * virtual > len(costs):
         raise ValueError(f"{stages} x {virtual} virtual stages exceed the {len(costs)} pipeline units")
     if virtual == 1:
-        return StagePlan(balance_cost(costs, stages), costs)
+        return StagePlan(balance_cost(costs, stages), costs, 1, split_decoder)
     m = chunks or 4 * stages
     best = None
     for start in (balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)):
         bal = _makespan_refined(costs, stages, virtual, m, start)
-        plan = StagePlan(bal, costs, virtual)
+        plan = StagePlan(bal, costs, virtual, split_decoder)
         t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m,
                           deferred_w=DEFERRED_W)[0]
         if best is None or t < best[0]:
@@ -243,13 +249,20 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0) -
 UNITS_PER_LAYER = 4  # attention core, attention output, mlp in, mlp out
 
 
-def unit_kind(cfg: LMConfig, index: int) -> str:
-    """``enc`` / ``core`` / ``out`` / ``mlp_in`` / ``mlp_out`` / ``norm`` / ``dec``."""
+def unit_kind(cfg: LMConfig, index: int, split_decoder: bool = False) -> str:
+    """``enc`` / ``core`` / ``out`` / ``mlp_in`` / ``mlp_out`` / ``norm`` / ``dec``
+    (``dec_head`` / ``dec_tail`` when the decoder is split)."""
     if index == 0:
         return "enc"
-    if index <= UNITS_PER_LAYER * cfg.num_layers:
+    body = UNITS_PER_LAYER * cfg.num_layers
+    if index <= body:
         return ("core", "out", "mlp_in", "mlp_out")[(index - 1) % UNITS_PER_LAYER]
-    return "norm" if (cfg.norm_first and index == UNITS_PER_LAYER * cfg.num_layers + 1) else "dec"
+    rest = index - body - 1 - (1 if cfg.norm_first else 0)
+    if rest < 0:
+        return "norm"
+    if split_decoder:
+        return "dec_head" if rest == 0 else "dec_tail"
+    return "dec"
 
 
 def unit_is_packed_core(cfg: LMConfig, index: int) -> bool:
@@ -264,41 +277,48 @@ def stage_input_shape(cfg: LMConfig, plan: StagePlan, vstage: int, micro_batch: 
     base = (micro_batch, cfg.seq_len, cfg.d_model)
     if vstage == 0:
         return base
-    kind = unit_kind(cfg, plan.slice(vstage).start - 1)
+    kind = unit_kind(cfg, plan.slice(vstage).start - 1, plan.split_decoder)
     if kind == "core":
         return (2,) + base
     if kind == "mlp_in":
         return (micro_batch, cfg.seq_len, cfg.d_model + cfg.dim_feedforward)
+    if kind == "dec_head":
+        return (micro_batch, cfg.seq_len, cfg.d_model + STAT_SLOTS)
     return base
 
 
-def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -> nn.Sequential:
+def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -> TargetSequential:
     """Instantiates ONLY this virtual stage's units (on ``device``, in ``dtype``)
-    and merges attention halves that ended up on the same stage."""
+    and merges attention / MLP halves that ended up on the same stage."""
     with torch.device("meta"):
-        proto = pipeline_units(build_lm_blocks(cfg))
+        proto = lm_pipeline_units(build_lm_blocks(cfg), split_decoder=plan.split_decoder)
     units = []
     for idx in plan.slice(vstage):
         u = proto[idx].to_empty(device=device)
         u.reset_parameters()
         units.append(u)
     del proto
-    stage = nn.Sequential(*merge_units(units))
+    stage = TargetSequential(*merge_units(units))
     for p in stage.parameters():
         if p.dtype.is_floating_point:
             p.data = p.data.to(dtype)
     return stage
 
 
-def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence[int] = (1, 2, 3)) -> Tuple[int, StagePlan]:
-    """Chunks per rank with the shortest simulated step (ties -> fewer chunks)."""
+def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence[int] = (1, 2, 3),
+                   split_options: Sequence[bool] = (False, True)) -> Tuple[int, StagePlan]:
+    """Chunks per rank (and whether to split the decoder) with the shortest
+    simulated step; ties (within 0.5 %) keep the simpler plan."""
     best = None
-    for v in candidates:
-        if stages * v > len(block_costs(cfg)) or (v > 1 and stages == 1):
+    for split in split_options:
+        if split and stages == 1:
             continue
-        plan = plan_stages(cfg, stages, v, chunks)
-        t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks,
-                             deferred_w=DEFERRED_W)
-        if best is None or t < best[0] * 0.995:
-            best = (t, v, plan)
+        for v in candidates:
+            if stages * v > len(block_costs(cfg, split)) or (v > 1 and stages == 1):
+                continue
+            plan = plan_stages(cfg, stages, v, chunks, split)
+            t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks,
+                                 deferred_w=DEFERRED_W)
+            if best is None or t < best[0] * 0.995:
+                best = (t, v, plan)
     return best[1], best[2]

@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from mipipe import ops
-from mipipe.models import CONFIGS, build_lm_blocks
+from mipipe.models import CONFIGS, TargetSequential, build_lm_blocks, lm_pipeline_units
 from mipipe.optim import FlatAdam
 from mipipe.parallel import PipelineEngine, plan_stages, schedule_actions
 from mipipe.models.transformer import merge_units, pipeline_units
@@ -156,20 +156,51 @@ def _gpu_cfg():
                                dim_feedforward=512, vocab=512, seq_len=64)
 
 
-def _worker(rank, world, port, checkpoint, q, gpu=False, virtual=1):
+def _split_cfg():
+    return dataclasses.replace(_tiny(), vocab=1000)
+
+
+def test_vocab_split_decoder_matches_full_cpu():
+    """DecoderHead + DecoderTail == Decoder + cross-entropy (loss and every gradient)."""
+    from mipipe.models import Decoder, split_decoder
+
+    torch.manual_seed(0)
+    dec = Decoder(1000, 32)
+    head, tail = split_decoder(dec)
+    assert head.va == 512 and tail.vb == 488
+    x = torch.randn(3, 8, 32, requires_grad=True)
+    t = torch.randint(0, 1000, (3, 8))
+    t[0, 0] = -100  # ignored
+    ref = torch.nn.functional.cross_entropy(dec(x).reshape(-1, 1000), t.reshape(-1), ignore_index=-100)
+    ref.backward()
+    x2 = x.detach().clone().requires_grad_()
+    loss = tail(head(x2, t), t)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5
+    assert torch.allclose(x2.grad, x.grad, atol=1e-6)
+    assert torch.allclose(head.weight.grad, dec.weight.grad[:512], atol=1e-6)
+    assert torch.allclose(tail.weight.grad[:488], dec.weight.grad[512:1000], atol=1e-6)
+    assert torch.allclose(tail.bias.grad[:488], dec.bias.grad[512:1000], atol=1e-6)
+    assert tail.weight.grad[488:].abs().max() == 0
+
+
+def _worker(rank, world, port, checkpoint, q, gpu=False, virtual=1, split=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = _gpu_cfg() if gpu else _tiny()
+        cfg = _gpu_cfg() if gpu else (_split_cfg() if split else _tiny())
         device = torch.device("cuda", 0) if gpu else torch.device("cpu")
         dtype = torch.bfloat16 if gpu else torch.float32
         m, mb = 4, 2
         torch.manual_seed(0)
         full = torch.nn.Sequential(*build_lm_blocks(cfg))
         names = {id(p): n for n, p in full.named_parameters()}
-        units = pipeline_units(list(full.children()))
-        plan = plan_stages(cfg, world, virtual)
-        chunks = [torch.nn.Sequential(*merge_units([units[i] for i in plan.slice(s)])).train().to(device, dtype)
+        units = lm_pipeline_units(list(full.children()), split_decoder=split)
+        if split:
+            for tag, u in (("dec_head", units[-2]), ("dec_tail", units[-1])):
+                names[id(u.weight)], names[id(u.bias)] = f"{tag}.weight", f"{tag}.bias"
+        plan = plan_stages(cfg, world, virtual, split_decoder=split)
+        chunks = [TargetSequential(*merge_units([units[i] for i in plan.slice(s)])).train().to(device, dtype)
                   for s in plan.vstages(rank)]
         stage = torch.nn.ModuleList(chunks)
         opt = FlatAdam(stage.parameters(), lr=1e-3, max_grad_norm=0.5)
@@ -181,7 +212,7 @@ def _worker(rank, world, port, checkpoint, q, gpu=False, virtual=1):
         inputs = [x.to(device) for x in inputs]
         targets = [t.to(device) for t in targets]
         opt.zero_grad()
-        st = eng.step(inputs if rank == 0 else None, targets if rank == world - 1 else None)
+        st = eng.step(inputs if rank == 0 else None, targets)
         opt.fold_grads()
         # numpy: pickled by value (a torch tensor would be shared by fd, which
         # dies with this process)
@@ -193,17 +224,30 @@ def _worker(rank, world, port, checkpoint, q, gpu=False, virtual=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("checkpoint,world,virtual", [("never", 2, 1), ("except_last", 2, 1), ("never", 2, 2),
-                                                      ("always", 2, 3), ("except_last", 3, 2)])
-def test_engine_multi_rank_gloo(checkpoint, world, virtual):
-    cfg = _tiny()
+@pytest.mark.parametrize("checkpoint,world,virtual,split", [("never", 2, 1, False), ("except_last", 2, 1, False),
+                                                            ("never", 2, 2, False), ("always", 2, 3, False),
+                                                            ("except_last", 3, 2, False), ("never", 2, 1, True),
+                                                            ("except_last", 2, 2, True), ("always", 3, 2, True)])
+def test_engine_multi_rank_gloo(checkpoint, world, virtual, split):
+    cfg = _split_cfg() if split else _tiny()
     m, mb = 4, 2
     ref, ref_loss = _reference(cfg, m, mb)
     ref_params = dict(ref.named_parameters())
+    if split:  # the vocabulary-split head / tail gradients are row blocks of the decoder's
+        dec_name = [n for n in ref_params if n.endswith(".weight")][-1].rsplit(".", 1)[0]
+        dw, db = ref_params[dec_name + ".weight"].grad, ref_params[dec_name + ".bias"].grad
+        va, v = 512, cfg.vocab
+        pad = lambda t: torch.cat([t, torch.zeros((512 - (v - va),) + t.shape[1:])])  # noqa: E731
+        ref_params = {n: p for n, p in ref_params.items() if not n.startswith(dec_name + ".")}
+        for name, g in (("dec_head.weight", dw[:va]), ("dec_head.bias", db[:va]),
+                        ("dec_tail.weight", pad(dw[va:v])), ("dec_tail.bias", pad(db[va:v]))):
+            ref_params[name] = torch.nn.Parameter(torch.zeros_like(g))
+            ref_params[name].grad = g
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, checkpoint, q, False, virtual)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, checkpoint, q, False, virtual, split))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=120) for _ in range(world)]
@@ -225,8 +269,9 @@ def test_engine_multi_rank_gloo(checkpoint, world, virtual):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("checkpoint,virtual", [("never", 1), ("always", 1), ("except_last", 2)])
-def test_engine_two_ranks_share_gpu(checkpoint, virtual):
+@pytest.mark.parametrize("checkpoint,virtual,split", [("never", 1, False), ("always", 1, False),
+                                                      ("except_last", 2, False), ("never", 2, True)])
+def test_engine_two_ranks_share_gpu(checkpoint, virtual, split):
     """Two pipeline ranks on one MI355X (gloo, host-staged boundaries): the HIP
     kernels of both stages and the multi-rank schedule against the single-rank
     engine on the whole model (same bf16 kernels, same initial weights)."""
@@ -248,13 +293,19 @@ def test_engine_two_ranks_share_gpu(checkpoint, virtual):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q, True, virtual)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, checkpoint, q, True, virtual, split)) for r in range(2)]
     for p in procs:
         p.start()
     results = [q.get(timeout=300) for _ in range(2)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if split:
+        dec_name = [n for n in ref if n.endswith(".weight")][-1].rsplit(".", 1)[0]
+        dw, db = ref.pop(dec_name + ".weight"), ref.pop(dec_name + ".bias")
+        va, v = 256, cfg.vocab  # split_point(512)
+        ref.update({"dec_head.weight": dw[:va], "dec_head.bias": db[:va],
+                    "dec_tail.weight": dw[va:], "dec_tail.bias": db[va:]})
     seen = set()
     for rank, loss, grads, sq in results:
         if loss is not None:
