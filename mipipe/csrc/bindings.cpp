@@ -650,7 +650,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention_bwd", &py_attention_bwd);
   m.def("gemm_supported", &py_gemm_supported);
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);
-  m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 1 ping-pong (default), 0 per-tile barrier");
+  m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 auto (default)");
   m.def("gemm_get_schedule", &gemm_get_schedule);
   m.def("linear_fwd", &py_linear_fwd);
   m.def("linear_dgrad", &py_linear_dgrad);

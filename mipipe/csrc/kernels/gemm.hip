@@ -297,6 +297,48 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t l
   }
 }
 
+// Loop-invariant per-lane byte offsets of the 4 pieces a wave stages per
+// operand tile; the K position lives in the scalar base, so each LDS-DMA is
+// issued in SADDR form (SGPR base + 32-bit VGPR offset) with no per-tile
+// address arithmetic.  gemm_supported() keeps rows * ld * 2 bytes < 4 GiB.
+template <bool KC>
+__device__ __forceinline__ void stage_offsets(int64_t ld, int i0, int lim, int wave, int lane, uint32_t (&off)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int inst = wave * 4 + u;
+    if (KC) {
+      const int row = 8 * inst + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int gi = min(i0 + row, lim - 1);
+      off[u] = (uint32_t)(((int64_t)gi * ld + 8 * c) * 2);
+    } else {
+      const int row = 2 * inst + (lane >> 5);
+      const int c16 = (lane & 31) ^ (ic_rk(row) << 1);
+      const int gi = min(i0 + 8 * c16, lim - 8);
+      off[u] = (uint32_t)(((int64_t)row * ld + gi) * 2);
+    }
+  }
+}
+
+__device__ __forceinline__ void glds16_saddr(const char* base, uint32_t off, const char* lds_dst) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)lds_dst);
+  asm volatile(
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2"
+      :
+      : "s"(m0), "v"(off), "s"(base)
+      : "memory", "m0");
+}
+
+template <bool KC>
+__device__ __forceinline__ void stage_fast(const bf16_t* base, int64_t ld, int k0, const uint32_t (&off)[4], char* tile,
+                                           int wave) {
+  const char* b = reinterpret_cast<const char*>(base) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) glds16_saddr(b, off[u], tile + (wave * 4 + u) * 1024);
+}
+
 // Operand base and local k of K-tile k0 (K-segmented operands, GemmArgs::seg_k).
 __device__ __forceinline__ const bf16_t* seg_base(const GemmArgs& g, bool is_a, int k0, int& kl) {
   if (g.seg_k == 0) {
@@ -342,7 +384,10 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane
 //     the last interval of tile u -- group 0 after its phase-3 MFMAs, group 1
 //     in its phase-3 load interval -- so every wave's reads of tile u+1 start
 //     after a barrier all DMAs of the tile have landed behind.
-int g_gemm_sched = 1;  // 1: ping-pong (default), 0: one barrier per K-tile
+// 0: one barrier per K-tile everywhere, 1: ping-pong everywhere, 2 (default):
+// ping-pong except the weight-gradient layout (both operands I-contiguous),
+// where the per-tile loop measured 1-4 % faster (profiles/gemm_saddr_ab.txt).
+int g_gemm_sched = 2;
 
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP>
 __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
@@ -362,12 +407,15 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BK;
+  uint32_t offA[4], offB[4];
+  stage_offsets<A_KC>(g.lda, m0, g.M, wave, lane, offA);
+  stage_offsets<B_KC>(g.ldb, n0, g.N, wave, lane, offB);
   {
     int kl;
     const bf16_t* A = seg_base(g, true, 0, kl);
-    stage<A_KC>(A, g.lda, m0, kl, g.M, smem, wave, lane);
+    stage_fast<A_KC>(A, g.lda, kl, offA, smem, wave);
     const bf16_t* B = seg_base(g, false, 0, kl);
-    stage<B_KC>(B, g.ldb, n0, kl, g.N, smem + kTileBytes, wave, lane);
+    stage_fast<B_KC>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
   }
 
   if constexpr (PP) {
@@ -400,12 +448,12 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         if (ph == 0 && more) {
           int kl;
           const bf16_t* A = seg_base(g, true, (u + 1) * BK, kl);
-          stage<A_KC>(A, g.lda, m0, kl, g.M, nxt, wave, lane);
+          stage_fast<A_KC>(A, g.lda, kl, offA, nxt, wave);
         }
         if (ph == 1 && more) {
           int kl;
           const bf16_t* B = seg_base(g, false, (u + 1) * BK, kl);
-          stage<B_KC>(B, g.ldb, n0, kl, g.N, nxt + kTileBytes, wave, lane);
+          stage_fast<B_KC>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
         }
         if (ph == 3 && wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -440,9 +488,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       char* nxt = smem + ((kt + 1) & 1) * kBufBytes;
       int kl;
       const bf16_t* A = seg_base(g, true, (kt + 1) * BK, kl);
-      stage<A_KC>(A, g.lda, m0, kl, g.M, nxt, wave, lane);
+      stage_fast<A_KC>(A, g.lda, kl, offA, nxt, wave);
       const bf16_t* B = seg_base(g, false, (kt + 1) * BK, kl);
-      stage<B_KC>(B, g.ldb, n0, kl, g.N, nxt + kTileBytes, wave, lane);
+      stage_fast<B_KC>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
     }
     const char* cur = smem + (kt & 1) * kBufBytes;
 #pragma unroll
@@ -588,7 +636,8 @@ void launch(const GemmArgs& g, hipStream_t s) {
       attr_set = true;
     }
     const int blocks = big_tiles(g);
-    if (big::g_gemm_sched == 1)
+    const bool pp = big::g_gemm_sched == 1 || (big::g_gemm_sched == 2 && (A_KC || B_KC));
+    if (pp)
       hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, true>), dim3(blocks), dim3(big::kThreads),
                          big::kSmemBytes, s, g);
     else
@@ -616,8 +665,9 @@ int gemm_get_schedule() { return big::g_gemm_sched; }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   // 16-byte operand chunks along M/N (I-contiguous layouts) and whole 64-deep K tiles.
+  // ... and 32-bit per-lane staging offsets: a K-contiguous operand spans < 4 GiB.
   return M >= 8 && N >= 8 && K > 0 && M % 8 == 0 && N % 8 == 0 && K % BK == 0 && M < (1LL << 30) &&
-         N < (1LL << 30);
+         N < (1LL << 30) && M * K < (1LL << 31) && N * K < (1LL << 31);
 }
 
 void gemm_bf16(const GemmArgs& gi, hipStream_t s) {

@@ -100,7 +100,8 @@ struct GemmArgs {
   const void* b_seg[kMaxSegs] = {};
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
-// Main-loop schedule of the 256x256 GEMM: 1 = ping-pong wave groups (default), 0 = one barrier per K-tile.
+// Main-loop schedule of the 256x256 GEMM: 0 = one barrier per K-tile, 1 = ping-pong wave groups,
+// 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout (default).
 void gemm_set_schedule(int mode);
 int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);

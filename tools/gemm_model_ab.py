@@ -49,4 +49,4 @@ for name, fl, fn in cases:
         t = timeit(fn)
         res.append(f"sched={sc} {t:8.1f} us {fl / t / 1e6:6.0f} TF/s")
     print(f"{name:32s} " + " | ".join(res))
-k.gemm_set_schedule(1)
+k.gemm_set_schedule(2)
