@@ -41,7 +41,9 @@ def parse():
                     help="sequences per micro-batch (default 32 for enc12_d4096 / ref_main, 8 for gpt2_xl)")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
-    ap.add_argument("--checkpoint", default="never", choices=["never", "except_last", "always"])
+    ap.add_argument("--checkpoint", default="auto", choices=["auto", "never", "except_last", "always"],
+                    help="auto = the BASELINE.json config for this model and PP: enc12 'except_last' at PP=8 "
+                         "(config #3), else 'never' (config #2); gpt2_xl 'always' (config #4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--clip", type=float, default=0.5)
@@ -90,7 +92,16 @@ def main() -> int:
         cfg.seq_len = args.seq_len
     S, E, V = cfg.seq_len, cfg.d_model, cfg.vocab
     pp = world
-    m = args.chunks or 4 * pp
+    if cfg.name == "gpt2_xl":
+        # BASELINE config #4: GPT-2-XL PP=8 chunks=8, checkpoint='always'
+        m = args.chunks or (8 if pp == 8 else 4 * pp)
+        auto_ckpt = "always"
+    else:
+        # configs #2 / #3: chunks = 4 x PP; the full-node PP=8 run uses 'except_last'
+        m = args.chunks or 4 * pp
+        auto_ckpt = "except_last" if pp == 8 else "never"
+    if args.checkpoint == "auto":
+        args.checkpoint = auto_ckpt
     mb = args.micro_batch or {"gpt2_xl": 8, "tiny": 8}.get(cfg.name, 32)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
