@@ -106,11 +106,14 @@ def main() -> int:
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
     splits = {"auto": (False, True), "on": (True,), "off": (False,)}[args.split_decoder]
+    # backward / forward cost: 2, plus the recomputed forward of checkpointed micro-batches
+    recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
+    bwd_ratio = 2.0 + recompute
     if args.virtual == "auto":
-        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits)
+        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio)
     else:
         virtual = int(args.virtual)
-        plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1)
+        plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1, bwd_ratio=bwd_ratio)
     torch.manual_seed(1234 + rank)
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype).train() for vs in plan.vstages(rank)]
@@ -127,8 +130,8 @@ def main() -> int:
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
                             act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device)
-    sim_t, sim_busy = simulate_step([plan.stage_cost(g) for g in range(pp * virtual)], pp, virtual, m,
-                                    deferred_w=0.5)
+    sim_t, sim_busy = simulate_step([plan.stage_cost(g) for g in range(pp * virtual)], pp, virtual, m, bwd_ratio,
+                                    deferred_w=1.0 / bwd_ratio)
 
     g = torch.Generator(device="cpu").manual_seed(0)
     tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)

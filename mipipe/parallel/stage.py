@@ -194,7 +194,8 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
 DEFERRED_W = 0.5
 
 
-def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int, start: List[int]) -> List[int]:
+def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int, start: List[int],
+                      bwd_ratio: float = 2.0) -> List[int]:
     """Coordinate descent on the simulated step time (:func:`simulate_step`)."""
     groups = ranks * virtual
 
@@ -203,7 +204,7 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
         for k in b:
             gc.append(sum(costs[pos:pos + k]))
             pos += k
-        return simulate_step(gc, ranks, virtual, chunks, deferred_w=DEFERRED_W)[0]
+        return simulate_step(gc, ranks, virtual, chunks, bwd_ratio, deferred_w=1.0 / bwd_ratio)[0]
 
     bal, best = list(start), score(start)
     improved = True
@@ -222,7 +223,8 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
     return bal
 
 
-def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, split_decoder: bool = False) -> StagePlan:
+def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, split_decoder: bool = False,
+                bwd_ratio: float = 2.0) -> StagePlan:
     """Plan for ``stages`` ranks with ``virtual`` chunks each (looping placement).
 
     With ``virtual > 1`` the split starts from the rank-total-balanced one and
@@ -237,10 +239,10 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, s
     m = chunks or 4 * stages
     best = None
     for start in (balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)):
-        bal = _makespan_refined(costs, stages, virtual, m, start)
+        bal = _makespan_refined(costs, stages, virtual, m, start, bwd_ratio)
         plan = StagePlan(bal, costs, virtual, split_decoder)
-        t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m,
-                          deferred_w=DEFERRED_W)[0]
+        t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m, bwd_ratio,
+                          deferred_w=1.0 / bwd_ratio)[0]
         if best is None or t < best[0]:
             best = (t, plan)
     return best[1]
@@ -306,9 +308,10 @@ def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -
 
 
 def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence[int] = (1, 2, 3),
-                   split_options: Sequence[bool] = (False, True)) -> Tuple[int, StagePlan]:
+                   split_options: Sequence[bool] = (False, True), bwd_ratio: float = 2.0) -> Tuple[int, StagePlan]:
     """Chunks per rank (and whether to split the decoder) with the shortest
-    simulated step; ties (within 0.5 %) keep the simpler plan."""
+    simulated step; ties (within 0.5 %) keep the simpler plan.  ``bwd_ratio``
+    is backward / forward cost (2, or 3 when every micro-batch is recomputed)."""
     best = None
     for split in split_options:
         if split and stages == 1:
@@ -316,9 +319,9 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence
         for v in candidates:
             if stages * v > len(block_costs(cfg, split)) or (v > 1 and stages == 1):
                 continue
-            plan = plan_stages(cfg, stages, v, chunks, split)
-            t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks,
-                                 deferred_w=DEFERRED_W)
+            plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio)
+            t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks, bwd_ratio,
+                                 deferred_w=1.0 / bwd_ratio)
             if best is None or t < best[0] * 0.995:
                 best = (t, v, plan)
     return best[1], best[2]
