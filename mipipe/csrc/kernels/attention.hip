@@ -57,6 +57,43 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ base, int6
   }
 }
 
+// Register prefetch of a 64 x D tile (T14): the next tile's global loads are
+// issued right after the barrier that publishes the current one, so they are
+// in flight during the current tile's MFMAs; the LDS write follows the next
+// barrier.  Used for D <= 128 (D = 256 has no registers to spare).
+// (named registers, not an array: a loop-carried uint4[] was kept in scratch)
+struct TileRegs {
+  uint4 r0, r1, r2, r3;
+};
+template <int D>
+__device__ __forceinline__ uint4 load_piece(const bf16_t* __restrict__ base, int64_t ld, int tid, int u) {
+  const int id = tid + u * kThreads;
+  const int r = id / Img<D>::kChunks, c = id % Img<D>::kChunks;
+  return *reinterpret_cast<const uint4*>(base + (int64_t)r * ld + c * 8);
+}
+template <int D>
+__device__ __forceinline__ void store_piece(char* img, int tid, int u, const uint4& v) {
+  const int id = tid + u * kThreads;
+  *reinterpret_cast<uint4*>(img + Img<D>::off(id / Img<D>::kChunks, id % Img<D>::kChunks)) = v;
+}
+template <int D>
+__device__ __forceinline__ void load_tile(const bf16_t* __restrict__ base, int64_t ld, int tid, TileRegs& t) {
+  constexpr int P = kRows * Img<D>::kChunks / kThreads;
+  static_assert(P <= 4, "register prefetch holds at most 4 pieces per thread");
+  t.r0 = load_piece<D>(base, ld, tid, 0);
+  if constexpr (P > 1) t.r1 = load_piece<D>(base, ld, tid, 1);
+  if constexpr (P > 2) t.r2 = load_piece<D>(base, ld, tid, 2);
+  if constexpr (P > 3) t.r3 = load_piece<D>(base, ld, tid, 3);
+}
+template <int D>
+__device__ __forceinline__ void store_tile(char* img, int tid, const TileRegs& t) {
+  constexpr int P = kRows * Img<D>::kChunks / kThreads;
+  store_piece<D>(img, tid, 0, t.r0);
+  if constexpr (P > 1) store_piece<D>(img, tid, 1, t.r1);
+  if constexpr (P > 2) store_piece<D>(img, tid, 2, t.r2);
+  if constexpr (P > 3) store_piece<D>(img, tid, 3, t.r3);
+}
+
 // B-operand fragment where B[k = d][n = row]: the n index is the image row
 // (16 rows from rb), k = 32 s + 8 (lane >> 4) + j is the column  -> row read.
 template <int D>
@@ -163,12 +200,27 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_fwd_kernel(At
   const int qrow0 = q0 + wave * 16 + 4 * (lane >> 4);  // this lane's rows qrow0 .. +3
   const int ntiles = CAUSAL ? qt + 1 : a.S / kRows;
 
+  constexpr bool PF = D <= 128;
+  TileRegs kr, vr;
+  if constexpr (PF) {
+    load_tile<D>(K, a.ld_qkv, tid, kr);
+    load_tile<D>(V, a.ld_qkv, tid, vr);
+  }
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * kRows;
     __syncthreads();
-    stage_tile<D>(K + (int64_t)k0 * a.ld_qkv, a.ld_qkv, kimg, tid);
-    stage_tile<D>(V + (int64_t)k0 * a.ld_qkv, a.ld_qkv, vimg, tid);
+    if constexpr (PF) {
+      store_tile<D>(kimg, tid, kr);
+      store_tile<D>(vimg, tid, vr);
+    } else {
+      stage_tile<D>(K + (int64_t)k0 * a.ld_qkv, a.ld_qkv, kimg, tid);
+      stage_tile<D>(V + (int64_t)k0 * a.ld_qkv, a.ld_qkv, vimg, tid);
+    }
     __syncthreads();
+    if constexpr (PF) if (t + 1 < ntiles) {
+      load_tile<D>(K + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, kr);
+      load_tile<D>(V + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, vr);
+    }
 
     f32x4 sacc[4];
 #pragma unroll
@@ -318,12 +370,27 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_dq_kernel(Att
   const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
   const int ntiles = CAUSAL ? qt + 1 : a.S / kRows;
 
+  constexpr bool PF = D <= 128;
+  TileRegs kr, vr;
+  if constexpr (PF) {
+    load_tile<D>(K, a.ld_qkv, tid, kr);
+    load_tile<D>(V, a.ld_qkv, tid, vr);
+  }
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * kRows;
     __syncthreads();
-    stage_tile<D>(K + (int64_t)k0 * a.ld_qkv, a.ld_qkv, kimg, tid);
-    stage_tile<D>(V + (int64_t)k0 * a.ld_qkv, a.ld_qkv, vimg, tid);
+    if constexpr (PF) {
+      store_tile<D>(kimg, tid, kr);
+      store_tile<D>(vimg, tid, vr);
+    } else {
+      stage_tile<D>(K + (int64_t)k0 * a.ld_qkv, a.ld_qkv, kimg, tid);
+      stage_tile<D>(V + (int64_t)k0 * a.ld_qkv, a.ld_qkv, vimg, tid);
+    }
     __syncthreads();
+    if constexpr (PF) if (t + 1 < ntiles) {
+      load_tile<D>(K + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, kr);
+      load_tile<D>(V + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, vr);
+    }
     f32x4 sacc[4], pacc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) sacc[j] = pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -407,16 +474,31 @@ __global__ void __launch_bounds__(kThreads, D >= 128 ? 1 : 2) attn_dkdv_kernel(A
   const int first = CAUSAL ? kt : 0;
   const int nq = a.S / kRows;
 
+  constexpr bool PF = D <= 128;
+  TileRegs qr, dr;
+  if constexpr (PF) {
+    load_tile<D>(Q + (int64_t)first * kRows * a.ld_qkv, a.ld_qkv, tid, qr);
+    load_tile<D>(dO + (int64_t)first * kRows * a.ld_o, a.ld_o, tid, dr);
+  }
   for (int t = first; t < nq; ++t) {
     const int q0 = t * kRows;
     __syncthreads();
-    stage_tile<D>(Q + (int64_t)q0 * a.ld_qkv, a.ld_qkv, qimg, tid);
-    stage_tile<D>(dO + (int64_t)q0 * a.ld_o, a.ld_o, dimg, tid);
+    if constexpr (PF) {
+      store_tile<D>(qimg, tid, qr);
+      store_tile<D>(dimg, tid, dr);
+    } else {
+      stage_tile<D>(Q + (int64_t)q0 * a.ld_qkv, a.ld_qkv, qimg, tid);
+      stage_tile<D>(dO + (int64_t)q0 * a.ld_o, a.ld_o, dimg, tid);
+    }
     if (tid < 64) {
       stats[tid] = a.lse[(int64_t)bh * a.S + q0 + tid] * kLog2e;
       stats[64 + tid] = a.delta[(int64_t)bh * a.S + q0 + tid];
     }
     __syncthreads();
+    if constexpr (PF) if (t + 1 < nq) {
+      load_tile<D>(Q + (int64_t)(q0 + kRows) * a.ld_qkv, a.ld_qkv, tid, qr);
+      load_tile<D>(dO + (int64_t)(q0 + kRows) * a.ld_o, a.ld_o, tid, dr);
+    }
     f32x4 sacc[4], pacc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) sacc[j] = pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -434,7 +516,27 @@ __global__ void __launch_bounds__(kThreads, D >= 128 ? 1 : 2) attn_dkdv_kernel(A
       const int ql = 16 * j + (lane & 15);
       const int q = q0 + ql;
       const float l2 = stats[ql], dl = stats[64 + ql];
-      uint32_t w = 0xFFFFFFFFu;
+      // Dropout words: element (q, key0 + r) uses word (q & 3) of
+      // Philox(q >> 2, key0 + r).  The 4 lanes of a quad share q >> 2 and
+      // key0 and each needs one word of each of the 4 Philox blocks, so each
+      // lane generates ONE block (key0 + (lane & 3)) and the quad transposes
+      // the 4 x 4 words with 4 lane shuffles (instead of 4 Philox calls each).
+      uint32_t kw0 = 0xFFFFFFFFu, kw1 = 0xFFFFFFFFu, kw2 = 0xFFFFFFFFu, kw3 = 0xFFFFFFFFu;
+      if (a.p > 0.f) {
+        const int t = lane & 3;
+        const uint4 mine = attn_mask_words(a, bh, q >> 2, key0 + t);
+        auto word = [&](int i) { return i == 0 ? mine.x : (i == 1 ? mine.y : (i == 2 ? mine.z : mine.w)); };
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int src = (lane & ~3) | ((t + k) & 3);
+          const uint32_t got = (uint32_t)__shfl((int)word((t - k) & 3), src, 64);  // word t of key0 + ((t+k)&3)
+          const int r = (t + k) & 3;
+          kw0 = r == 0 ? got : kw0;
+          kw1 = r == 1 ? got : kw1;
+          kw2 = r == 2 ? got : kw2;
+          kw3 = r == 3 ? got : kw3;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = key0 + r;
@@ -443,9 +545,7 @@ __global__ void __launch_bounds__(kThreads, D >= 128 ? 1 : 2) attn_dkdv_kernel(A
         float dp = pacc[j][r];
         float pdrop = pr;
         if (a.p > 0.f) {
-          const uint4 mw = attn_mask_words(a, bh, q >> 2, key);
-          const uint32_t ws[4] = {mw.x, mw.y, mw.z, mw.w};
-          w = ws[q & 3];
+          const uint32_t w = r == 0 ? kw0 : (r == 1 ? kw1 : (r == 2 ? kw2 : kw3));
           const bool keep = w >= a.threshold;
           pdrop = keep ? pr * pscale : 0.f;
           dp = keep ? dp * pscale : 0.f;

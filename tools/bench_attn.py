@@ -27,17 +27,18 @@ def timeit(fn, iters=20):
 
 B, S, H, D = (int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (32, 128, 16, 256)))
 causal = len(sys.argv) > 5 and sys.argv[5] == "causal"
+P = float(sys.argv[6]) if len(sys.argv) > 6 else 0.2
 qkv = torch.randn(B, S, 3, H, D, device="cuda").to(torch.bfloat16)
 q, kk, v = (qkv.select(2, i) for i in range(3))
 scale = D ** -0.5
-o, lse, seed, off = k.attention_fwd(q, kk, v, causal, 0.2, scale)
+o, lse, seed, off = k.attention_fwd(q, kk, v, causal, P, scale)
 dout = torch.randn_like(o)
 dq = torch.empty_like(qkv)
-print(f"B={B} S={S} H={H} D={D} causal={causal}")
+print(f"B={B} S={S} H={H} D={D} causal={causal} p={P}")
 for fused in (0, 1):
     k.attention_set_fused_bwd(fused)
-    f = timeit(lambda: k.attention_fwd(q, kk, v, causal, 0.2, scale))
-    t = timeit(lambda: k.attention_bwd(dout, q, kk, v, o, lse, causal, 0.2, scale, seed, off,
+    f = timeit(lambda: k.attention_fwd(q, kk, v, causal, P, scale))
+    t = timeit(lambda: k.attention_bwd(dout, q, kk, v, o, lse, causal, P, scale, seed, off,
                                        dq.select(2, 0), dq.select(2, 1), dq.select(2, 2)))
     print(f"  whole-sequence kernels={fused}: fwd {f:.1f} us  bwd {t:.1f} us")
 k.attention_set_fused_bwd(1)
