@@ -7,18 +7,23 @@
 //   forward  Y  = X  . W^T   A = X  [T, K] (K-contiguous)  B = W  [N, K] (K-contiguous)
 //   dgrad    dX = dY . W     A = dY [T, N] (K-contiguous)  B = W  [N, K] read as [K, N] (N-contiguous)
 //   wgrad    dW += dY^T . X  A = dY read as [K=T, M] (M-contiguous), B = X [K=T, N] (N-contiguous)
-// Operand tiles are staged into LDS in their memory layout (16-byte global
-// loads, coalesced); K-contiguous fragments are read with ds_read_b128 and
-// K-strided ones with the gfx950 transposing read ds_read_b64_tr_b16, so no
-// layout ever needs a transpose pass in HBM.  Both LDS images are XOR-swizzled
-// so the 16-lane read groups hit distinct banks (T2/T10).
+// Operand tiles are staged into LDS in their memory layout (16-byte loads,
+// coalesced); K-contiguous fragments are read with ds_read_b128 and K-strided
+// ones with the gfx950 transposing read ds_read_b64_tr_b16, so no layout ever
+// needs a transpose pass in HBM.  Both LDS images are XOR-swizzled so the
+// lane groups of a read hit distinct banks (T2/T10).
 //
-// Geometry: 128x128x64 block tile, 4 waves (2x2), 64x64 per wave as 4x4
-// v_mfma_f32_16x16x32_bf16 tiles; global->register prefetch of tile k+1 is
-// issued before the MFMAs of tile k and written to the other LDS buffer after
-// them (T14), one barrier per K-tile.  Block ids are remapped so consecutive
-// tiles of an 8-row group share an XCD's L2 (T1, bijective form).
-//
+// Main kernel (big::gemm256_kernel): 256x256x64 block tile, 8 waves (2 M x 4 N,
+// 128x64 per wave as 8x4 v_mfma_f32_16x16x32_bf16 tiles), operand tiles staged
+// by LDS-DMA (global_load_lds_dwordx4, SADDR form with loop-invariant per-lane
+// offsets) into two 64 KiB buffers, and either a ping-pong main loop (the two
+// wave groups one barrier interval apart: one group's 16-MFMA cluster runs
+// while the other reads its fragments) or one barrier per K-tile.  Edge tiles
+// (M, N any multiple of 8) are clamped on load and masked on store; K may be
+// split into segments living in different buffers (deferred weight gradients).
+// Block ids are remapped so consecutive tiles of an 8-row group share an XCD's
+// L2 (T1, bijective form).  A 128x128 register-staged kernel serves grids too
+// small for 256x256 tiles.
 // Epilogues:
 //   kEpiStoreBf16 -- + bias, activation (ReLU/GELU), dropout (Philox mask in
 //                    the "column-quad" layout shared with the elementwise
@@ -249,58 +254,20 @@ constexpr int kTileBytes = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int kBufBytes = 2 * kTileBytes;    // A + B
 constexpr int kSmemBytes = 128 * 260 * 4;    // 130 KiB: 2 x 64 KiB operand buffers, reused by the epilogue
 
-typedef __attribute__((address_space(3))) void lds_void;
-
 // I-contiguous image with 512-byte rows (256 i values).
 __device__ __forceinline__ int ic_off(int r, int c8) { return r * 512 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
 
-// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4), issued from inline
-// asm on purpose: the compiler cannot prove that a DMA into one LDS buffer does
-// not alias the ds_reads of the other, and after a __builtin_amdgcn_global_load_lds
-// it inserts s_waitcnt vmcnt(0) before EVERY following ds_read -- which makes
-// each phase wait for the next tile's DMA to land and serialises staging with
-// compute.  Hidden from the waitcnt pass, the DMA is ordered only by the
-// kernel's own counted waits (vmcnt before the barrier that precedes the read).
-__device__ __forceinline__ void glds16(const void* src, const char* lds_dst) {
-  const uint32_t m0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)lds_dst);
-  asm volatile(
-      "s_mov_b32 m0, %0\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off"
-      :
-      : "s"(m0), "v"(src)
-      : "memory", "m0");
-}
-
-// Edge tiles: i indices past `lim` (M for A, N for B) are clamped onto the last
-// valid row / 8-column chunk, so every DMA reads mapped memory; the garbage
-// they produce lands only in accumulator rows/columns the epilogue masks off.
-template <bool KC>
-__device__ __forceinline__ void stage(const bf16_t* __restrict__ base, int64_t ld, int i0, int k0, int lim,
-                                      char* tile, int wave, int lane) {
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int inst = wave * 4 + u;  // 32 x 1 KiB pieces per tile
-    const bf16_t* src;
-    if (KC) {
-      const int row = 8 * inst + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      const int gi = min(i0 + row, lim - 1);
-      src = base + (int64_t)gi * ld + k0 + 8 * c;
-    } else {
-      const int row = 2 * inst + (lane >> 5);
-      const int c16 = (lane & 31) ^ (ic_rk(row) << 1);
-      const int gi = min(i0 + 8 * c16, lim - 8);
-      src = base + (int64_t)(k0 + row) * ld + gi;
-    }
-    glds16(src, tile + inst * 1024);
-  }
-}
-
+// LDS-DMA staging (global_load_lds_dwordx4: 16 bytes per lane, lane-linear
+// 1 KiB per wave-instruction; the bank swizzle is applied to the per-lane
+// SOURCE address).
+//
 // Loop-invariant per-lane byte offsets of the 4 pieces a wave stages per
 // operand tile; the K position lives in the scalar base, so each LDS-DMA is
 // issued in SADDR form (SGPR base + 32-bit VGPR offset) with no per-tile
 // address arithmetic.  gemm_supported() keeps rows * ld * 2 bytes < 4 GiB.
+// Edge tiles: i indices past `lim` (M for A, N for B) are clamped onto the last
+// valid row / 8-column chunk, so every DMA reads mapped memory; the garbage
+// they produce lands only in accumulator rows/columns the epilogue masks off.
 template <bool KC>
 __device__ __forceinline__ void stage_offsets(int64_t ld, int i0, int lim, int wave, int lane, uint32_t (&off)[4]) {
 #pragma unroll
@@ -320,6 +287,12 @@ __device__ __forceinline__ void stage_offsets(int64_t ld, int i0, int lim, int w
   }
 }
 
+// Issued from inline asm on purpose: the compiler cannot prove that a DMA into
+// one LDS buffer does not alias the ds_reads of the other, and after a
+// __builtin_amdgcn_global_load_lds it inserts s_waitcnt vmcnt(0) before EVERY
+// following ds_read -- each phase would wait for the next tile's DMA to land.
+// Hidden from the waitcnt pass, the DMA is ordered only by the kernel's own
+// counted waits (vmcnt before the barrier that precedes the read).
 __device__ __forceinline__ void glds16_saddr(const char* base, uint32_t off, const char* lds_dst) {
   const uint32_t m0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)lds_dst);
   asm volatile(
