@@ -455,6 +455,41 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad) {
   gemm_bf16(g, cur_stream(dy));
 }
 
+// Deferred bias gradient over the micro-batches of a step: out (+)= column sums
+// of every [rows, cols] input, one stage-1 launch per input into a shared
+// partial buffer and ONE reduction.
+void py_column_sum_segments(std::vector<Tensor> xs, Tensor out, bool accumulate) {
+  MP_CHECK(!xs.empty(), "column_sum_segments: empty list");
+  check_cuda(out, "out");
+  const int64_t cols = xs[0].size(-1);
+  MP_CHECK(out.numel() == cols && out.is_contiguous(), "column_sum_segments: bad out");
+  const bool out_f32 = out.scalar_type() == at::kFloat;
+  MP_CHECK(out_f32 || out.scalar_type() == xs[0].scalar_type(), "column_sum_segments: out must be fp32 or the input dtype");
+  std::vector<int64_t> rows(xs.size());
+  std::vector<int> parts(xs.size());
+  int total = 0;
+  for (size_t i = 0; i < xs.size(); ++i) {
+    check_cuda(xs[i], "x");
+    MP_CHECK(xs[i].is_contiguous() && xs[i].size(-1) == cols && xs[i].scalar_type() == xs[0].scalar_type(),
+             "column_sum_segments: inputs must be contiguous with equal width and dtype");
+    rows[i] = xs[i].numel() / std::max<int64_t>(cols, 1);
+    parts[i] = colsum_parts(rows[i]);
+    total += parts[i];
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  auto part = at::empty({total, cols}, xs[0].options().dtype(at::kFloat));
+  auto s = cur_stream(out);
+  int first = 0;
+  for (size_t i = 0; i < xs.size(); ++i) {
+    dispatch_fb(xs[i], "column_sum_segments", [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      column_sum_partial<T>(cptr<T>(xs[i]), rows[i], (int)cols, ptr<float>(part) + (int64_t)first * cols, parts[i], s);
+    });
+    first += parts[i];
+  }
+  reduce_parts(ptr<float>(part), nullptr, total, (int)cols, out.data_ptr(), nullptr, out_f32, accumulate, s);
+}
+
 // Deferred weight gradient over the micro-batches of a step:
 //   main_grad[N, K] += sum_i dy_i^T . x_i
 // as K-segmented GEMMs (up to GemmArgs::kMaxSegs micro-batches per launch),
@@ -656,6 +691,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_dgrad", &py_linear_dgrad);
   m.def("linear_wgrad", &py_linear_wgrad);
   m.def("linear_wgrad_segments", &py_linear_wgrad_segments);
+  m.def("column_sum_segments", &py_column_sum_segments);
   m.def("gemm_f32", &py_gemm_f32);
   m.def("sumsq", &py_sumsq);
   m.def("adam_step", &py_adam);

@@ -166,6 +166,20 @@ int colsum_parts(int64_t rows) {
 }
 
 template <typename T>
+void column_sum_partial(const T* x, int64_t rows, int cols, float* part, int nparts, hipStream_t s) {
+  if (rows == 0 || cols == 0) return;
+  const int rows_per = (int)((rows + nparts - 1) / nparts);
+  if (cols % 8 == 0) {
+    const int nvec = cols / 8;
+    dim3 g1((unsigned)((nvec + 255) / 256), (unsigned)nparts);
+    hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+  } else {
+    dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);
+    hipLaunchKernelGGL((colsum_part_scalar_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+  }
+}
+
+template <typename T>
 void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, void* out, bool out_f32, bool accumulate,
                 hipStream_t s) {
   if (rows == 0 || cols == 0) return;
@@ -185,6 +199,8 @@ template void bias_act_dropout_fwd<float>(const float*, const float*, float*, in
 template void bias_act_dropout_fwd<bf16_t>(const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
 template void bias_act_dropout_bwd<float>(const float*, const float*, const float*, float*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
 template void bias_act_dropout_bwd<bf16_t>(const bf16_t*, const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
+template void column_sum_partial<float>(const float*, int64_t, int, float*, int, hipStream_t);
+template void column_sum_partial<bf16_t>(const bf16_t*, int64_t, int, float*, int, hipStream_t);
 template void column_sum<float>(const float*, int64_t, int, float*, int, void*, bool, bool, hipStream_t);
 template void column_sum<bf16_t>(const bf16_t*, int64_t, int, float*, int, void*, bool, bool, hipStream_t);
 

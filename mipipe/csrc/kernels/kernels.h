@@ -68,6 +68,10 @@ template <typename T>
 void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int64_t rows, int cols, int act, float p,
                           uint64_t seed, uint64_t offset, hipStream_t s);
 int colsum_parts(int64_t rows);
+// Stage 1 only: per-part column sums of `rows` rows into part[nparts][cols]
+// (several inputs can write disjoint part slices and share one reduce_parts).
+template <typename T>
+void column_sum_partial(const T* x, int64_t rows, int cols, float* part, int nparts, hipStream_t s);
 template <typename T>
 void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, void* out, bool out_f32, bool accumulate,
                 hipStream_t s);

@@ -73,19 +73,25 @@ class _Linear(torch.autograd.Function):
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
         main_b = getattr(bias, "main_grad", None) if need_db else None
+        # inside deferred_wgrad(): the bias gradient joins the step's batch too
+        defer_b = main_b is not None and _DEFERRED is not None and d2.shape[-1] % 8 == 0
         act, p = ctx.act, ctx.p
         if act != 0 or p > 0.0:
             # GEMM-saved GELU pre-activation already includes the bias.
             bias_for_bwd = None if ctx.fused_tile else bias
             dpre, db = k.bias_act_bwd(d2, saved if saved is not None else d2, bias_for_bwd, act, p,
-                                      ctx.seed, ctx.offset, need_db, main_b)
+                                      ctx.seed, ctx.offset, need_db and not defer_b, None if defer_b else main_b)
         else:
             dpre = d2
             db = None
-            if main_b is not None:
+            if defer_b:
+                pass
+            elif main_b is not None:
                 k.column_sum(d2, main_b, True)  # fp32 main_grad += colsum(dy)
             elif need_db:
                 db = k.column_sum(d2)
+        if defer_b:
+            _defer_bias(bias, dpre)
 
         dx = None
         if ctx.needs_input_grad[0]:
@@ -128,6 +134,12 @@ def _defer(w: Tensor, dy: Tensor, x: Tensor) -> None:
     entry[2].append(x)
 
 
+def _defer_bias(b: Tensor, dy: Tensor) -> None:
+    """Bias gradients: column sums of every queued dY, ONE reduction per bias."""
+    entry = _DEFERRED.setdefault(id(b), (b, [], None))
+    entry[1].append(dy)
+
+
 def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
     """Weight gradient ``dy^T x`` of ``w`` (2-D operands) for ops with their own
     backward: into ``w.main_grad`` (deferred inside :func:`deferred_wgrad`) when
@@ -157,6 +169,9 @@ def flush_wgrad() -> None:
     queue, _DEFERRED = _DEFERRED, {}
     for w, dys, xs in queue.values():
         k = native_or_none(dys[0])
+        if xs is None:  # a bias
+            k.column_sum_segments(dys, w.main_grad, True)
+            continue
         T = dys[0].shape[0]
         uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
         if uniform and T % 64 == 0:

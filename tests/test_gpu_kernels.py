@@ -592,3 +592,33 @@ def test_vocab_split_decoder_gpu(k):
     assert rel(head.weight.grad, dec.weight.grad[:512]) < 2e-2
     assert rel(tail.weight.grad[:488], dec.weight.grad[512:1000]) < 2e-2
     assert rel(tail.bias.grad[:488], dec.bias.grad[512:1000]) < 2e-2
+
+
+def test_column_sum_segments(k):
+    torch.manual_seed(9)
+    xs = [torch.randn(r, 264, device=DEV).to(torch.bfloat16) for r in (128, 4096, 40)]
+    out = torch.randn(264, device=DEV)
+    expect = out + sum(x.float().sum(0) for x in xs)
+    k.column_sum_segments(xs, out, True)
+    assert torch.allclose(out, expect, atol=5e-2, rtol=1e-3)
+
+
+def test_deferred_bias_grad(k):
+    from mipipe import ops
+
+    torch.manual_seed(10)
+    w = (torch.randn(256, 128, device=DEV) / 12).to(torch.bfloat16).requires_grad_()
+    b = torch.zeros(256, device=DEV).to(torch.bfloat16).requires_grad_()
+    w.main_grad = torch.zeros(256, 128, device=DEV)
+    b.main_grad = torch.zeros(256, device=DEV)
+    gs = [torch.randn(64, 256, device=DEV).to(torch.bfloat16) for _ in range(3)]
+    xs = [torch.randn(64, 128, device=DEV).to(torch.bfloat16) for _ in range(3)]
+    with ops.deferred_wgrad():
+        for x, g in zip(xs, gs):
+            ops.linear(x, w, b, "relu", 0.0, True).backward(g)
+        assert b.main_grad.abs().max().item() == 0.0
+    expect = torch.zeros(256, device=DEV)
+    for x, g in zip(xs, gs):
+        pre = x.float() @ w.detach().float().t()
+        expect += (g.float() * (pre > 0).float()).sum(0)
+    assert ((b.main_grad - expect).abs().max() / expect.abs().max()).item() < 2e-2
