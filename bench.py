@@ -130,8 +130,11 @@ def main() -> int:
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
                             act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device)
-    sim_t, sim_busy = simulate_step([plan.stage_cost(g) for g in range(pp * virtual)], pp, virtual, m, bwd_ratio,
-                                    deferred_w=1.0 / bwd_ratio)
+    # explicit recompute (issued before each gradient wait, as the engine does)
+    from mipipe.pipeline import checkpoint_stop_for
+    sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
+                                    pp, virtual, m, 2.0, deferred_w=0.5,
+                                    checkpoint_stop=checkpoint_stop_for(args.checkpoint, m))
 
     g = torch.Generator(device="cpu").manual_seed(0)
     tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)

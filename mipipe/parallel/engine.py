@@ -293,13 +293,16 @@ class PipelineEngine:
             mod = self.modules[c]
             last = self._last(c)
             x = stage_in[c][i]
-            tm = self._timer()
-            if not last:
-                grad_w[c][i].wait()
-            if tm:
-                tm[0].record()
             if stage_out[c][i] is None:
+                # Recompute needs no gradient, so it is issued BEFORE the stream
+                # waits on the incoming gradient: the recomputed forward overlaps
+                # the gradient transfer and the downstream rank's backward, as
+                # the reference's Recompute node does (it hangs off a phony that
+                # is not ordered after Wait, /root/reference/pipeline.py:161-185).
                 # Recompute with the RNG state of the original forward.
+                tr = self._timer()
+                if tr:
+                    tr[0].record()
                 st = rng[c][i]
                 devices = [self.device] if self.device.type == "cuda" else []
                 with torch.random.fork_rng(devices=devices):
@@ -310,8 +313,16 @@ class PipelineEngine:
                         y = self._run(mod, x, targets, i)
                         if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
                             y = self._loss(mod, y, targets, i) / m
+                if tr:
+                    tr[1].record()
+                    events.append(("B", tr))
             else:
                 y = stage_out[c][i]
+            if not last:
+                grad_w[c][i].wait()
+            tm = self._timer()
+            if tm:
+                tm[0].record()
             if last:
                 y.backward()
             else:

@@ -10,7 +10,7 @@ attention and MLP halves of a layer.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 from torch import nn
@@ -134,7 +134,8 @@ def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
 
 
 def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks: int,
-                  bwd_ratio: float = 2.0, deferred_w: float = 0.0) -> Tuple[float, List[float]]:
+                  bwd_ratio: float = 2.0, deferred_w: float = 0.0,
+                  checkpoint_stop: Optional[int] = None) -> Tuple[float, List[float]]:
     """Event simulation of one synchronous step (breadth-first looping order,
     as :class:`~mipipe.parallel.engine.PipelineEngine` runs it; transfers free).
 
@@ -142,7 +143,14 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
     ``bwd_ratio`` x forward, of which the fraction ``deferred_w`` (weight
     gradients under ``defer_wgrad``) runs after the rank's last backward.
     Returns the makespan and per-rank busy time (bubble = 1 - mean busy /
-    makespan)."""
+    makespan).
+
+    With ``checkpoint_stop`` given, recompute is modelled explicitly instead
+    of being folded into ``bwd_ratio``: micro-batches ``i < checkpoint_stop``
+    run a recompute (one forward) right before their backward, and -- as the
+    engine issues it before its gradient wait -- the recompute does not wait
+    for the downstream gradient.  ``stage_costs`` then price forward +
+    ``bwd_ratio`` x forward WITHOUT recompute."""
     nv = ranks * virtual
     fwd = [c / (1.0 + bwd_ratio) for c in stage_costs]
     bwd_all = [c * bwd_ratio / (1.0 + bwd_ratio) for c in stage_costs]
@@ -150,8 +158,13 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
     wgt = [b * deferred_w for b in bwd_all]
     f_done = [[None] * chunks for _ in range(nv)]
     b_done = [[None] * chunks for _ in range(nv)]
+    stop = checkpoint_stop or 0
+
+    def _bwd(s: int, i: int) -> List[Tuple[str, int, int]]:
+        return ([("R", s, i)] if i < stop else []) + [("B", s, i)]
+
     order = {r: [("F", c * ranks + r, i) for c in range(virtual) for i in range(chunks)]
-             + [("B", c * ranks + r, i) for c in reversed(range(virtual)) for i in reversed(range(chunks))]
+             + [a for c in reversed(range(virtual)) for i in reversed(range(chunks)) for a in _bwd(c * ranks + r, i)]
              for r in range(ranks)}
     pos = [0] * ranks
     clock = [0.0] * ranks
@@ -171,6 +184,8 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
                     dur = fwd[s]
                 elif kind == "W":
                     dep, dur = 0.0, wgt[s]
+                elif kind == "R":
+                    dep, dur = 0.0, fwd[s]
                 else:
                     dep = f_done[s][i] if s == nv - 1 else b_done[s + 1][i]
                     dur = bwd[s]
@@ -179,7 +194,7 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
                 start = max(clock[r], dep)
                 clock[r] = start + dur
                 busy[r] += dur
-                if kind != "W":
+                if kind in ("F", "B"):
                     (f_done if kind == "F" else b_done)[s][i] = clock[r]
                 pos[r] += 1
                 remaining -= 1
