@@ -130,7 +130,7 @@ std::tuple<Tensor, std::optional<Tensor>, Tensor, Tensor, int64_t, int64_t> py_l
 // accumulated there and None is returned for them.
 std::tuple<Tensor, std::optional<Tensor>, std::optional<Tensor>, std::optional<Tensor>> py_layernorm_bwd(
     Tensor dy, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double p, int64_t seed, int64_t offset,
-    std::optional<Tensor> acc_gamma, std::optional<Tensor> acc_beta) {
+    std::optional<Tensor> acc_gamma, std::optional<Tensor> acc_beta, std::optional<Tensor> addend) {
   check_cuda(dy, "dy");
   check_cuda(z, "z");
   check_same(dy, z, "dy", "z");
@@ -140,6 +140,10 @@ std::tuple<Tensor, std::optional<Tensor>, std::optional<Tensor>, std::optional<T
   MP_CHECK(z.numel() == dy.numel(), "layernorm_bwd: shape mismatch");
   MP_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: stats size mismatch");
   MP_CHECK(cols % 8 == 0 && ln_max_vec((int)cols) > 0, "layernorm_bwd: bad hidden size");
+  if (addend) {
+    check_same(dy, *addend, "dy", "addend");
+    MP_CHECK(addend->numel() == dy.numel() && addend->is_contiguous(), "layernorm_bwd: addend must match dy");
+  }
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   auto dz = at::empty_like(dy);
   std::optional<Tensor> dx;
@@ -154,7 +158,7 @@ std::tuple<Tensor, std::optional<Tensor>, std::optional<Tensor>, std::optional<T
   }
   Tensor dgamma = acc ? *acc_gamma : at::empty_like(gamma);
   Tensor dbeta = acc ? *acc_beta : at::empty_like(gamma);
-  const int nparts = std::max(1, ln_bwd_parts((int)rows));
+  const int nparts = std::max(1, ln_bwd_parts((int)rows, (int)cols));
   auto part = at::empty({2, nparts, cols}, dy.options().dtype(at::kFloat));
   auto s = cur_stream(dy);
   std::optional<Tensor> rg, rb;
@@ -173,6 +177,7 @@ std::tuple<Tensor, std::optional<Tensor>, std::optional<Tensor>, std::optional<T
     using T = std::remove_pointer_t<decltype(tag)>;
     a.dy = cptr<T>(dy); a.z = cptr<T>(z); a.mean = cptr<float>(mean); a.rstd = cptr<float>(rstd);
     a.gamma = cptr<T>(gamma); a.dz = ptr<T>(dz); a.dx = dx ? ptr<T>(*dx) : nullptr;
+    a.addend = addend ? cptr<T>(*addend) : nullptr;
     a.dgamma_part = ptr<float>(part); a.dbeta_part = ptr<float>(part) + (size_t)nparts * cols;
     a.dgamma = dgamma.data_ptr(); a.dbeta = dbeta.data_ptr();
     a.out_f32 = dgamma.scalar_type() == at::kFloat; a.accumulate = acc;
@@ -272,7 +277,7 @@ Tensor py_column_sum(Tensor x, std::optional<Tensor> out, bool accumulate) {
     if (!accumulate) o.zero_();
     return o;
   }
-  const int nparts = colsum_parts(rows);
+  const int nparts = colsum_parts(rows, cols);
   auto part = at::empty({nparts, cols}, x.options().dtype(at::kFloat));
   auto s = cur_stream(x);
   dispatch_fb(x, "column_sum", [&](auto* tag) {
@@ -422,16 +427,23 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
 }
 
 // dx[M,K] = dy[M,N] . w[N,K]
-Tensor py_linear_dgrad(Tensor dy, Tensor w) {
+// dx = dy . w (+ res): `res` is the gradient the input receives from its
+// other consumer (a residual branch), added in the epilogue.
+Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
   check_bf16_2d(dy, "dy");
   check_bf16_2d(w, "w");
   const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
   MP_CHECK(w.size(0) == N, "linear_dgrad: inner dims differ");
   MP_CHECK(gemm_supported(M, K, N), "linear_dgrad: unsupported shape");
+  if (res) {
+    check_bf16_2d(*res, "res");
+    MP_CHECK(res->size(0) == M && res->size(1) == K && res->is_contiguous(), "linear_dgrad: res must be contiguous [M, K]");
+  }
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   auto dx = at::empty({M, K}, dy.options());
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = w.data_ptr(); g.C = dx.data_ptr();
+  if (res) g.res = res->data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)M; g.N = (int)K; g.K = (int)N;
   g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreBf16;
   gemm_bf16(g, cur_stream(dy));
@@ -473,7 +485,7 @@ void py_column_sum_segments(std::vector<Tensor> xs, Tensor out, bool accumulate)
     MP_CHECK(xs[i].is_contiguous() && xs[i].size(-1) == cols && xs[i].scalar_type() == xs[0].scalar_type(),
              "column_sum_segments: inputs must be contiguous with equal width and dtype");
     rows[i] = xs[i].numel() / std::max<int64_t>(cols, 1);
-    parts[i] = colsum_parts(rows[i]);
+    parts[i] = colsum_parts(rows[i], cols);
     total += parts[i];
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
@@ -670,7 +682,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_fwd", &py_layernorm_fwd);
   m.def("layernorm_bwd", &py_layernorm_bwd, py::arg("dy"), py::arg("z"), py::arg("mean"), py::arg("rstd"),
         py::arg("gamma"), py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("acc_gamma") = py::none(),
-        py::arg("acc_beta") = py::none());
+        py::arg("acc_beta") = py::none(), py::arg("addend") = py::none());
   m.def("bias_act_fwd", &py_bias_act_fwd);
   m.def("bias_act_bwd", &py_bias_act_bwd, py::arg("dy"), py::arg("saved"), py::arg("bias"), py::arg("act"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dbias"), py::arg("dbias_acc") = py::none());
@@ -688,7 +700,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 auto (default)");
   m.def("gemm_get_schedule", &gemm_get_schedule);
   m.def("linear_fwd", &py_linear_fwd);
-  m.def("linear_dgrad", &py_linear_dgrad);
+  m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none());
   m.def("linear_wgrad", &py_linear_wgrad);
   m.def("linear_wgrad_segments", &py_linear_wgrad_segments);
   m.def("column_sum_segments", &py_column_sum_segments);

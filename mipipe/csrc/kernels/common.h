@@ -147,10 +147,24 @@ __device__ __forceinline__ uint32_t dropout_keep4(uint64_t seed, uint64_t offset
          ((uint32_t)(r.w >= threshold) << 3);
 }
 
-// 8 consecutive elements starting at a multiple of 8 (two Philox groups).
+// 8 consecutive elements starting at a multiple of 8 from ONE Philox block:
+// element i draws the 16-bit uniform (word i/2 >> 16*(i&1)) and is kept iff it
+// is >= floor(p * 2^16).  The RNG is the VALU cost of a dropout pass (10
+// rounds x 4 quarter-rate multiplies per block), so halving the blocks per
+// element matters for the memory-bound LayerNorm / embedding kernels; p is
+// resolved to 1/65536 (0.2 -> 0.199997).
 __device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset, uint64_t elem8, uint32_t threshold) {
-  const uint64_t g = elem8 >> 2;  // elem8 is a multiple of 8 -> even group
-  return dropout_keep4(seed, offset, g, threshold) | (dropout_keep4(seed, offset, g + 1, threshold) << 4);
+  if (threshold == 0xFFFFFFFFu) return 0u;  // p >= 1: drop everything
+  const uint4 r = Philox(seed, elem8 >> 3, offset).next4();
+  const uint32_t t = threshold >> 16;
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  uint32_t keep = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    keep |= (uint32_t)((w[i] & 0xFFFFu) >= t) << (2 * i);
+    keep |= (uint32_t)((w[i] >> 16) >= t) << (2 * i + 1);
+  }
+  return keep;
 }
 
 __host__ __device__ inline uint32_t dropout_threshold(float p) {

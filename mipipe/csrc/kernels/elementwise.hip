@@ -90,23 +90,49 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
   }
 }
 
-// Stage 1 of a column sum: block b sums rows [b*rows_per, (b+1)*rows_per) of
-// each column owned by its threads (8 columns per thread, 16-byte loads).
+// Stage 1 of a column sum.  A block owns a 64-column strip of rows
+// [blockIdx.y * rows_per, ...): 8 column lanes x 8 columns (16-byte loads, a
+// wave reads 8 rows x 128 contiguous bytes) by 32 row lanes, each row lane
+// summing every 32nd row with 4 loads in flight; the 32 row sums of each
+// column are folded through LDS and the block writes ONE partial row.  Parts
+// cover >= 256 rows each, so the partial image stays small (<= 64 rows) and
+// the second stage (reduce_parts) is a launch, not a second pass.
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ x, int rows, int cols, int rows_per,
                                                           float* __restrict__ part) {
-  const int nvec = cols >> 3;
+  __shared__ float sm[32][65];
+  const int cx = threadIdx.x & 7, ry = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * 64 + cx * 8;
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(rows, r0 + rows_per);
-  for (int vi = blockIdx.x * blockDim.x + threadIdx.x; vi < nvec; vi += gridDim.x * blockDim.x) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int r = r0; r < r1; ++r) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < cols) {
+    int r = r0 + ry;
+    for (; r + 96 < r1; r += 128) {
+      float a[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Io<T>::load8(x + (size_t)(r + 32 * u) * cols + c0, a[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += a[u][i];
+    }
+    for (; r < r1; r += 32) {
       float a[8];
-      Io<T>::load8(x + (size_t)r * cols + vi * 8, a);
+      Io<T>::load8(x + (size_t)r * cols + c0, a);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += a[i];
     }
-    Io<float>::store8(part + (size_t)blockIdx.y * cols + vi * 8, acc);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sm[ry][cx * 8 + i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) s += sm[k][threadIdx.x];
+    if (c < cols) part[(size_t)blockIdx.y * cols + c] = s;
   }
 }
 
@@ -157,12 +183,19 @@ void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int
   launch_bias_act<T, true>(dy, saved, bias, dx, rows, cols, act, p, seed, offset, s);
 }
 
-int colsum_parts(int64_t rows) {
-  // ~16 rows per part: enough workgroups in stage 1 to stream at HBM rate
-  // (4096 rows x 4096 cols -> 256 parts x 2 column blocks); stage 2 reads the
-  // 4 MiB of partials with 64 coalesced workgroups.
-  int64_t parts = (rows + 15) / 16;
-  return (int)(parts < 1 ? 1 : (parts > 512 ? 512 : parts));
+int colsum_parts(int64_t rows, int64_t cols) {
+  if (cols % 8 != 0) {
+    // scalar path: ~16 rows per part keeps enough one-column threads in flight
+    int64_t parts = (rows + 15) / 16;
+    return (int)(parts < 1 ? 1 : (parts > 512 ? 512 : parts));
+  }
+  // 2-D tiled path: >= 256 rows per part and >= ~1024 blocks when the shape
+  // allows it (4096 x 4096 -> 64 strips x 16 parts).
+  const int64_t strips = (cols + 63) / 64;
+  int64_t parts = (rows + 255) / 256;
+  const int64_t want = (1024 + strips - 1) / strips;
+  if (parts > want) parts = want;
+  return (int)(parts < 1 ? 1 : (parts > 64 ? 64 : parts));
 }
 
 template <typename T>
@@ -170,8 +203,7 @@ void column_sum_partial(const T* x, int64_t rows, int cols, float* part, int npa
   if (rows == 0 || cols == 0) return;
   const int rows_per = (int)((rows + nparts - 1) / nparts);
   if (cols % 8 == 0) {
-    const int nvec = cols / 8;
-    dim3 g1((unsigned)((nvec + 255) / 256), (unsigned)nparts);
+    dim3 g1((unsigned)((cols + 63) / 64), (unsigned)nparts);
     hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
   } else {
     dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);
@@ -185,8 +217,7 @@ void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, voi
   if (rows == 0 || cols == 0) return;
   const int rows_per = (int)((rows + nparts - 1) / nparts);
   if (cols % 8 == 0) {
-    const int nvec = cols / 8;
-    dim3 g1((unsigned)((nvec + 255) / 256), (unsigned)nparts);
+    dim3 g1((unsigned)((cols + 63) / 64), (unsigned)nparts);
     hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
   } else {
     dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);

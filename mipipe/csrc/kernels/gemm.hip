@@ -27,7 +27,9 @@
 // Epilogues:
 //   kEpiStoreBf16 -- + bias, activation (ReLU/GELU), dropout (Philox mask in
 //                    the "column-quad" layout shared with the elementwise
-//                    backward), optional pre-activation aux output, bf16 store;
+//                    backward), optional pre-activation aux output, optional
+//                    bf16 addend `res` (a fan-out's other gradient: the
+//                    autograd add kernel folded into the dgrad), bf16 store;
 //   kEpiAccumF32  -- C(fp32) += acc  (weight gradients straight into main_grad);
 //   kEpiStoreF32  -- fp32 store.
 #include "common.h"
@@ -232,6 +234,7 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          if (g.res != nullptr) out[r] += bf2f(reinterpret_cast<const bf16_t*>(g.res)[(int64_t)(row0 + r) * g.ldc + col]);
           C[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out[r]);
           if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre[r]);
         }
@@ -492,30 +495,54 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   const int quad = lane >> 4, col_in = lane & 15;
   const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
   if (EPI == kEpiStoreBf16) {
+    // With a residual addend, the addend values of half the lane's rows (64)
+    // are loaded before that half's first store (in program order, so no
+    // aliasing question serialises them): 64 loads in flight instead of one
+    // per store, within the 256-VGPR budget of 2 waves/SIMD.
+    const bool has_res = g.res != nullptr;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
+    for (int half = 0; half < 2; ++half) {
+      bf16_t rv[4][4][4];
+      if (has_res) {
+        const bf16_t* R = reinterpret_cast<const bf16_t*>(g.res);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // Predicated (never continue/break: the accumulator array must stay
-        // fully unrolled in registers -- an early exit spills it to scratch).
-        const int col = n0 + wn * 64 + 16 * j + col_in;
-        const bool col_ok = col < g.N;
-        const float b = (g.bias != nullptr && col_ok) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
-        uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        if (g.p > 0.f) {
-          const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
-          const uint4 w = Philox(g.seed, sub, g.offset).next4();
-          ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
-        }
+        for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pre = acc[i][j][r] + b;
-          float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
-          if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
-          if (col_ok && row0 + r < g.M) {
-            reinterpret_cast<bf16_t*>(g.C)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out);
-            if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre);
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = m0 + wm * 128 + 16 * (4 * half + ii) + 4 * quad + r;
+              const int col = n0 + wn * 64 + 16 * j + col_in;
+              rv[ii][j][r] = (col < g.N && row < g.M) ? R[(int64_t)row * g.ldc + col] : (bf16_t)0;
+            }
+      }
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = 4 * half + ii;
+        const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // Predicated (never continue/break: the accumulator array must stay
+          // fully unrolled in registers -- an early exit spills it to scratch).
+          const int col = n0 + wn * 64 + 16 * j + col_in;
+          const bool col_ok = col < g.N;
+          const float b = (g.bias != nullptr && col_ok) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
+          uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+          if (g.p > 0.f) {
+            const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
+            const uint4 w = Philox(g.seed, sub, g.offset).next4();
+            ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pre = acc[i][j][r] + b;
+            float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
+            if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
+            if (has_res) out += bf2f(rv[ii][j][r]);
+            if (col_ok && row0 + r < g.M) {
+              reinterpret_cast<bf16_t*>(g.C)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out);
+              if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre);
+            }
           }
         }
       }

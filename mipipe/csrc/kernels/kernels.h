@@ -37,6 +37,7 @@ struct LnBwdArgs {
   const float* rstd = nullptr;
   const T* gamma = nullptr;
   T* dz = nullptr;           // grad of z (= grad of the residual input)
+  const T* addend = nullptr; // optional extra gradient of z, added to dz (fan-out fusion)
   T* dx = nullptr;           // grad of the dropout branch (nullptr if p == 0)
   float* dgamma_part = nullptr;  // [nparts, cols] workspace
   float* dbeta_part = nullptr;
@@ -54,7 +55,7 @@ void reduce_parts(const float* part_a, const float* part_b, int nparts, int cols
                   bool out_f32, bool accumulate, hipStream_t s);
 
 int ln_max_vec(int cols);
-int ln_bwd_parts(int rows);
+int ln_bwd_parts(int rows, int cols);
 template <typename T> void layernorm_fwd(const LnArgs<T>& a, hipStream_t s);
 template <typename T> void layernorm_bwd(const LnBwdArgs<T>& a, hipStream_t s);
 
@@ -67,7 +68,7 @@ void bias_act_dropout_fwd(const T* x, const T* bias, T* y, int64_t rows, int col
 template <typename T>
 void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int64_t rows, int cols, int act, float p,
                           uint64_t seed, uint64_t offset, hipStream_t s);
-int colsum_parts(int64_t rows);
+int colsum_parts(int64_t rows, int64_t cols);
 // Stage 1 only: per-part column sums of `rows` rows into part[nparts][cols]
 // (several inputs can write disjoint part slices and share one reduce_parts).
 template <typename T>
@@ -85,6 +86,7 @@ struct GemmArgs {
   void* C = nullptr;        // bf16 or fp32 (epilogue)
   const void* bias = nullptr;  // bf16 [N] (kEpiStoreBf16 only)
   void* aux = nullptr;         // bf16 pre-activation output (optional)
+  const void* res = nullptr;   // bf16 [M, ldc] added to the bf16 output (optional, kEpiStoreBf16)
   int64_t lda = 0, ldb = 0, ldc = 0;
   int M = 0, N = 0, K = 0;
   bool a_kc = true;   // A stored [M, K] (true) or [K, M] (false)

@@ -93,13 +93,35 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(
   }
 }
 
-template <typename T, int MAXV>
-__global__ void __launch_bounds__(kThreads) ln_bwd_kernel(
+// Row reduction of a pair over one 256-thread row group of a G-group block
+// (every thread of the block calls it: the barriers are block-wide).
+template <int G>
+__device__ __forceinline__ void group_sum2(float& a, float& b, float (*scratch)[8], int grp, int t) {
+  const int lane = t & 63, wid = t >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane == 0) {
+    scratch[grp][wid] = a;
+    scratch[grp][4 + wid] = b;
+  }
+  __syncthreads();
+  a = scratch[grp][0] + scratch[grp][1] + scratch[grp][2] + scratch[grp][3];
+  b = scratch[grp][4] + scratch[grp][5] + scratch[grp][6] + scratch[grp][7];
+  __syncthreads();
+}
+
+// G row groups of 256 threads per block, each on its own row; the groups'
+// dgamma/dbeta partials are folded through LDS so a block writes ONE partial
+// row pair (G = 2 halves the partial image the second stage re-reads).
+template <typename T, int MAXV, int G>
+__global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ z, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const T* __restrict__ gamma, T* __restrict__ dz, T* __restrict__ dx,
     float* __restrict__ dgamma_part, float* __restrict__ dbeta_part, int rows, int cols, float p,
-    uint32_t threshold, uint64_t seed, uint64_t offset) {
-  __shared__ float scratch[2 * (kThreads / 64)];
+    uint32_t threshold, uint64_t seed, uint64_t offset, const T* __restrict__ addend) {
+  __shared__ float scratch[G][8];
+  __shared__ float fold[G > 1 ? 2 * MAXV * 8 * kThreads : 1];
+  const int grp = threadIdx.x / kThreads, t = threadIdx.x % kThreads;
   const int nvec = cols >> 3;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
 
@@ -107,20 +129,25 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(
   float dg[MAXV][8], db[MAXV][8];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
-    const int vi = threadIdx.x + k * kThreads;
+    const int vi = t + k * kThreads;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dg[k][i] = db[k][i] = 0.f;
+    for (int i = 0; i < 8; ++i) dg[k][i] = db[k][i] = g[k][i] = 0.f;
     if (vi < nvec) Io<T>::load8(gamma + vi * 8, g[k]);
   }
 
   // Rows are software-pipelined: the next row's z / dy loads are in flight
-  // while this row's reductions and stores run (a block walks rows/grid rows).
+  // while this row's reductions and stores run.
+  const int stride = gridDim.x * G;
+  const int iters = (rows + stride - 1) / stride;  // uniform over the block (barriers inside)
+  auto row_of = [&](int it) { return it * stride + blockIdx.x * G + grp; };
   float zn[MAXV][8], dn[MAXV][8];
   auto load_row = [&](int row) {
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      const int vi = threadIdx.x + k * kThreads;
-      if (vi < nvec) {
+      const int vi = t + k * kThreads;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zn[k][i] = dn[k][i] = 0.f;
+      if (vi < nvec && row < rows) {
         const size_t e = (size_t)row * cols + (size_t)vi * 8;
         Io<T>::load8(z + e, zn[k]);
         Io<T>::load8(dy + e, dn[k]);
@@ -128,11 +155,13 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(
     }
   };
   constexpr bool kPrefetch = MAXV <= 2;  // wider rows: the extra row would spill
-  if (kPrefetch && blockIdx.x < rows) load_row(blockIdx.x);
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  if (kPrefetch) load_row(row_of(0));
+  for (int it = 0; it < iters; ++it) {
+    const int row = row_of(it);
+    const bool valid = row < rows;
     const size_t base = (size_t)row * cols;
-    const float mean = mean_in[row];
-    const float rstd = rstd_in[row];
+    const float mean = valid ? mean_in[row] : 0.f;
+    const float rstd = valid ? rstd_in[row] : 0.f;
     if (!kPrefetch) load_row(row);
     float zc[MAXV][8], dc[MAXV][8];
 #pragma unroll
@@ -142,57 +171,85 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(
         zc[k][i] = zn[k][i];
         dc[k][i] = dn[k][i];
       }
-    if (kPrefetch && row + (int)gridDim.x < rows) load_row(row + gridDim.x);
+    if (kPrefetch && it + 1 < iters) load_row(row_of(it + 1));
     float xh[MAXV][8], gy[MAXV][8];
     float a = 0.f, b = 0.f;  // sum(g*dy), sum(g*dy*xhat)
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      const int vi = threadIdx.x + k * kThreads;
-      if (vi < nvec) {
-        const float* zz = zc[k];
-        const float* d = dc[k];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          xh[k][i] = (zz[i] - mean) * rstd;
-          gy[k][i] = d[i] * g[k][i];
-          dg[k][i] += d[i] * xh[k][i];
-          db[k][i] += d[i];
-          a += gy[k][i];
-          b += gy[k][i] * xh[k][i];
-        }
+      for (int i = 0; i < 8; ++i) {
+        xh[k][i] = (zc[k][i] - mean) * rstd;
+        gy[k][i] = dc[k][i] * g[k][i];
+        dg[k][i] += dc[k][i] * xh[k][i];
+        db[k][i] += dc[k][i];
+        a += gy[k][i];
+        b += gy[k][i] * xh[k][i];
       }
     }
-    block_sum2(a, b, scratch);
+    group_sum2<G>(a, b, scratch, grp, t);
     const float inv_n = 1.f / (float)cols;
     a *= inv_n;
     b *= inv_n;
+    if (valid) {
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      const int vi = threadIdx.x + k * kThreads;
-      if (vi < nvec) {
-        const size_t e = base + (size_t)vi * 8;
-        float o[8];
+      for (int k = 0; k < MAXV; ++k) {
+        const int vi = t + k * kThreads;
+        if (vi < nvec) {
+          const size_t e = base + (size_t)vi * 8;
+          float o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = rstd * (gy[k][i] - a - xh[k][i] * b);
-        Io<T>::store8(dz + e, o);
-        if (dx != nullptr) {
-          const uint32_t keep = dropout_keep8(seed, offset, e, threshold);
+          for (int i = 0; i < 8; ++i) o[i] = rstd * (gy[k][i] - a - xh[k][i] * b);
+          if (addend != nullptr) {
+            float ad[8];
+            Io<T>::load8(addend + e, ad);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = ((keep >> i) & 1) ? o[i] * scale : 0.f;
-          Io<T>::store8(dx + e, o);
+            for (int i = 0; i < 8; ++i) o[i] += ad[i];
+          }
+          Io<T>::store8(dz + e, o);
+          if (dx != nullptr) {
+            const uint32_t keep = dropout_keep8(seed, offset, e, threshold);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = ((keep >> i) & 1) ? o[i] * scale : 0.f;
+            Io<T>::store8(dx + e, o);
+          }
         }
       }
     }
   }
+  if constexpr (G > 1) {
+    // groups 1..G-1 hand their partials to group 0 through LDS, one at a time
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = threadIdx.x + k * kThreads;
-    if (vi < nvec) {
-      const size_t o = (size_t)blockIdx.x * cols + vi * 8;
+    for (int src = 1; src < G; ++src) {
+      if (grp == src) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        dgamma_part[o + i] = dg[k][i];
-        dbeta_part[o + i] = db[k][i];
+        for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            fold[((0 * MAXV + k) * 8 + i) * kThreads + t] = dg[k][i];
+            fold[((1 * MAXV + k) * 8 + i) * kThreads + t] = db[k][i];
+          }
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            dg[k][i] += fold[((0 * MAXV + k) * 8 + i) * kThreads + t];
+            db[k][i] += fold[((1 * MAXV + k) * 8 + i) * kThreads + t];
+          }
+      }
+      __syncthreads();
+    }
+  }
+  if (grp == 0) {
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = t + k * kThreads;
+      if (vi < nvec) {
+        const size_t o = (size_t)blockIdx.x * cols + vi * 8;
+        Io<float>::store8(dgamma_part + o, dg[k]);
+        Io<float>::store8(dbeta_part + o, db[k]);
       }
     }
   }
@@ -206,9 +263,11 @@ void launch_fwd(const LnArgs<T>& a, hipStream_t s) {
 
 template <typename T, int MAXV>
 void launch_bwd(const LnBwdArgs<T>& a, hipStream_t s) {
-  hipLaunchKernelGGL((ln_bwd_kernel<T, MAXV>), dim3(a.nparts), dim3(kThreads), 0, s, a.dy, a.z, a.mean, a.rstd,
-                     a.gamma, a.dz, a.dx, a.dgamma_part, a.dbeta_part, a.rows, a.cols, a.p,
-                     dropout_threshold(a.p), a.seed, a.offset);
+  // one partial row pair per block (a.nparts blocks, see ln_bwd_parts)
+  constexpr int G = MAXV <= 2 ? 2 : 1;
+  hipLaunchKernelGGL((ln_bwd_kernel<T, MAXV, G>), dim3(a.nparts), dim3(kThreads * G), 0, s, a.dy, a.z, a.mean,
+                     a.rstd, a.gamma, a.dz, a.dx, a.dgamma_part, a.dbeta_part, a.rows, a.cols, a.p,
+                     dropout_threshold(a.p), a.seed, a.offset, a.addend);
   reduce_parts(a.dgamma_part, a.dbeta_part, a.nparts, a.cols, a.dgamma, a.dbeta, a.out_f32, a.accumulate, s);
 }
 
@@ -223,7 +282,12 @@ int ln_max_vec(int cols) {
   return -1;
 }
 
-int ln_bwd_parts(int rows) { return rows < 512 ? rows : 512; }
+int ln_bwd_parts(int rows, int cols) {
+  // blocks of 2 x 256 threads for rows up to 4096 wide (2048 waves in flight
+  // at 256 blocks), single-group blocks of 256 beyond
+  const int cap = ln_max_vec(cols) <= 2 ? 256 : 512;
+  return rows < cap ? (rows < 1 ? 1 : rows) : cap;
+}
 
 template <typename T>
 void layernorm_fwd(const LnArgs<T>& a, hipStream_t s) {

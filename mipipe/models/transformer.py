@@ -22,12 +22,17 @@ blocks can be checked against PyTorch.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
 from torch import Tensor, nn
 
 from .. import ops
+
+# Fan-out fusion of the residual-branch gradient (see AttentionCore.forward_fanout);
+# MIPIPE_FANOUT=0 turns it off (A/B measurements).
+FANOUT = os.environ.get("MIPIPE_FANOUT", "1") != "0"
 
 __all__ = [
     "AttentionCore",
@@ -74,16 +79,32 @@ class AttentionCore(nn.Module):
             nn.init.zeros_(self.norm_bias)
 
     def forward(self, x: Tensor) -> Tensor:
+        return self.forward_fanout(x, fanout=False)[0]
+
+    def forward_fanout(self, x: Tensor, fanout: bool = True):
+        """``(o, x')``: ``x'`` is the block input for the residual branch.  With
+        ``fanout`` the first consumer of ``x`` (LN1 for pre-norm, the QKV
+        projection for post-norm) also returns it, so the residual gradient is
+        added inside that op's backward kernel (no autograd add pass)."""
         B, S, E = x.shape
         H, D = self.nhead, self.head_dim
+        xr = x
         if self.norm_first:
-            x = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
-        qkv = ops.linear(x, self.in_proj_weight, self.in_proj_bias)
+            if fanout:
+                x, xr = ops.layer_norm_fanout(x, self.norm_weight, self.norm_bias, self.eps)
+            else:
+                x = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0,
+                                               self.training)
+            qkv = ops.linear(x, self.in_proj_weight, self.in_proj_bias)
+        elif fanout:
+            qkv, xr = ops.linear_fanout(x, self.in_proj_weight, self.in_proj_bias)
+        else:
+            qkv = ops.linear(x, self.in_proj_weight, self.in_proj_bias)
         # The projection output viewed as [B, S, 3, H, D] feeds the kernel in
         # place; its output [B, S, H, D] is already [B, S, E] -- no transposes.
         o = ops.attention_packed(qkv.view(B, S, 3, H, D), causal=self.causal, dropout_p=self.dropout,
                                  training=self.training)
-        return o.reshape(B, S, E)
+        return o.reshape(B, S, E), xr
 
     def flops_per_token(self, seq_len: int) -> float:
         e = self.d_model
@@ -147,7 +168,8 @@ class SelfAttentionBlock(nn.Module):
         self.out.reset_parameters()
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.out(x, self.core(x))
+        o, xr = self.core.forward_fanout(x, FANOUT)
+        return self.out(xr, o)
 
     def flops_per_token(self, seq_len: int) -> float:
         return self.core.flops_per_token(seq_len) + self.out.flops_per_token(seq_len)
@@ -213,10 +235,22 @@ class FeedForwardIn(nn.Module):
             nn.init.zeros_(self.norm_bias)
 
     def forward(self, x: Tensor) -> Tensor:
+        return self.forward_fanout(x, fanout=False)[0]
+
+    def forward_fanout(self, x: Tensor, fanout: bool = True):
+        """``(h, x')`` -- see :meth:`AttentionCore.forward_fanout`."""
         p = self.dropout if self.training else 0.0
+        w, b, act = self.linear1_weight, self.linear1_bias, self.activation
         if self.norm_first:
-            x = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0, self.training)
-        return ops.linear(x, self.linear1_weight, self.linear1_bias, self.activation, p, self.training)
+            if fanout:
+                xn, xr = ops.layer_norm_fanout(x, self.norm_weight, self.norm_bias, self.eps)
+            else:
+                xn, xr = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0,
+                                                    self.training), x
+            return ops.linear(xn, w, b, act, p, self.training), xr
+        if fanout:
+            return ops.linear_fanout(x, w, b, act, p, self.training)
+        return ops.linear(x, w, b, act, p, self.training), x
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2 * self.d_model * self.dim_feedforward
@@ -286,7 +320,8 @@ class FeedForwardBlock(nn.Module):
         self.fc_out.reset_parameters()
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.fc_out(x, self.fc_in(x))
+        h, xr = self.fc_in.forward_fanout(x, FANOUT)
+        return self.fc_out(xr, h)
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2 * 2 * self.d_model * self.dim_feedforward

@@ -5,8 +5,8 @@ Each op has one GPU implementation -- a hand-written CDNA4 HIP kernel in
 CPU tensors (plumbing tests).  GPU tensors never fall back to eager PyTorch:
 a missing extension raises (``mipipe._native_loader.kernels``).
 """
-from .layernorm import add_dropout_layer_norm, layer_norm_reference
-from .linear import deferred_wgrad, flush_wgrad, linear
+from .layernorm import add_dropout_layer_norm, layer_norm_fanout, layer_norm_reference
+from .linear import deferred_wgrad, flush_wgrad, linear, linear_fanout
 from .attention import attention, attention_packed, attention_reference
 from .activation import bias_act_dropout
 from .loss import cross_entropy
@@ -14,8 +14,10 @@ from .embedding import embed_scale_posenc_dropout
 
 __all__ = [
     "add_dropout_layer_norm",
+    "layer_norm_fanout",
     "layer_norm_reference",
     "linear",
+    "linear_fanout",
     "deferred_wgrad",
     "flush_wgrad",
     "attention",

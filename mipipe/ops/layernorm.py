@@ -14,7 +14,7 @@ from torch import Tensor
 
 from ._util import native_or_none
 
-__all__ = ["add_dropout_layer_norm", "layer_norm_reference"]
+__all__ = ["add_dropout_layer_norm", "layer_norm_fanout", "layer_norm_reference"]
 
 
 def layer_norm_reference(
@@ -28,7 +28,8 @@ def layer_norm_reference(
 
 class _AddDropoutLayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, p):  # type: ignore[override]
+    def forward(ctx, x, residual, weight, bias, eps, p, fanout=False):  # type: ignore[override]
+        ctx.set_materialize_grads(False)
         k = native_or_none(x)
         xc = x.contiguous()
         rc = residual.contiguous() if residual is not None else None
@@ -39,25 +40,34 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
         ctx.offset = offset
         ctx.has_residual = residual is not None
         ctx.bias_main_grad = getattr(bias, "main_grad", None)
+        if fanout:
+            # x again for its other consumer (pre-norm residual); its gradient
+            # is added to dx inside the LayerNorm backward kernel
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):  # type: ignore[override]
+    def backward(ctx, dy, dfan=None):  # type: ignore[override]
         z, mean, rstd, weight = ctx.saved_tensors
+        if dy is None:  # only the fan-out branch carries a gradient
+            return dfan, None, None, None, None, None, None
         k = native_or_none(dy)
         mg = getattr(weight, "main_grad", None)
         mb = ctx.bias_main_grad
+        add = dfan.contiguous() if dfan is not None and dfan.dtype == dy.dtype else None
         if mg is not None and mb is not None:
             # dgamma/dbeta accumulate straight into the fp32 main_grad buffers
             dz, dx, dgamma, dbeta = k.layernorm_bwd(dy.contiguous(), z, mean, rstd, weight, ctx.p, ctx.seed,
-                                                    ctx.offset, mg, mb)
+                                                    ctx.offset, mg, mb, add)
         else:
             dz, dx, dgamma, dbeta = k.layernorm_bwd(dy.contiguous(), z, mean, rstd, weight, ctx.p, ctx.seed,
-                                                    ctx.offset)
+                                                    ctx.offset, None, None, add)
         if dx is None:
             dx = dz
+        if dfan is not None and add is None:
+            dx = dx + dfan
         dres = dz if ctx.has_residual else None
-        return dx, dres, dgamma, dbeta, None, None
+        return dx, dres, dgamma, dbeta, None, None, None
 
 
 def add_dropout_layer_norm(
@@ -74,3 +84,12 @@ def add_dropout_layer_norm(
     if not x.is_cuda:
         return layer_norm_reference(x, residual, weight, bias, eps, p, True)
     return _AddDropoutLayerNorm.apply(x, residual, weight, bias, float(eps), p)
+
+
+def layer_norm_fanout(x: Tensor, weight: Tensor, bias: Tensor, eps: float = 1e-5):
+    """``(LayerNorm(x), x')``: ``x'`` is ``x`` for its other consumer (the
+    pre-norm residual ``x' + f(LN(x))``); the gradient reaching ``x'`` is added
+    inside the LayerNorm backward kernel instead of by an autograd add kernel."""
+    if not x.is_cuda or not torch.is_grad_enabled() or not x.requires_grad:
+        return add_dropout_layer_norm(x, None, weight, bias, eps, 0.0, True), x
+    return _AddDropoutLayerNorm.apply(x, None, weight, bias, float(eps), 0.0, True)

@@ -25,7 +25,7 @@ from torch import Tensor
 from ._util import native_or_none
 from .activation import ACTIVATIONS, bias_act_reference
 
-__all__ = ["linear", "deferred_wgrad", "flush_wgrad", "accumulate_wgrad"]
+__all__ = ["linear", "linear_fanout", "deferred_wgrad", "flush_wgrad", "accumulate_wgrad"]
 
 
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
@@ -42,7 +42,8 @@ def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, act, p):  # type: ignore[override]
+    def forward(ctx, x, weight, bias, act, p, fanout=False):  # type: ignore[override]
+        ctx.set_materialize_grads(False)
         k = native_or_none(x)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
@@ -64,11 +65,18 @@ class _Linear(torch.autograd.Function):
         ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
         ctx.fused_tile = fused_tile
         ctx.in_shape = shape
-        return y.view(*shape[:-1], w.shape[0])
+        y = y.view(*shape[:-1], w.shape[0])
+        if fanout:
+            # the input again, for its other consumer: its gradient comes back
+            # to this node and is added in the dgrad GEMM's epilogue
+            return y, x.view_as(x)
+        return y
 
     @staticmethod
-    def backward(ctx, dy):  # type: ignore[override]
+    def backward(ctx, dy, dres=None):  # type: ignore[override]
         x2, w, bias, saved = ctx.saved_tensors
+        if dy is None:  # only the fan-out branch carries a gradient
+            return dres, None, None, None, None, None
         k = native_or_none(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
@@ -95,11 +103,18 @@ class _Linear(torch.autograd.Function):
 
         dx = None
         if ctx.needs_input_grad[0]:
+            r2 = None
+            if dres is not None:
+                r2 = dres.reshape(-1, dres.shape[-1])
+                if not (ctx.fused_tile and r2.dtype == torch.bfloat16 and r2.is_contiguous()):
+                    r2 = None
             if ctx.fused_tile:
-                dx = k.linear_dgrad(dpre, w)
+                dx = k.linear_dgrad(dpre, w, r2)
             else:
                 dx = torch.matmul(dpre, w)
             dx = dx.view(ctx.in_shape)
+            if dres is not None and r2 is None:
+                dx = dx + dres
 
         dw = None
         if ctx.needs_input_grad[1]:
@@ -112,7 +127,7 @@ class _Linear(torch.autograd.Function):
                 main.add_(torch.matmul(dpre.t(), x2).float())
             else:
                 dw = torch.matmul(dpre.t(), x2)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 # ---------------------------------------------------------------- deferred wgrad
@@ -215,3 +230,22 @@ def linear(
         y = F.linear(x, weight)
         return bias_act_reference(y, bias, activation, p, True)
     return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p)
+
+
+def linear_fanout(
+    x: Tensor,
+    weight: Tensor,
+    bias: Optional[Tensor] = None,
+    activation: Optional[str] = None,
+    dropout_p: float = 0.0,
+    training: bool = True,
+):
+    """``(linear(x, ...), x')`` where ``x'`` is ``x`` for the input's OTHER
+    consumer (a post-norm residual branch).  Mathematically the identity; the
+    point is the backward: the gradient reaching ``x'`` is added to ``dx`` in
+    the dgrad GEMM's epilogue instead of by a separate autograd add kernel
+    (one full read/write pass of the activation per fan-out)."""
+    if not x.is_cuda or not torch.is_grad_enabled() or not x.requires_grad:
+        return linear(x, weight, bias, activation, dropout_p, training), x
+    p = float(dropout_p) if training else 0.0
+    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p, True)
