@@ -314,8 +314,9 @@ std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignor
 
 // out (optional): [N, >= V] destination with unit column stride (e.g. a
 // zero-padded vocabulary buffer); row_scale (optional): per-row scale, see loss.hip.
+// zero_pad: columns [V, out.size(1)) of `out` are zeroed (padded-vocabulary gradient).
 Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, std::optional<Tensor> scale, int64_t ignore_index,
-                 std::optional<Tensor> row_scale, std::optional<Tensor> out) {
+                 std::optional<Tensor> row_scale, std::optional<Tensor> out, bool zero_pad) {
   check_rows(logits, "logits");
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0) && lse.numel() == logits.size(0),
            "cross_entropy_bwd: shape mismatch");
@@ -340,7 +341,8 @@ Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, std::optional<Tensor>
     using T = std::remove_pointer_t<decltype(tag)>;
     cross_entropy_bwd<T>(cptr<T>(logits), cptr<int64_t>(target), cptr<float>(lse),
                          scale ? cptr<float>(*scale) : nullptr, row_scale ? cptr<float>(*row_scale) : nullptr,
-                         logits.size(0), logits.size(1), logits.stride(0), d.stride(0), ignore_index, ptr<T>(d), s);
+                         logits.size(0), logits.size(1), logits.stride(0), d.stride(0), ignore_index, ptr<T>(d),
+                         zero_pad ? d.size(1) : logits.size(1), s);
   });
   return d;
 }
@@ -636,8 +638,13 @@ void py_adam(Tensor master, std::optional<Tensor> model, Tensor grad, Tensor m, 
     check_cuda(*t, "adam buffer");
     MP_CHECK(t->scalar_type() == at::kFloat, "adam: master/grad/m/v must be fp32");
     MP_CHECK(t->numel() == master.numel(), "adam: size mismatch");
+    MP_CHECK(t->is_contiguous() && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+             "adam: buffers must be contiguous and 16-byte aligned (vectorised kernel)");
   }
-  if (model) MP_CHECK(model->numel() == master.numel() && model->is_contiguous(), "adam: model size mismatch");
+  if (model) {
+    MP_CHECK(model->numel() == master.numel() && model->is_contiguous(), "adam: model size mismatch");
+    MP_CHECK(reinterpret_cast<uintptr_t>(model->data_ptr()) % 16 == 0, "adam: model copy must be 16-byte aligned");
+  }
   if (sumsq_t) MP_CHECK(sumsq_t->scalar_type() == at::kFloat && sumsq_t->numel() == 1, "adam: bad sumsq");
   at::hip::HIPGuardMasqueradingAsCUDA guard(master.device());
   AdamHyper h;
@@ -689,7 +696,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("column_sum", &py_column_sum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cross_entropy_fwd", &py_ce_fwd);
   m.def("cross_entropy_bwd", &py_ce_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("scale"),
-        py::arg("ignore_index"), py::arg("row_scale") = py::none(), py::arg("out") = py::none());
+        py::arg("ignore_index"), py::arg("row_scale") = py::none(), py::arg("out") = py::none(),
+        py::arg("zero_pad") = false);
   m.def("embedding_fwd", &py_embed_fwd);
   m.def("embedding_bwd", &py_embed_bwd);
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });

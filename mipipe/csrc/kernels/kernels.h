@@ -146,7 +146,7 @@ void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int
 template <typename T>
 void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale,
                        const float* row_scale, int64_t rows, int64_t V, int64_t ld, int64_t ld_out,
-                       int64_t ignore_index, T* dlogits, hipStream_t s);
+                       int64_t ignore_index, T* dlogits, int64_t zero_to, hipStream_t s);
 
 // ------------------------------------------------------------------ embedding
 template <typename T>

@@ -85,6 +85,28 @@ class Encoder(nn.Module):
         return 0.0
 
 
+class _VocabSlice(torch.autograd.Function):
+    """``y[..., :V]`` of the padded logits.  Backward: when the incoming
+    gradient is the fused cross-entropy's zero-padded buffer (its usual
+    producer), that buffer IS the padded gradient -- no zero-fill + copy."""
+
+    @staticmethod
+    def forward(ctx, y, v):  # type: ignore[override]
+        ctx.shape = y.shape
+        return y[..., :v]
+
+    @staticmethod
+    def backward(ctx, g):  # type: ignore[override]
+        from ..ops.loss import take_zero_padded
+
+        width = ctx.shape[-1]
+        if take_zero_padded(g, width):
+            return torch.as_strided(g, ctx.shape, torch.empty(ctx.shape, device="meta").stride()), None
+        out = g.new_zeros(ctx.shape)
+        out[..., : g.shape[-1]] = g
+        return out, None
+
+
 class Decoder(nn.Module):
     """Linear ``E -> V`` (``main.py:42-55``).
 
@@ -111,7 +133,11 @@ class Decoder(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         y = ops.linear(x, self.weight, self.bias)
-        return y[..., : self.ntoken] if self.padded != self.ntoken else y
+        if self.padded == self.ntoken:
+            return y
+        if y.is_cuda and torch.is_grad_enabled() and y.requires_grad:
+            return _VocabSlice.apply(y, self.ntoken)
+        return y[..., : self.ntoken]
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2.0 * self.weight.shape[0] * self.weight.shape[1]

@@ -12,12 +12,37 @@ from torch import Tensor
 
 from ._util import native_or_none
 
-__all__ = ["cross_entropy"]
+__all__ = ["cross_entropy", "mark_zero_padded", "take_zero_padded"]
+
+# data_ptr -> padded width of gradient buffers whose pad columns are zero,
+# written by the cross-entropy backward and consumed (once) by the Decoder's
+# vocabulary-slice backward.  Entries are ints, never tensors.
+_ZERO_PADDED = {}
+
+
+def mark_zero_padded(buf: Tensor) -> None:
+    if len(_ZERO_PADDED) > 64:  # stale entries (a graph that never reached the slice)
+        _ZERO_PADDED.clear()
+    _ZERO_PADDED[buf.data_ptr()] = (buf.shape[-1], buf.untyped_storage().nbytes())
+
+
+def take_zero_padded(g: Tensor, width: int) -> bool:
+    """True if ``g`` is the ``[..., :V]`` view of a zero-padded gradient buffer
+    of row width ``width`` (and forgets the buffer)."""
+    ent = _ZERO_PADDED.get(g.data_ptr())
+    if ent is None or ent[0] != width or g.stride(-1) != 1 or g.storage_offset() != 0:
+        return False
+    rows = g.numel() // g.shape[-1] if g.shape[-1] else 0
+    if g.stride(-2) != width or ent[1] < rows * width * g.element_size():
+        return False
+    del _ZERO_PADDED[g.data_ptr()]
+    return True
 
 
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, ignore_index):  # type: ignore[override]
+        _ZERO_PADDED.clear()  # marks live from a CE backward to the slice backward of the same pass
         k = native_or_none(logits)
         lc = logits if (logits.dim() == 2 and logits.stride(1) == 1) else logits.contiguous()
         loss_rows, lse = k.cross_entropy_fwd(lc, target.contiguous(), ignore_index)
@@ -31,6 +56,17 @@ class _CrossEntropy(torch.autograd.Function):
         logits, target, lse, count = ctx.saved_tensors
         k = native_or_none(logits)
         scale = (dloss.to(torch.float32) / count).reshape(1).contiguous()
+        n, v = logits.shape
+        ld = logits.stride(0)
+        if ld > v:
+            # Rows of a padded-vocabulary buffer (the Decoder's [..., :V] view):
+            # the gradient gets the same padded geometry, zeros in the pad, so
+            # its rows are 16-byte aligned (vector path) and the Decoder's
+            # slice backward can hand the padded buffer on without a copy.
+            buf = torch.empty((n, ld), dtype=logits.dtype, device=logits.device)
+            k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index, None, buf, True)
+            mark_zero_padded(buf)
+            return buf[:, :v], None, None
         return k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index), None, None
 
 

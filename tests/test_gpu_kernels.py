@@ -119,13 +119,20 @@ def test_column_sum(k, cols, rows):
 # ------------------------------------------------------------------ cross entropy
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("V", [1000, 28782])
-def test_cross_entropy(k, dtype, V):
+@pytest.mark.parametrize("padded", [False, True])
+def test_cross_entropy(k, dtype, V, padded):
     from mipipe.ops import cross_entropy
 
     N = 200
-    logits = (3 * torch.randn(N, V, device=DEV)).to(dtype).requires_grad_()
+    vp = (V + 255) // 256 * 256 if padded else V
+    base = (3 * torch.randn(N, vp, device=DEV)).to(dtype)
+    logits = base[:, :V].detach().requires_grad_() if not padded else None
+    if padded:  # a [N, :V] view of a padded-vocabulary buffer (the Decoder's output)
+        base.requires_grad_()
+        logits = base[:, :V]
     t = torch.randint(0, V, (N,), device=DEV)
     t[3] = -100
+    t[5] = V - 1  # a target in the scalar tail
     loss = cross_entropy(logits, t)
     lf = logits.detach().float().requires_grad_()
     ref = F.cross_entropy(lf, t, ignore_index=-100)
@@ -133,7 +140,10 @@ def test_cross_entropy(k, dtype, V):
     loss.backward()
     ref.backward()
     atol = 1e-5 if dtype == torch.float32 else 2e-4
-    assert torch.allclose(logits.grad.float(), lf.grad, atol=atol, rtol=2e-2)
+    g = base.grad[:, :V] if padded else logits.grad
+    assert torch.allclose(g.float(), lf.grad, atol=atol, rtol=2e-2)
+    if padded:
+        assert base.grad[:, V:].abs().max().item() == 0.0
 
 
 # ------------------------------------------------------------------ embedding
@@ -668,3 +678,30 @@ def test_fanout_ops_match_plain(k):
         torch.autograd.backward([yn, xr * 1.0], [gln, gr])
         grads.append(x.grad.float())
     assert torch.allclose(grads[0], grads[1], atol=3e-2, rtol=2e-2)
+
+
+def test_decoder_padded_vocab_grad(k):
+    """Decoder (padded vocabulary) + fused CE: the zero-padded CE gradient is
+    handed to the decoder GEMM without a copy; gradients match fp32 torch."""
+    from mipipe.models.lm import Decoder
+    from mipipe.ops import cross_entropy
+
+    torch.manual_seed(12)
+    V, E, B, S = 1000, 256, 2, 64
+    dec = Decoder(V, E, device=DEV, dtype=torch.bfloat16)
+    assert dec.padded > V
+    x = torch.randn(B, S, E, device=DEV).to(torch.bfloat16).requires_grad_()
+    t = torch.randint(0, V, (B, S), device=DEV)
+    y = dec(x)
+    assert y.shape == (B, S, V)
+    loss = cross_entropy(y.reshape(-1, V), t.reshape(-1))
+    loss.backward()
+    w = dec.weight.detach().float()[:V].requires_grad_()
+    b = dec.bias.detach().float()[:V].requires_grad_()
+    xf = x.detach().float().requires_grad_()
+    ref = F.cross_entropy((xf @ w.t() + b).reshape(-1, V), t.reshape(-1))
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-2
+    assert torch.allclose(x.grad.float(), xf.grad, atol=2e-3, rtol=5e-2)
+    assert torch.allclose(dec.weight.grad.float()[:V], w.grad, atol=2e-3, rtol=5e-2)
+    assert dec.weight.grad.float()[V:].abs().max().item() == 0.0
