@@ -452,8 +452,8 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
   return dx;
 }
 
-// main_grad[N,K] (fp32) += dy[T,N]^T . x[T,K]
-void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad) {
+// main_grad[N,K] (fp32) += dy[T,N]^T . x[T,K]   (= when !accumulate)
+void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad, bool accumulate) {
   check_bf16_2d(dy, "dy");
   check_bf16_2d(x, "x");
   check_cuda(main_grad, "main_grad");
@@ -465,7 +465,7 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad) {
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = x.data_ptr(); g.C = main_grad.data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)T;
-  g.a_kc = false; g.b_kc = false; g.epi = kEpiAccumF32;
+  g.a_kc = false; g.b_kc = false; g.epi = accumulate ? kEpiAccumF32 : kEpiStoreF32;
   gemm_bf16(g, cur_stream(dy));
 }
 
@@ -509,7 +509,9 @@ void py_column_sum_segments(std::vector<Tensor> xs, Tensor out, bool accumulate)
 // as K-segmented GEMMs (up to GemmArgs::kMaxSegs micro-batches per launch),
 // so the fp32 read-modify-write of main_grad happens once per launch instead
 // of once per micro-batch and K is long enough to amortise the tile prologue.
-void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, Tensor main_grad) {
+// accumulate = false: the FIRST launch overwrites main_grad (its first write of
+// the step after a lazy zero_grad), later launches accumulate.
+void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, Tensor main_grad, bool accumulate) {
   MP_CHECK(!dys.empty() && dys.size() == xs.size(), "linear_wgrad_segments: need matching non-empty lists");
   check_cuda(main_grad, "main_grad");
   const int64_t T = dys[0].size(0), N = dys[0].size(1), K = xs[0].size(1);
@@ -528,7 +530,7 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
     GemmArgs g;
     g.C = main_grad.data_ptr();
     g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)(T * n);
-    g.a_kc = false; g.b_kc = false; g.epi = kEpiAccumF32;
+    g.a_kc = false; g.b_kc = false; g.epi = (accumulate || first > 0) ? kEpiAccumF32 : kEpiStoreF32;
     g.seg_k = (int)T;
     for (int i = 0; i < n; ++i) {
       g.a_seg[i] = dys[first + i].data_ptr();
@@ -709,8 +711,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_get_schedule", &gemm_get_schedule);
   m.def("linear_fwd", &py_linear_fwd);
   m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none());
-  m.def("linear_wgrad", &py_linear_wgrad);
-  m.def("linear_wgrad_segments", &py_linear_wgrad_segments);
+  m.def("linear_wgrad", &py_linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("main_grad"),
+        py::arg("accumulate") = true);
+  m.def("linear_wgrad_segments", &py_linear_wgrad_segments, py::arg("dys"), py::arg("xs"), py::arg("main_grad"),
+        py::arg("accumulate") = true);
   m.def("column_sum_segments", &py_column_sum_segments);
   m.def("gemm_f32", &py_gemm_f32);
   m.def("sumsq", &py_sumsq);

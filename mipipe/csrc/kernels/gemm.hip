@@ -490,8 +490,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   //    (waves wm = 0, then wm = 1): each wave spills its 128 x 64 tile into a
   //    [128][260] fp32 image (the 4-float row pad makes the scattered 4-byte
   //    writes conflict-free), then all 512 threads stream whole 1 KiB rows
-  //    back with 16-byte accesses -- fp32 read-modify-write for the weight
-  //    gradient, 16-byte bf16 stores otherwise.
+  //    back with 16-byte accesses -- fp32 read-modify-write for an
+  //    accumulated weight gradient, plain 16-byte fp32 stores for the first
+  //    write of a step (kEpiStoreF32).
   const int quad = lane >> 4, col_in = lane & 15;
   const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
   if (EPI == kEpiStoreBf16) {
@@ -549,19 +550,6 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     }
     return;  // direct 2-byte stores measured faster than staging for bf16 (profiles/gemm_ablation.txt)
   }
-  if (EPI == kEpiStoreF32) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 128 + 16 * i + 4 * quad + r, col = n0 + wn * 64 + 16 * j + col_in;
-          if (row < g.M && col < g.N) reinterpret_cast<float*>(g.C)[(int64_t)row * g.ldc + col] = acc[i][j][r];
-        }
-    return;
-  }
-
   constexpr int kStride = 260;  // floats per staged row (256 + 4 pad)
   float* stg = reinterpret_cast<float*>(smem);
   __syncthreads();  // every wave is done reading the operand buffers

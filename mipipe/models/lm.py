@@ -20,6 +20,7 @@ import torch
 from torch import Tensor, nn
 
 from .. import ops
+from ..ops.linear import mark_gemm_weight
 from .transformer import transformer_blocks
 
 __all__ = [
@@ -121,7 +122,7 @@ class Decoder(nn.Module):
         fk = {"device": device, "dtype": dtype}
         self.ntoken = ntoken
         self.padded = (ntoken + pad_to - 1) // pad_to * pad_to
-        self.weight = nn.Parameter(torch.empty(self.padded, d_model, **fk))
+        self.weight = mark_gemm_weight(nn.Parameter(torch.empty(self.padded, d_model, **fk)))
         self.bias = nn.Parameter(torch.zeros(self.padded, **fk))
         self.reset_parameters()
 

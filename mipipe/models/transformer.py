@@ -29,6 +29,7 @@ import torch
 from torch import Tensor, nn
 
 from .. import ops
+from ..ops.linear import mark_gemm_weight
 
 # Fan-out fusion of the residual-branch gradient (see AttentionCore.forward_fanout);
 # MIPIPE_FANOUT=0 turns it off (A/B measurements).
@@ -63,7 +64,7 @@ class AttentionCore(nn.Module):
         fk = {"device": device, "dtype": dtype}
         self.d_model, self.nhead, self.head_dim = d_model, nhead, d_model // nhead
         self.dropout, self.norm_first, self.causal, self.eps = dropout, norm_first, causal, layer_norm_eps
-        self.in_proj_weight = nn.Parameter(torch.empty(3 * d_model, d_model, **fk))
+        self.in_proj_weight = mark_gemm_weight(nn.Parameter(torch.empty(3 * d_model, d_model, **fk)))
         self.in_proj_bias = nn.Parameter(torch.empty(3 * d_model, **fk))
         if norm_first:
             self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
@@ -119,7 +120,7 @@ class AttentionOutput(nn.Module):
         super().__init__()
         fk = {"device": device, "dtype": dtype}
         self.d_model, self.dropout, self.norm_first, self.eps = d_model, dropout, norm_first, layer_norm_eps
-        self.out_proj_weight = nn.Parameter(torch.empty(d_model, d_model, **fk))
+        self.out_proj_weight = mark_gemm_weight(nn.Parameter(torch.empty(d_model, d_model, **fk)))
         self.out_proj_bias = nn.Parameter(torch.empty(d_model, **fk))
         if not norm_first:
             self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
@@ -219,7 +220,7 @@ class FeedForwardIn(nn.Module):
         fk = {"device": device, "dtype": dtype}
         self.d_model, self.dim_feedforward = d_model, dim_feedforward
         self.dropout, self.activation, self.norm_first, self.eps = dropout, activation, norm_first, layer_norm_eps
-        self.linear1_weight = nn.Parameter(torch.empty(dim_feedforward, d_model, **fk))
+        self.linear1_weight = mark_gemm_weight(nn.Parameter(torch.empty(dim_feedforward, d_model, **fk)))
         self.linear1_bias = nn.Parameter(torch.empty(dim_feedforward, **fk))
         if norm_first:
             self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))
@@ -265,7 +266,7 @@ class FeedForwardOut(nn.Module):
         fk = {"device": device, "dtype": dtype}
         self.d_model, self.dim_feedforward = d_model, dim_feedforward
         self.dropout, self.norm_first, self.eps = dropout, norm_first, layer_norm_eps
-        self.linear2_weight = nn.Parameter(torch.empty(d_model, dim_feedforward, **fk))
+        self.linear2_weight = mark_gemm_weight(nn.Parameter(torch.empty(d_model, dim_feedforward, **fk)))
         self.linear2_bias = nn.Parameter(torch.empty(d_model, **fk))
         if not norm_first:
             self.norm_weight = nn.Parameter(torch.empty(d_model, **fk))

@@ -30,7 +30,7 @@ import torch
 from torch import Tensor, nn
 
 from ..ops._util import native_or_none
-from ..ops.linear import accumulate_wgrad
+from ..ops.linear import accumulable, accumulate_wgrad, mark_gemm_weight
 
 __all__ = ["DecoderHead", "DecoderTail", "split_point", "split_decoder", "STAT_SLOTS"]
 
@@ -56,7 +56,7 @@ def _dgrad(k, tile: bool, d: Tensor, w: Tensor) -> Tensor:
 
 
 def _bias_grad(k, d: Tensor, b: Tensor) -> Optional[Tensor]:
-    main = getattr(b, "main_grad", None)
+    main = accumulable(b)
     if main is not None:
         if k is not None:
             k.column_sum(d, main, True)
@@ -176,7 +176,7 @@ class DecoderHead(nn.Module):
     def __init__(self, ntoken: int, d_model: int, va: int, *, device=None, dtype=None) -> None:
         super().__init__()
         self.ntoken, self.va = ntoken, va
-        self.weight = nn.Parameter(torch.empty(va, d_model, device=device, dtype=dtype))
+        self.weight = mark_gemm_weight(nn.Parameter(torch.empty(va, d_model, device=device, dtype=dtype)))
         self.bias = nn.Parameter(torch.zeros(va, device=device, dtype=dtype))
         self.reset_parameters()
 
@@ -204,7 +204,7 @@ class DecoderTail(nn.Module):
         self.ntoken, self.va, self.vb = ntoken, va, ntoken - va
         self.padded = (self.vb + pad_to - 1) // pad_to * pad_to
         self.ignore_index = ignore_index
-        self.weight = nn.Parameter(torch.empty(self.padded, d_model, device=device, dtype=dtype))
+        self.weight = mark_gemm_weight(nn.Parameter(torch.empty(self.padded, d_model, device=device, dtype=dtype)))
         self.bias = nn.Parameter(torch.zeros(self.padded, device=device, dtype=dtype))
         self.reset_parameters()
 

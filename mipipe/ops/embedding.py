@@ -13,6 +13,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from ._util import native_or_none
+from .linear import accumulable
 
 __all__ = ["embed_scale_posenc_dropout"]
 
@@ -32,7 +33,7 @@ class _Embed(torch.autograd.Function):
         (tokens,) = ctx.saved_tensors
         weight = ctx.weight
         k = native_or_none(dout)
-        main = getattr(weight, "main_grad", None)
+        main = accumulable(weight)
         if main is not None:
             k.embedding_bwd(tokens, dout.contiguous(), main, ctx.scale, ctx.p, ctx.seed, ctx.offset)
             return None, None, None, None, None

@@ -13,6 +13,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from ._util import native_or_none
+from .linear import accumulable
 
 __all__ = ["add_dropout_layer_norm", "layer_norm_fanout", "layer_norm_reference"]
 
@@ -39,7 +40,7 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
         ctx.seed = seed
         ctx.offset = offset
         ctx.has_residual = residual is not None
-        ctx.bias_main_grad = getattr(bias, "main_grad", None)
+        ctx.bias = bias
         if fanout:
             # x again for its other consumer (pre-norm residual); its gradient
             # is added to dx inside the LayerNorm backward kernel
@@ -52,8 +53,8 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
         if dy is None:  # only the fan-out branch carries a gradient
             return dfan, None, None, None, None, None, None
         k = native_or_none(dy)
-        mg = getattr(weight, "main_grad", None)
-        mb = ctx.bias_main_grad
+        mg = accumulable(weight)
+        mb = accumulable(ctx.bias) if ctx.bias is not None else None
         add = dfan.contiguous() if dfan is not None and dfan.dtype == dy.dtype else None
         if mg is not None and mb is not None:
             # dgamma/dbeta accumulate straight into the fp32 main_grad buffers

@@ -25,7 +25,43 @@ from torch import Tensor
 from ._util import native_or_none
 from .activation import ACTIVATIONS, bias_act_reference
 
-__all__ = ["linear", "linear_fanout", "deferred_wgrad", "flush_wgrad", "accumulate_wgrad"]
+__all__ = ["linear", "linear_fanout", "deferred_wgrad", "flush_wgrad", "accumulate_wgrad", "mark_gemm_weight"]
+
+
+def mark_gemm_weight(p: Tensor) -> Tensor:
+    """Tags a weight whose gradient only this module's GEMMs write.  The flat
+    optimizer then skips zero-filling its ``main_grad`` in ``zero_grad`` and
+    the first weight-gradient GEMM of the step OVERWRITES it (plain fp32
+    stores, no read-modify-write); see :func:`_claim`."""
+    p._mipipe_gemm_weight = True  # type: ignore[attr-defined]
+    return p
+
+
+def _claim(p: Tensor) -> bool:
+    """Whether the next gradient write into ``p.main_grad`` must accumulate:
+    False exactly once after a lazy ``FlatAdam.zero_grad`` (the buffer holds
+    stale values then, and the first writer overwrites it)."""
+    if getattr(p, "_mg_fresh", False):
+        p._mg_fresh = False  # type: ignore[attr-defined]
+        return False
+    return True
+
+
+def accumulable(p: Tensor) -> Optional[Tensor]:
+    """``p.main_grad`` ready for ACCUMULATING writers (atomics, += epilogues):
+    a lazily-zeroed buffer is zero-filled first (a tagged weight reached by a
+    writer that cannot overwrite, e.g. a tied embedding)."""
+    main = getattr(p, "main_grad", None)
+    if main is not None and not _claim(p):
+        main.zero_()
+    return main
+
+
+def _add_or_copy(main: Tensor, g: Tensor, p: Tensor) -> None:
+    if _claim(p):
+        main.add_(g.float())
+    else:
+        main.copy_(g)
 
 
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
@@ -80,7 +116,7 @@ class _Linear(torch.autograd.Function):
         k = native_or_none(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
-        main_b = getattr(bias, "main_grad", None) if need_db else None
+        main_b = accumulable(bias) if need_db else None
         # inside deferred_wgrad(): the bias gradient joins the step's batch too
         defer_b = main_b is not None and _DEFERRED is not None and d2.shape[-1] % 8 == 0
         act, p = ctx.act, ctx.p
@@ -122,9 +158,9 @@ class _Linear(torch.autograd.Function):
             if main is not None and ctx.fused_tile and _DEFERRED is not None:
                 _defer(w, dpre, x2)
             elif main is not None and ctx.fused_tile:
-                k.linear_wgrad(dpre, x2, main)
+                k.linear_wgrad(dpre, x2, main, _claim(w))
             elif main is not None:
-                main.add_(torch.matmul(dpre.t(), x2).float())
+                _add_or_copy(main, torch.matmul(dpre.t(), x2), w)
             else:
                 dw = torch.matmul(dpre.t(), x2)
         return dx, dw, db, None, None, None
@@ -167,11 +203,11 @@ def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
         if _DEFERRED is not None:
             _defer(w, dy.contiguous(), x.contiguous())
         else:
-            k.linear_wgrad(dy.contiguous(), x.contiguous(), main)
+            k.linear_wgrad(dy.contiguous(), x.contiguous(), main, _claim(w))
         return None
     g = torch.matmul(dy.t(), x)
     if main is not None:
-        main.add_(g.float())
+        _add_or_copy(main, g, w)
         return None
     return g.to(w.dtype)
 
@@ -190,10 +226,10 @@ def flush_wgrad() -> None:
         T = dys[0].shape[0]
         uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
         if uniform and T % 64 == 0:
-            k.linear_wgrad_segments(dys, xs, w.main_grad)
+            k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
         else:
             for d, x in zip(dys, xs):
-                k.linear_wgrad(d, x, w.main_grad)
+                k.linear_wgrad(d, x, w.main_grad, _claim(w))
 
 
 class deferred_wgrad:

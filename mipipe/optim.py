@@ -20,6 +20,7 @@ Semantics match ``torch.optim.Adam`` (L2 weight decay) or ``AdamW``
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import torch
@@ -32,6 +33,13 @@ __all__ = ["FlatAdam"]
 
 class _Group:
     def __init__(self, params: List[nn.Parameter], device: torch.device, dtype: torch.dtype) -> None:
+        # GEMM-only weights (ops.linear.mark_gemm_weight) first: their main_grad
+        # is never zero-filled -- the step's first weight-gradient GEMM
+        # overwrites it -- so zero_grad fills only the tail [n_lazy:).
+        lazy = [p for p in params if getattr(p, "_mipipe_gemm_weight", False)]
+        params = lazy + [p for p in params if not getattr(p, "_mipipe_gemm_weight", False)]
+        self.lazy = lazy
+        self.n_lazy = sum(p.numel() for p in lazy)
         self.params = params
         self.device = device
         self.dtype = dtype
@@ -88,20 +96,41 @@ class FlatAdam:
     def params(self) -> List[nn.Parameter]:
         return [p for g in self.groups for p in g.params]
 
-    def zero_grad(self, set_to_none: bool = True) -> None:
+    def zero_grad(self, set_to_none: bool = True, lazy: Optional[bool] = None) -> None:
+        """Zeroes the gradients.  ``lazy``: GEMM-only weights are marked fresh
+        instead of filled (their first gradient write overwrites; any still
+        fresh at the optimizer step are zeroed then).  Default: on, unless
+        MIPIPE_LAZY_ZERO=0."""
+        if lazy is None:
+            lazy = os.environ.get("MIPIPE_LAZY_ZERO", "1") != "0"
         for g in self.groups:
-            g.main_grad.zero_()
+            if lazy and g.n_lazy:
+                g.main_grad[g.n_lazy:].zero_()
+                for p in g.lazy:
+                    p._mg_fresh = True  # type: ignore[attr-defined]
+            else:
+                g.main_grad.zero_()
+                for p in g.lazy:
+                    p._mg_fresh = False  # type: ignore[attr-defined]
             for p in g.params:
                 p.grad = None
 
     def fold_grads(self) -> None:
-        """Adds any autograd ``.grad`` (ops without main_grad support) into main_grad."""
+        """Adds any autograd ``.grad`` (ops without main_grad support) into
+        main_grad and zeroes lazily-zeroed gradients nothing wrote this step."""
         with torch.no_grad():
             for g in self.groups:
                 for p in g.params:
+                    fresh = getattr(p, "_mg_fresh", False)
                     if p.grad is not None:
-                        p.main_grad.add_(p.grad.float())  # type: ignore[attr-defined]
+                        if fresh:
+                            p.main_grad.copy_(p.grad)  # type: ignore[attr-defined]
+                        else:
+                            p.main_grad.add_(p.grad.float())  # type: ignore[attr-defined]
                         p.grad = None
+                    elif fresh:
+                        p.main_grad.zero_()  # type: ignore[attr-defined]
+                    p._mg_fresh = False  # type: ignore[attr-defined]
 
     def grad_sumsq(self) -> Optional[Tensor]:
         """fp32 [1] tensor: sum of squared gradients of all local groups (on the

@@ -19,6 +19,7 @@ from ..balance import balance_cost
 from ..models.lm import LMConfig, TargetSequential, build_lm_blocks, lm_pipeline_units
 from ..models.transformer import merge_units
 from ..models.vocab_split import STAT_SLOTS, split_point
+from ..ops.linear import mark_gemm_weight
 
 __all__ = ["StagePlan", "plan_stages", "block_costs", "stage_input_shape", "build_stage", "simulate_step", "choose_virtual"]
 
@@ -311,8 +312,13 @@ def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -
         proto = lm_pipeline_units(build_lm_blocks(cfg), split_decoder=plan.split_decoder)
     units = []
     for idx in plan.slice(vstage):
+        # to_empty() builds new Parameter objects: carry the GEMM-weight tags over
+        tagged = {n for n, p in proto[idx].named_parameters() if getattr(p, "_mipipe_gemm_weight", False)}
         u = proto[idx].to_empty(device=device)
         u.reset_parameters()
+        for n, p in u.named_parameters():
+            if n in tagged:
+                mark_gemm_weight(p)
         units.append(u)
     del proto
     stage = TargetSequential(*merge_units(units))

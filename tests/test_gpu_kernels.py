@@ -705,3 +705,41 @@ def test_decoder_padded_vocab_grad(k):
     assert torch.allclose(x.grad.float(), xf.grad, atol=2e-3, rtol=5e-2)
     assert torch.allclose(dec.weight.grad.float()[:V], w.grad, atol=2e-3, rtol=5e-2)
     assert dec.weight.grad.float()[V:].abs().max().item() == 0.0
+
+
+def test_lazy_zero_grad_overwrites(k):
+    """FlatAdam.zero_grad(lazy=True): GEMM-only weights are not zero-filled;
+    their first weight-gradient GEMM of the step overwrites main_grad (deferred
+    and immediate paths) -- gradients equal an eager zero_grad's, and a second
+    step does not accumulate onto the first."""
+    from mipipe import ops
+    from mipipe.models import CONFIGS, build_lm_blocks
+    from mipipe.optim import FlatAdam
+
+    torch.manual_seed(13)
+    cfg = CONFIGS["tiny"]
+    model = torch.nn.Sequential(*build_lm_blocks(cfg, device=DEV, dtype=torch.bfloat16)).train()
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    tok = torch.randint(0, cfg.vocab, (2, 4, cfg.seq_len + 1), device=DEV)
+
+    def run(lazy, defer):
+        opt.zero_grad(lazy=lazy)
+        ctx = ops.deferred_wgrad() if defer else None
+        if ctx:
+            ctx.__enter__()
+        for i in range(2):
+            torch.manual_seed(100 + i)
+            y = model(tok[i, :, :-1])
+            ops.cross_entropy(y.reshape(-1, cfg.vocab), tok[i, :, 1:].reshape(-1)).backward()
+        if ctx:
+            ctx.__exit__(None, None, None)
+        opt.fold_grads()
+        return torch.cat([g.main_grad.clone() for g in opt.groups])
+
+    for defer in (True, False):
+        eager = run(False, defer)
+        lazy1 = run(True, defer)
+        lazy2 = run(True, defer)
+        assert torch.allclose(lazy1, lazy2, atol=1e-5, rtol=1e-4)  # embedding atomics: order-dependent
+        assert torch.allclose(lazy1, eager, atol=1e-5, rtol=1e-4)
+        assert any(getattr(p, "_mipipe_gemm_weight", False) for p in model.parameters())
