@@ -54,6 +54,9 @@ def parse():
                     help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
                     help="model chunks per rank (looping placement); 'auto' = shortest simulated step")
+    ap.add_argument("--skips", default="none", choices=["none", "unet"],
+                    help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
+                         "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
     return ap.parse_args()
 
 
@@ -116,7 +119,11 @@ def main() -> int:
         plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1, bwd_ratio=bwd_ratio)
     torch.manual_seed(1234 + rank)
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
-    stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype).train() for vs in plan.vstages(rank)]
+    from mipipe.models.long_skip import unet_pairs
+
+    skip_pairs = unet_pairs(cfg.num_layers) if args.skips == "unet" else []
+    stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype, skips=skip_pairs).train()
+              for vs in plan.vstages(rank)]
     params = [p for st_ in stages for p in st_.parameters()]
     n_params_local = sum(p.numel() for p in params)
 
@@ -129,7 +136,8 @@ def main() -> int:
 
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
                             act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
-                            act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device)
+                            act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device,
+                            skip_shapes={"skip": ((mb, S, E), dtype)})
     # explicit recompute (issued before each gradient wait, as the engine does)
     from mipipe.pipeline import checkpoint_stop_for
     sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
@@ -170,6 +178,9 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
     ms = float(ms_t.item())
+    peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 2**30 if on_gpu else 0.0], device=device)
+    if world > 1:
+        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
 
     loss_val = None
     if is_last and st.loss is not None:
@@ -231,6 +242,8 @@ def main() -> int:
                 "schedule": "gpipe" if virtual == 1 else f"gpipe-looping(v={virtual})",
                 "virtual_chunks_per_rank": virtual,
                 "vocab_split_decoder": plan.split_decoder,
+                "skips": args.skips if not skip_pairs else f"{args.skips}: {len(skip_pairs)} long residuals, "
+                                                           f"{len(engine.skip_routes)} cross-stage",
                 "parallelism": f"pp{world}",
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
@@ -239,6 +252,7 @@ def main() -> int:
             "bubble_theory_pct": round(100.0 * (pp - 1) / (virtual * m + pp - 1), 2),
             "bubble_sim_pct": round(100.0 * (1 - sum(sim_busy) / len(sim_busy) / sim_t), 2),
             "loss": loss_val,
+            "peak_hbm_gib_per_gpu": round(float(peak.item()), 2) if on_gpu else None,
             "baseline_note": "vs_baseline divides by the reference's ~3.5k tokens/s (BASELINE.md, 2 GPUs, fp32, "
                              "16x d2048 model, checkpoint='never'); see BASELINE.md",
         }

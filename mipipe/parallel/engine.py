@@ -15,7 +15,11 @@ ranks with RCCL send/recv over xGMI.  It keeps the reference's semantics:
   micro-batches run forward under ``no_grad`` keeping only the stage input and
   the RNG state, and are recomputed (bit-identical dropout) right before their
   backward (``/root/reference/pipe.py:255-260,354``);
-* eval mode never checkpoints (``pipeline.py:153-155``).
+* eval mode never checkpoints (``pipeline.py:153-155``);
+* ``@skippable`` cross-stage skips (``pipeline.py:136-138``): a stashed tensor
+  goes straight from the stashing rank to the popping rank on its own
+  communicator, and its gradient comes back the same way
+  (:mod:`mipipe.parallel.skips`).
 
 Looping placement (``virtual`` > 1 model chunks per rank): rank ``r`` of ``n``
 owns virtual stages ``r, r+n, r+2n, ...``; a micro-batch flows
@@ -39,7 +43,7 @@ from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence, Tuple, Union
+from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
 import torch.distributed as dist
@@ -48,7 +52,9 @@ from torch import Tensor, nn
 from .. import ops
 from ..checkpoint import enable_checkpointing, enable_recomputing
 from ..pipeline import checkpoint_stop_for
-from .p2p import Channels
+from ..skip.tracker import use_skip_tracker
+from .p2p import Channels, DirectLinks
+from .skips import EngineSkipTracker, SkipRoute, gather_routes
 
 __all__ = ["PipelineEngine", "StepStats", "schedule_actions"]
 
@@ -113,13 +119,17 @@ class PipelineEngine:
         act_dtype: its dtype.
         loss_fn: ``loss_fn(output, target) -> scalar`` on the last virtual stage.
         group: process group of the pipeline (default: WORLD), or a ready
-            :class:`Channels`.
+            :class:`Channels` (then cross-stage skips need ``skip_routes``).
         schedule: ``gpipe`` (reference order; looping when virtual > 1) or ``1f1b``.
         defer_wgrad: run the backward's weight-gradient GEMMs after this rank's
             last backward (:func:`mipipe.ops.deferred_wgrad`): input gradients
             reach the upstream rank sooner, which shortens the pipeline drain
             by (n-1) weight-gradient times, and each weight's micro-batches
             become one K-segmented GEMM.  Same gradients.
+        skip_shapes: ``{skip name or key: (shape, dtype)}`` of cross-stage skips
+            whose tensor is not shaped like the popping stage's input.
+        skip_routes: explicit cross-stage routes (default: gathered from every
+            rank's ``@skippable`` layers at construction, a collective).
     """
 
     def __init__(
@@ -136,6 +146,8 @@ class PipelineEngine:
         schedule: str = "gpipe",
         measure: bool = False,
         defer_wgrad: bool = True,
+        skip_shapes: Optional[Dict[str, Tuple[Sequence[int], torch.dtype]]] = None,
+        skip_routes: Optional[Dict[str, SkipRoute]] = None,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
             raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
@@ -181,6 +193,60 @@ class PipelineEngine:
         # kept for callers: rank-level first/last of the whole pipeline
         self.is_first = self.rank == 0
         self.is_last = self.rank == n - 1
+        self._setup_skips(group, skip_shapes, skip_routes)
+
+    # ------------------------------------------------------------------ skips
+    def _setup_skips(self, group, skip_shapes, skip_routes) -> None:
+        """Cross-stage skip routes, the per-chunk key lists and the direct links."""
+        if skip_routes is not None:
+            routes = dict(skip_routes)
+        elif self.chan is not None and not isinstance(group, Channels):
+            routes = gather_routes(self.modules, self.vstage, self.act_shapes, self.act_dtype, group=group,
+                                   skip_shapes=skip_shapes)
+        else:
+            routes = {}  # one rank, one chunk: every skip stays inside the chunk
+        self.skip_routes: Dict[str, SkipRoute] = routes
+        self._pops = [sorted(k for k, r in routes.items() if r.pop_vstage == vs) for vs in self.vstage]
+        self._stashes = [sorted(k for k, r in routes.items() if r.stash_vstage == vs) for vs in self.vstage]
+        n = self.world
+        pairs = []
+        for r in routes.values():
+            s, d = r.stash_vstage % n, r.pop_vstage % n
+            if s != d:
+                pairs.append((s, d))
+                if r.has_grad:
+                    pairs.append((d, s))
+        self._skip_links: Optional[DirectLinks] = None
+        if pairs:
+            self._skip_links = DirectLinks(self.chan.ranks, pairs)
+            self._skip_links.warmup(self.device)
+
+    def _actions_of(self, rank: int, training: bool) -> List[Tuple[str, int, int]]:
+        if training:
+            return schedule_actions(self.schedule, self.chunks, self.world, rank, self.virtual)
+        return [("F", c, i) for c in range(self.virtual) for i in range(self.chunks)]
+
+    def _post_skip_recvs(self, into: Dict, training: bool, grad: bool) -> None:
+        """Posts every skip (``grad``: skip-gradient) receive of the step, per
+        source rank in the order that rank sends them: its schedule's F (B)
+        actions, keys sorted within an action."""
+        n = self.world
+        want = "B" if grad else "F"
+        for src in range(n):
+            if src == self.rank:
+                continue
+            for kind, c, i in self._actions_of(src, training):
+                if kind != want:
+                    continue
+                vs = c * n + src
+                for key in sorted(self.skip_routes):
+                    r = self.skip_routes[key]
+                    if grad and not (r.pop_vstage == vs and r.stash_vstage % n == self.rank and r.has_grad):
+                        continue
+                    if not grad and not (r.stash_vstage == vs and r.pop_vstage % n == self.rank):
+                        continue
+                    buf = torch.empty(r.shape, dtype=r.dtype, device=self.device)
+                    into[(key, i)] = (buf, self._skip_links.recv(src, self.rank, buf))
 
     # ------------------------------------------------------------------ helpers
     def _first(self, c: int) -> bool:
@@ -195,8 +261,11 @@ class PipelineEngine:
         return torch.empty(self.act_shapes[c], dtype=self.act_dtype, device=self.device)
 
     @staticmethod
-    def _run(mod: nn.Module, x: Tensor, targets, i: int) -> Tensor:
+    def _run(mod: nn.Module, x: Tensor, targets, i: int, tracker: Optional[EngineSkipTracker] = None) -> Tensor:
         """Chunk forward; chunks that want the targets (vocabulary-split decoder) get them."""
+        if tracker is not None:
+            with use_skip_tracker(tracker):
+                return PipelineEngine._run(mod, x, targets, i)
         if getattr(mod, "wants_target", False):
             if targets is None:
                 raise ValueError("this stage needs the targets (vocabulary-split decoder): pass targets on every rank")
@@ -224,12 +293,13 @@ class PipelineEngine:
         into the parameters (or their ``main_grad``); the caller runs the
         optimizer.  Returns the mean loss on the last stage.
         """
-        m, v = self.chunks, self.virtual
+        m, v, n = self.chunks, self.virtual, self.world
         training = self.modules[0].training and torch.is_grad_enabled()
         stop = checkpoint_stop_for(self.checkpoint, m) if self.modules[0].training else 0
         stats = StepStats()
         t0 = time.perf_counter()
         chan = self.chan
+        routes = self.skip_routes
 
         # Post every activation receive of the forward phase up front, in the
         # order the upstream rank sends them (chunk-major, micro-batch minor).
@@ -240,6 +310,13 @@ class PipelineEngine:
                 for i in range(m):
                     recv_x[c][i] = self._new_act(c)
                     recv_w[c][i] = chan.recv_act(recv_x[c][i])
+        # ... and every skip receive (each skip has its own directed link).
+        sk_rx: Dict = {}
+        sk_grad_rx: Dict = {}
+        sk_local: Dict = {}        # (key, i) -> skip handed between chunks of this rank
+        sk_local_grad: Dict = {}
+        if self._skip_links is not None:
+            self._post_skip_recvs(sk_rx, training, grad=False)
 
         stage_in = [[None] * m for _ in range(v)]
         stage_out = [[None] * m for _ in range(v)]
@@ -247,9 +324,47 @@ class PipelineEngine:
         rng = [[None] * m for _ in range(v)]
         grad_w = [[None] * m for _ in range(v)]
         grad_buf = [[None] * m for _ in range(v)]
+        skip_in = [[None] * m for _ in range(v)]
+        skip_out = [[None] * m for _ in range(v)]
         losses: List[Tensor] = []
         sends = []
         events = []
+
+        def skip_tracker(c: int, i: int) -> Optional[EngineSkipTracker]:
+            """Tracker of chunk c / micro-batch i, holding its received skips."""
+            if not routes:
+                return None
+            if skip_in[c][i] is None:
+                incoming = {}
+                for key in self._pops[c]:
+                    r = routes[key]
+                    if r.stash_vstage % n == self.rank:
+                        t = sk_local.pop((key, i))
+                    else:
+                        t, work = sk_rx.pop((key, i))
+                        work.wait()
+                    if training and r.has_grad:
+                        t.requires_grad_(True)
+                    incoming[key] = t
+                skip_in[c][i] = incoming
+            return EngineSkipTracker(routes, skip_in[c][i])
+
+        def ship_skips(c: int, i: int, tracker: Optional[EngineSkipTracker]) -> None:
+            if tracker is None:
+                return
+            for key in self._stashes[c]:
+                if key not in tracker.outgoing:
+                    raise RuntimeError(f"stage {self.vstage[c]} did not stash skip '{key}'")
+                t = tracker.outgoing[key]
+                r = routes[key]
+                dst = r.pop_vstage % n
+                if dst == self.rank:
+                    sk_local[(key, i)] = t.detach()
+                    continue
+                if tuple(t.shape) != tuple(r.shape) or t.dtype != r.dtype:
+                    raise RuntimeError(f"skip '{key}' is {tuple(t.shape)} {t.dtype}, the popping stage expects "
+                                       f"{tuple(r.shape)} {r.dtype} (pass skip_shapes=)")
+                sends.append(self._skip_links.send(self.rank, dst, t))
 
         def forward(c: int, i: int) -> None:
             mod = self.modules[c]
@@ -262,15 +377,16 @@ class PipelineEngine:
                 recv_x[c][i] = recv_w[c][i] = None
                 if training:
                     x.requires_grad_(True)
+            tracker = skip_tracker(c, i)
             tm = self._timer()
             if tm:
                 tm[0].record()
             if training and i < stop:
                 rng[c][i] = _RNGState(self.device)
                 with torch.no_grad(), enable_checkpointing():
-                    y = self._run(mod, x, targets, i)
+                    y = self._run(mod, x, targets, i, tracker)
             else:
-                y = self._run(mod, x, targets, i)
+                y = self._run(mod, x, targets, i, tracker)
             if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
                 loss = self._loss(mod, y, targets, i)
                 losses.append(loss.detach())
@@ -283,6 +399,9 @@ class PipelineEngine:
             out_meta[c][i] = torch.empty(y.shape, dtype=y.dtype, device="meta")
             if not last:
                 sends.append(chan.send_act(y.detach()))
+            ship_skips(c, i, tracker)
+            if tracker is not None and training and i >= stop:
+                skip_out[c][i] = tracker.outgoing
 
         def post_grad_recv(c: int, i: int) -> None:
             if not self._last(c) and grad_w[c][i] is None:
@@ -305,40 +424,67 @@ class PipelineEngine:
                     tr[0].record()
                 st = rng[c][i]
                 devices = [self.device] if self.device.type == "cuda" else []
+                tracker = skip_tracker(c, i)
                 with torch.random.fork_rng(devices=devices):
                     torch.set_rng_state(st.cpu)
                     if st.dev is not None:
                         torch.cuda.set_rng_state(st.dev, self.device)
                     with torch.enable_grad(), enable_recomputing():
-                        y = self._run(mod, x, targets, i)
+                        y = self._run(mod, x, targets, i, tracker)
                         if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
                             y = self._loss(mod, y, targets, i) / m
+                if tracker is not None:
+                    skip_out[c][i] = tracker.outgoing
                 if tr:
                     tr[1].record()
                     events.append(("B", tr))
             else:
                 y = stage_out[c][i]
+            # Stashed skips are outputs of this chunk too: their gradients
+            # (from the popping stage) seed the same backward pass.
+            outs, seeds = [y], [None if last else grad_buf[c][i]]
+            for key in self._stashes[c]:
+                r = routes[key]
+                if not r.has_grad:
+                    continue
+                if r.pop_vstage % n == self.rank:
+                    g = sk_local_grad.pop((key, i))
+                else:
+                    g, work = sk_grad_rx.pop((key, i))
+                    work.wait()
+                t = skip_out[c][i][key]
+                if t.requires_grad:
+                    outs.append(t)
+                    seeds.append(g)
             if not last:
                 grad_w[c][i].wait()
             tm = self._timer()
             if tm:
                 tm[0].record()
-            if last:
+            if len(outs) == 1 and last:
                 y.backward()
             else:
-                torch.autograd.backward(y, grad_buf[c][i])
+                torch.autograd.backward(outs, seeds)
             if tm:
                 tm[1].record()
                 events.append(("B", tm))
             stage_out[c][i] = grad_buf[c][i] = grad_w[c][i] = None
             if not self._first(c):
                 sends.append(chan.send_grad(x.grad))
-            stage_in[c][i] = rng[c][i] = None
+            for key in self._pops[c]:
+                r = routes[key]
+                if not r.has_grad:
+                    continue
+                leaf = skip_in[c][i][key]
+                g = leaf.grad if leaf.grad is not None else torch.zeros_like(leaf)
+                src = r.stash_vstage % n
+                if src == self.rank:
+                    sk_local_grad[(key, i)] = g
+                else:
+                    sends.append(self._skip_links.send(self.rank, src, g))
+            stage_in[c][i] = rng[c][i] = skip_in[c][i] = skip_out[c][i] = None
 
-        if training:
-            actions = schedule_actions(self.schedule, m, self.world, self.rank, v)
-        else:
-            actions = [("F", c, i) for c in range(v) for i in range(m)]
+        actions = self._actions_of(self.rank, training)
         started_backward = False
         defer = ops.deferred_wgrad() if (training and self.defer_wgrad) else None
         try:
@@ -357,6 +503,8 @@ class PipelineEngine:
                             for cc in reversed(range(v)):
                                 for k in reversed(range(m)):
                                     post_grad_recv(cc, k)
+                        if self._skip_links is not None:
+                            self._post_skip_recvs(sk_grad_rx, training, grad=True)
                     post_grad_recv(c, i)
                     backward(c, i)
             if defer is not None and started_backward:

@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
-__all__ = ["P2P", "Channels", "exchange_shape"]
+__all__ = ["P2P", "Channels", "DirectLinks", "exchange_shape"]
 
 
 class _HostStagedWork:
@@ -166,6 +166,53 @@ class Channels:
 
     def recv_grad(self, t: Tensor):
         return self._recv(self._link(self._bwd, self.rank), t)
+
+
+class DirectLinks:
+    """One communicator per DIRECTED pipeline-rank pair ``(src, dst)`` of ``pairs``.
+
+    Carries cross-stage skip tensors (``@skippable`` stash -> pop) straight
+    from the stashing rank to the popping rank, and their gradients back.
+    Every MI355X of a node has its own xGMI link to every other, so a skip
+    from stage 0 to stage 3 is one hop on a link the activation traffic does
+    not use, not a relay through stages 1 and 2 (the reference's portals do
+    the same with one peer copy, ``/root/reference/pipeline.py:136-138``).
+    One communicator per direction for the reason given in :class:`Channels`.
+    Every process of the default group constructs the same DirectLinks in
+    the same order (``dist.new_group`` is collective)."""
+
+    def __init__(self, ranks: Sequence[int], pairs: Sequence[Tuple[int, int]]) -> None:
+        self.ranks = list(ranks)
+        self.host_staged = dist.get_backend() == "gloo"
+        self._links = {}
+        for src, dst in sorted(set(pairs)):
+            a, b = self.ranks[src], self.ranks[dst]
+            self._links[(src, dst)] = (dist.new_group(sorted([a, b])), a, b)
+
+    def warmup(self, device: torch.device) -> None:
+        """Eager communicator creation, pairs in one global order (see :meth:`Channels.warmup`)."""
+        dev = torch.device("cpu") if self.host_staged else device
+        me = dist.get_rank()
+        for key in sorted(self._links):
+            group, src, dst = self._links[key]
+            if me == src:
+                dist.send(torch.zeros(1, device=dev), dst, group=group)
+            elif me == dst:
+                dist.recv(torch.zeros(1, device=dev), src, group=group)
+
+    def send(self, src: int, dst: int, t: Tensor):
+        group, _, gdst = self._links[(src, dst)]
+        if self.host_staged and t.device.type != "cpu":
+            host = t.detach().to("cpu")
+            return _HostStagedWork(dist.isend(host, gdst, group=group), host)
+        return dist.isend(t.detach().contiguous(), gdst, group=group)
+
+    def recv(self, src: int, dst: int, t: Tensor):
+        group, gsrc, _ = self._links[(src, dst)]
+        if self.host_staged and t.device.type != "cpu":
+            host = torch.empty(t.shape, dtype=t.dtype)
+            return _HostStagedWork(dist.irecv(host, gsrc, group=group), host, t)
+        return dist.irecv(t, gsrc, group=group)
 
 
 _DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32]

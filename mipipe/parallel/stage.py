@@ -305,9 +305,12 @@ def stage_input_shape(cfg: LMConfig, plan: StagePlan, vstage: int, micro_batch: 
     return base
 
 
-def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -> TargetSequential:
+def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype,
+                skips: Sequence[Tuple[int, int]] = ()) -> TargetSequential:
     """Instantiates ONLY this virtual stage's units (on ``device``, in ``dtype``)
-    and merges attention / MLP halves that ended up on the same stage."""
+    and merges attention / MLP halves that ended up on the same stage.
+    ``skips``: long cross-stage residuals (layer a -> layer b,
+    :mod:`mipipe.models.long_skip`) whose ends fall in this stage."""
     with torch.device("meta"):
         proto = lm_pipeline_units(build_lm_blocks(cfg), split_decoder=plan.split_decoder)
     units = []
@@ -321,6 +324,10 @@ def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype) -
                 mark_gemm_weight(p)
         units.append(u)
     del proto
+    if skips:
+        from ..models.long_skip import insert_long_skips
+
+        units = insert_long_skips(units, skips, start=plan.slice(vstage).start)
     stage = TargetSequential(*merge_units(units))
     for p in stage.parameters():
         if p.dtype.is_floating_point:

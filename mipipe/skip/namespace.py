@@ -6,7 +6,7 @@ Two instances of the same ``@skippable`` class stash under the same *name*;
 from __future__ import annotations
 
 import itertools
-from typing import Any
+from typing import Any, Optional
 
 __all__ = ["Namespace"]
 
@@ -16,13 +16,17 @@ _ids = itertools.count()
 class Namespace:
     """An opaque, totally ordered, hashable token."""
 
-    __slots__ = ("id",)
+    __slots__ = ("id", "label")
 
-    def __init__(self) -> None:
+    def __init__(self, label: Optional[str] = None) -> None:
         self.id = next(_ids)
+        # A label names the namespace the same way in every process: the
+        # multi-process engine keys cross-stage skips by it (ids depend on
+        # construction order).  Labels must be unique within a model.
+        self.label = label
 
     def __repr__(self) -> str:
-        return f"<Namespace '{self.id}'>"
+        return f"<Namespace '{self.label if self.label is not None else self.id}'>"
 
     def __hash__(self) -> int:
         return hash(("mipipe.Namespace", self.id))

@@ -28,7 +28,8 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
-@pytest.mark.parametrize("nproc,extra", [(1, []), (2, []), (2, ["--chunks-per-rank", "1", "--checkpoint", "always"])])
+@pytest.mark.parametrize("nproc,extra", [(1, []), (2, []), (2, ["--chunks-per-rank", "1", "--checkpoint", "always"]),
+                                         (3, ["--skips", "unet", "--chunks-per-rank", "1"])])
 def test_bench_json_contract(nproc, extra):
     args = ["--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--device", "cpu", "--config", "tiny",
             "--micro-batch", "2"] + extra
