@@ -139,3 +139,82 @@ def test_engine_cross_stage_skips_gloo(world, virtual, checkpoint):
             seen.add(name)
     assert seen == set(ref)
     assert crosses, "the split must put at least one skip across stages"
+
+
+def _gpu_cfg():
+    return dataclasses.replace(CONFIGS["tiny"], dropout=0.0, num_layers=4, d_model=256, nhead=4,
+                               dim_feedforward=512, vocab=512, seq_len=64)
+
+
+def _gpu_worker(rank, world, port, q):
+    from mipipe.optim import FlatAdam
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg, dev, m, mb = _gpu_cfg(), torch.device("cuda", 0), 4, 2
+        torch.manual_seed(0)
+        full = torch.nn.Sequential(*build_lm_blocks(cfg))
+        names = {id(p): n for n, p in full.named_parameters()}
+        units = lm_pipeline_units(list(full.children()))
+        plan = plan_stages(cfg, world, 1)
+        sl = plan.slice(rank)
+        stage = TargetSequential(*merge_units(insert_long_skips([units[i] for i in sl], PAIRS, start=sl.start)))
+        stage = stage.train().to(dev, torch.bfloat16)
+        opt = FlatAdam(stage.parameters(), lr=1e-3)
+        eng = PipelineEngine(stage, chunks=m, checkpoint="except_last",
+                             act_shape=stage_input_shape(cfg, plan, rank, mb), act_dtype=torch.bfloat16,
+                             loss_fn=_loss_fn(cfg) if rank == world - 1 else None, device=dev,
+                             skip_shapes={"skip": ((mb, cfg.seq_len, cfg.d_model), torch.bfloat16)})
+        inputs, targets = _data(cfg, m, mb)
+        opt.zero_grad()
+        st = eng.step([x.to(dev) for x in inputs] if rank == 0 else None, [t.to(dev) for t in targets])
+        opt.fold_grads()
+        grads = {names[id(p)]: p.main_grad.float().cpu().numpy().copy() for p in stage.parameters()}
+        q.put((rank, None if st.loss is None else float(st.loss), grads, len(eng.skip_routes)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_engine_skips_two_ranks_share_gpu():
+    """The long-residual LM on the HIP kernels, split over two ranks on one
+    MI355X (host-staged boundaries and skips) vs the one-rank engine."""
+    from mipipe.optim import FlatAdam
+
+    cfg, dev, m, mb = _gpu_cfg(), torch.device("cuda", 0), 4, 2
+    torch.manual_seed(0)
+    full = torch.nn.Sequential(*build_lm_blocks(cfg))
+    model = TargetSequential(*merge_units(insert_long_skips(lm_pipeline_units(list(full.children())), PAIRS)))
+    model = model.train().to(dev, torch.bfloat16)
+    names = {id(p): n for n, p in full.named_parameters()}
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    eng = PipelineEngine(model, chunks=m, checkpoint="never", act_shape=(mb, cfg.seq_len), act_dtype=torch.bfloat16,
+                         loss_fn=_loss_fn(cfg), device=dev)
+    inputs, targets = _data(cfg, m, mb)
+    opt.zero_grad()
+    ref_loss = float(eng.step([x.to(dev) for x in inputs], [t.to(dev) for t in targets]).loss)
+    opt.fold_grads()
+    ref = {names[id(p)]: p.main_grad.float().cpu() for p in model.parameters()}
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = set()
+    assert sum(r[3] for r in results) > 0, "no skip crossed the two stages"
+    for rank, loss, grads, _ in results:
+        if loss is not None:
+            assert abs(loss - ref_loss) < 2e-3 * abs(ref_loss)
+        for name, g in grads.items():
+            g = torch.from_numpy(g)
+            scale = ref[name].abs().max().item() + 1e-6
+            assert (g - ref[name]).abs().max().item() < 2e-2 * scale, name
+            seen.add(name)
+    assert seen == set(ref)
