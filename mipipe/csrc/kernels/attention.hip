@@ -303,6 +303,196 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_fwd_kernel(At
   }
 }
 
+// ------------------------------------------------------------------ forward, D = 64, 32 rows per wave
+// At D = 64 the 16-row kernel above is LDS-bound: per 64-key tile a wave
+// reads 16 KiB of K/V fragments for only 16 MFMAs (128 LDS clocks against 64
+// MFMA clocks per CU).  Here each wave owns TWO 16-row blocks (a workgroup =
+// 128 query rows) and every K/V fragment read from LDS feeds both, halving
+// LDS traffic per MFMA.  The softmax is trimmed to what the tile needs:
+//   * row max over the 16 lanes of a row by 4 DPP steps (quad_perm xor 1,
+//     xor 2, row_half_mirror, row_mirror) instead of ds_bpermute shuffles;
+//   * the row sum l stays a per-lane partial (alpha is uniform along a row)
+//     and is reduced once after the last tile;
+//   * causal masking is applied only to tiles that cross this wave's
+//     diagonal, and tiles wholly above it are skipped (barriers kept);
+//   * causal query tiles are issued longest-first, so the short ones fill the
+//     tail of the grid.
+// The dropout mask, lse and O are bit-compatible with attn_fwd_kernel (same
+// Philox keying), so the backward kernels are unchanged.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_max16_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp_mov<0x141>(v));  // row_half_mirror
+  v = fmaxf(v, dpp_mov<0x140>(v));  // row_mirror
+  return v;
+}
+
+constexpr int kWideRows = 128;  // query rows per workgroup of the wide kernel
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 2) attn_fwd_wide_kernel(AttnArgs a) {
+  constexpr int D = 64, NS = 2, ND = 4, RB = 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + Img<D>::kBytes;
+  bf16_t* scr_all = reinterpret_cast<bf16_t*>(smem + 2 * Img<D>::kBytes);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qt = CAUSAL ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qt * kWideRows;
+  const int wrow0 = q0 + wave * 32;  // this wave's rows wrow0 .. wrow0 + 31
+
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+
+  bf16x8 qf[RB][NS];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const bf16_t* qrow = Q + (int64_t)(wrow0 + 16 * rb + (lane & 15)) * a.ld_qkv;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[rb][s] = frag_global(qrow, s, lane);
+  }
+  f32x4 o[RB][ND];
+  float m[RB][4], l[RB][4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) o[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      m[rb][r] = -INFINITY;
+      l[rb][r] = 0.f;
+    }
+  }
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  const int ntiles = CAUSAL ? (q0 + kWideRows) / kRows : a.S / kRows;
+
+  TileRegs kr, vr;
+  load_tile<D>(K, a.ld_qkv, tid, kr);
+  load_tile<D>(V, a.ld_qkv, tid, vr);
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * kRows;
+    __syncthreads();
+    store_tile<D>(kimg, tid, kr);
+    store_tile<D>(vimg, tid, vr);
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      load_tile<D>(K + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, kr);
+      load_tile<D>(V + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, vr);
+    }
+    if (CAUSAL && k0 > wrow0 + 31) continue;  // wholly above this wave's diagonal
+    const bool diag = CAUSAL && k0 + kRows - 1 > wrow0;
+
+    f32x4 sacc[RB][4];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sacc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 kf = frag_rows<D>(kimg, 16 * j, s, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          sacc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[rb][s], kf, sacc[rb][j], 0, 0, 0);
+      }
+
+    bf16x8 pf[RB][2];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int qrow0 = wrow0 + 16 * rb + 4 * (lane >> 4);
+      float sv[4][4];
+      float tmax[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = sacc[rb][j][r] * sl2;
+          if (diag && key > qrow0 + r) x = -INFINITY;
+          sv[j][r] = x;
+          tmax[r] = fmaxf(tmax[r], x);
+        }
+      }
+      float alpha[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mn = fmaxf(m[rb][r], row_max16_dpp(tmax[r]));
+        alpha[r] = m[rb][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[rb][r] - mn);
+        m[rb][r] = mn;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        if (a.p > 0.f) {
+          const uint4 mw = attn_mask_words(a, bh, qrow0 >> 2, k0 + 16 * j + (lane & 15));
+          w[0] = mw.x; w[1] = mw.y; w[2] = mw.z; w[3] = mw.w;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pr = m[rb][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sv[j][r] - m[rb][r]);
+          l[rb][r] = (j == 0 ? l[rb][r] * alpha[r] : l[rb][r]) + pr;
+          sv[j][r] = (a.p > 0.f) ? (w[r] >= a.threshold ? pr * pscale : 0.f) : pr;
+        }
+      }
+#pragma unroll
+      for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[rb][t2][r] *= alpha[r];
+      bf16_t* scr = scr_all + (wave * RB + rb) * 16 * kScrStride;
+      scratch_write(scr, sv, lane);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's scratch writes done
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const bf16_t* scr = scr_all + (wave * RB + rb) * 16 * kScrStride;
+      pf[rb][0] = scratch_frag(scr, 0, lane);
+      pf[rb][1] = scratch_frag(scr, 1, lane);
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 vf = frag_cols<D>(vimg, 16 * t2, s, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          o[rb][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[rb][s], vf, o[rb][t2], 0, 0, 0);
+      }
+  }
+
+  bf16_t* O = reinterpret_cast<bf16_t*>(a.o) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int qrow0 = wrow0 + 16 * rb + 4 * (lane >> 4);
+    float inv[4], lt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      lt[r] = row_reduce_sum16(l[rb][r]);
+      inv[r] = lt[r] > 0.f ? 1.f / lt[r] : 0.f;
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        O[(int64_t)(qrow0 + r) * a.ld_o + 16 * t2 + (lane & 15)] = f2bf(o[rb][t2][r] * inv[r]);
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        a.lse[(int64_t)bh * a.S + qrow0 + r] = (m[rb][r] + log2f(lt[r] > 0.f ? lt[r] : 1.f)) / kLog2e;
+    }
+  }
+}
+size_t wide_fwd_smem() { return 2 * Img<64>::kBytes + 4 * 2 * 16 * kScrStride * 2; }
+
 // ------------------------------------------------------------------ delta = rowsum(dO * O)
 __global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a, int D) {
   // one wave per (b, s, h) row
@@ -435,6 +625,140 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_dq_kernel(Att
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       dQ[(int64_t)(qrow0 + r) * a.ld_qkv + 16 * t2 + (lane & 15)] = f2bf(dq[t2][r] * a.scale);
+}
+
+// ------------------------------------------------------------------ dQ, D = 64, 32 rows per wave
+// Same restructuring as attn_fwd_wide_kernel: each K/V fragment read from LDS
+// feeds the MFMAs of both 16-row blocks of the wave; tiles above the wave's
+// diagonal are skipped and only diagonal tiles are masked.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 2) attn_dq_wide_kernel(AttnArgs a) {
+  constexpr int D = 64, NS = 2, ND = 4, RB = 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + Img<D>::kBytes;
+  bf16_t* scr_all = reinterpret_cast<bf16_t*>(smem + 2 * Img<D>::kBytes);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qt = CAUSAL ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = qt * kWideRows;
+  const int wrow0 = q0 + wave * 32;
+  const int64_t boff = (int64_t)b * a.sb_qkv + (int64_t)h * a.sh_qkv;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + boff;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + boff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + boff;
+  const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + (int64_t)b * a.sb_o + (int64_t)h * a.sh_o;
+
+  bf16x8 qf[RB][NS], df[RB][NS];
+  float lse2[RB][4], dl[RB][4];
+  f32x4 dq[RB][ND];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int myrow = wrow0 + 16 * rb + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[rb][s] = frag_global(Q + (int64_t)myrow * a.ld_qkv, s, lane);
+      df[rb][s] = frag_global(dO + (int64_t)myrow * a.ld_o, s, lane);
+    }
+    const int qrow0 = wrow0 + 16 * rb + 4 * (lane >> 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      lse2[rb][r] = a.lse[(int64_t)bh * a.S + qrow0 + r] * kLog2e;
+      dl[rb][r] = a.delta[(int64_t)bh * a.S + qrow0 + r];
+    }
+#pragma unroll
+    for (int t = 0; t < ND; ++t) dq[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float sl2 = a.scale * kLog2e;
+  const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  const int ntiles = CAUSAL ? (q0 + kWideRows) / kRows : a.S / kRows;
+
+  TileRegs kr, vr;
+  load_tile<D>(K, a.ld_qkv, tid, kr);
+  load_tile<D>(V, a.ld_qkv, tid, vr);
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * kRows;
+    __syncthreads();
+    store_tile<D>(kimg, tid, kr);
+    store_tile<D>(vimg, tid, vr);
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      load_tile<D>(K + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, kr);
+      load_tile<D>(V + (int64_t)(k0 + kRows) * a.ld_qkv, a.ld_qkv, tid, vr);
+    }
+    if (CAUSAL && k0 > wrow0 + 31) continue;
+    const bool diag = CAUSAL && k0 + kRows - 1 > wrow0;
+
+    f32x4 sacc[RB][4], pacc[RB][4];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sacc[rb][j] = pacc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 kfr = frag_rows<D>(kimg, 16 * j, s, lane);
+        const bf16x8 vfr = frag_rows<D>(vimg, 16 * j, s, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          sacc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[rb][s], kfr, sacc[rb][j], 0, 0, 0);
+          pacc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[rb][s], vfr, pacc[rb][j], 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int qrow0 = wrow0 + 16 * rb + 4 * (lane >> 4);
+      float ds[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + 16 * j + (lane & 15);
+        uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        if (a.p > 0.f) {
+          const uint4 mw = attn_mask_words(a, bh, qrow0 >> 2, key);
+          w[0] = mw.x; w[1] = mw.y; w[2] = mw.z; w[3] = mw.w;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pr = __builtin_amdgcn_exp2f(sacc[rb][j][r] * sl2 - lse2[rb][r]);
+          if (diag && key > qrow0 + r) pr = 0.f;
+          float dp = pacc[rb][j][r];
+          if (a.p > 0.f) dp = w[r] >= a.threshold ? dp * pscale : 0.f;
+          ds[j][r] = pr * (dp - dl[rb][r]);
+        }
+      }
+      scratch_write(scr_all + (wave * RB + rb) * 16 * kScrStride, ds, lane);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    bf16x8 sf[RB][2];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const bf16_t* scr = scr_all + (wave * RB + rb) * 16 * kScrStride;
+      sf[rb][0] = scratch_frag(scr, 0, lane);
+      sf[rb][1] = scratch_frag(scr, 1, lane);
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 kc = frag_cols<D>(kimg, 16 * t2, s, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          dq[rb][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sf[rb][s], kc, dq[rb][t2], 0, 0, 0);
+      }
+  }
+  bf16_t* dQ = reinterpret_cast<bf16_t*>(a.dq) + boff;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int qrow0 = wrow0 + 16 * rb + 4 * (lane >> 4);
+#pragma unroll
+    for (int t2 = 0; t2 < ND; ++t2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dQ[(int64_t)(qrow0 + r) * a.ld_qkv + 16 * t2 + (lane & 15)] = f2bf(dq[rb][t2][r] * a.scale);
+  }
 }
 
 // ------------------------------------------------------------------ dK, dV
@@ -952,7 +1276,12 @@ size_t fwd_smem() { return 2 * Img<D>::kBytes + 4 * 16 * kScrStride * 2; }
 template <int D>
 size_t dkdv_smem() { return fwd_smem<D>() + 128 * sizeof(float); }
 
-int g_attn_fused_bwd = 1;  // S == 128: whole-sequence forward/backward kernels (1) or the general ones (0)
+int g_attn_fused_bwd = 1;
+// D = 64: 32-rows-per-wave forward (1, default) or the 16-row kernel (0); MIPIPE_ATTN_WIDE=0 for A/B runs.
+const int g_attn_wide = [] {
+  const char* e = getenv("MIPIPE_ATTN_WIDE");
+  return e == nullptr ? 1 : atoi(e);
+}();  // S == 128: whole-sequence forward/backward kernels (1) or the general ones (0)
 
 template <typename Kern>
 void set_smem(Kern k, size_t bytes) {
@@ -969,6 +1298,13 @@ void run_fwd(const AttnArgs& a, hipStream_t s) {
     }
     hipLaunchKernelGGL((shortseq::attn_fwd_s128_kernel<D, CAUSAL>), dim3(a.B * a.H), dim3(shortseq::kThreads),
                        shortseq::kFwdSmem, s, a);
+    return;
+  }
+  if (D == 64 && a.S % kWideRows == 0 && g_attn_wide) {
+    static bool once_w = false;
+    if (!once_w) { set_smem(attn_fwd_wide_kernel<CAUSAL>, wide_fwd_smem()); once_w = true; }
+    hipLaunchKernelGGL((attn_fwd_wide_kernel<CAUSAL>), dim3(a.S / kWideRows, a.B * a.H), dim3(kThreads),
+                       wide_fwd_smem(), s, a);
     return;
   }
   const size_t sm = fwd_smem<D>();
@@ -999,6 +1335,13 @@ void run_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.S * a.H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, D);
   hipLaunchKernelGGL((attn_dkdv_kernel<D, CAUSAL>), dim3(a.S / kRows, a.B * a.H), dim3(kThreads), sm2, s, a);
+  if (D == 64 && a.S % kWideRows == 0 && g_attn_wide) {
+    static bool once_w = false;
+    if (!once_w) { set_smem(attn_dq_wide_kernel<CAUSAL>, wide_fwd_smem()); once_w = true; }
+    hipLaunchKernelGGL((attn_dq_wide_kernel<CAUSAL>), dim3(a.S / kWideRows, a.B * a.H), dim3(kThreads),
+                       wide_fwd_smem(), s, a);
+    return;
+  }
   hipLaunchKernelGGL((attn_dq_kernel<D, CAUSAL>), dim3(a.S / kRows, a.B * a.H), dim3(kThreads), sm, s, a);
 }
 
