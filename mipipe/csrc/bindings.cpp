@@ -401,7 +401,8 @@ bool py_gemm_supported(int64_t M, int64_t N, int64_t K) { return gemm_supported(
 // y[M,N] = act(x[M,K] . w[N,K]^T + bias) with dropout; optional pre-activation.
 std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor x, Tensor w,
                                                                            std::optional<Tensor> bias, int64_t act,
-                                                                           double p, bool save_preact) {
+                                                                           double p, bool save_preact,
+                                                                           std::optional<Tensor> res) {
   check_bf16_2d(x, "x");
   check_bf16_2d(w, "w");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
@@ -412,6 +413,10 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
     check_cuda(*bias, "bias");
     MP_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N, "linear_fwd: bad bias");
   }
+  if (res) {
+    check_bf16_2d(*res, "res");
+    MP_CHECK(res->size(0) == M && res->size(1) == N && res->is_contiguous(), "linear_fwd: res must be contiguous [M, N]");
+  }
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty({M, N}, x.options());
   std::optional<Tensor> pre;
@@ -421,6 +426,7 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   GemmArgs g;
   g.A = x.data_ptr(); g.B = w.data_ptr(); g.C = y.data_ptr();
   g.bias = bias ? bias->data_ptr() : nullptr; g.aux = pre ? pre->data_ptr() : nullptr;
+  if (res) g.res = res->data_ptr();  // y = res + dropout(act(x . w^T + b)): the residual add in the epilogue
   g.lda = K; g.ldb = K; g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreBf16; g.act = (int)act; g.p = (float)p;
   g.seed = seed; g.offset = offset;
@@ -709,7 +715,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);
   m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 auto (default)");
   m.def("gemm_get_schedule", &gemm_get_schedule);
-  m.def("linear_fwd", &py_linear_fwd);
+  m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
+        py::arg("save_preact"), py::arg("res") = py::none());
   m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none());
   m.def("linear_wgrad", &py_linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("main_grad"),
         py::arg("accumulate") = true);

@@ -138,8 +138,7 @@ class AttentionOutput(nn.Module):
     def forward(self, x: Tensor, o: Tensor) -> Tensor:
         p = self.dropout if self.training else 0.0
         if self.norm_first:
-            a = ops.linear(o, self.out_proj_weight, self.out_proj_bias, None, p, self.training)
-            return x + a
+            return ops.linear_residual(o, self.out_proj_weight, self.out_proj_bias, x, p, self.training)
         a = ops.linear(o, self.out_proj_weight, self.out_proj_bias)
         return ops.add_dropout_layer_norm(a, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
 
@@ -284,7 +283,7 @@ class FeedForwardOut(nn.Module):
     def forward(self, x: Tensor, h: Tensor) -> Tensor:
         p = self.dropout if self.training else 0.0
         if self.norm_first:
-            return x + ops.linear(h, self.linear2_weight, self.linear2_bias, None, p, self.training)
+            return ops.linear_residual(h, self.linear2_weight, self.linear2_bias, x, p, self.training)
         h = ops.linear(h, self.linear2_weight, self.linear2_bias)
         return ops.add_dropout_layer_norm(h, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
 

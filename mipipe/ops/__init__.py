@@ -6,7 +6,7 @@ CPU tensors (plumbing tests).  GPU tensors never fall back to eager PyTorch:
 a missing extension raises (``mipipe._native_loader.kernels``).
 """
 from .layernorm import add_dropout_layer_norm, layer_norm_fanout, layer_norm_reference
-from .linear import deferred_wgrad, flush_wgrad, linear, linear_fanout
+from .linear import deferred_wgrad, flush_wgrad, linear, linear_fanout, linear_residual
 from .attention import attention, attention_packed, attention_reference
 from .activation import bias_act_dropout
 from .loss import cross_entropy
@@ -18,6 +18,7 @@ __all__ = [
     "layer_norm_reference",
     "linear",
     "linear_fanout",
+    "linear_residual",
     "deferred_wgrad",
     "flush_wgrad",
     "attention",

@@ -78,7 +78,7 @@ def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, act, p, fanout=False):  # type: ignore[override]
+    def forward(ctx, x, weight, bias, act, p, fanout=False, res=None):  # type: ignore[override]
         ctx.set_materialize_grads(False)
         k = native_or_none(x)
         shape = x.shape
@@ -87,8 +87,15 @@ class _Linear(torch.autograd.Function):
         fused_tile = _tile_ok(k, x2, w)
         seed = offset = 0
         preact = None
+        ctx.has_res = res is not None
         if fused_tile:
-            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2)
+            r2 = None
+            if res is not None:
+                r2 = res.reshape(-1, w.shape[0])
+                if r2.dtype != torch.bfloat16 or not r2.is_contiguous():
+                    r2 = r2.to(torch.bfloat16).contiguous()
+            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2, r2)
+            res = None  # added in the epilogue
         else:
             y = torch.matmul(x2, w.t())
             if act != 0 or p > 0.0 or bias is not None:
@@ -102,6 +109,8 @@ class _Linear(torch.autograd.Function):
         ctx.fused_tile = fused_tile
         ctx.in_shape = shape
         y = y.view(*shape[:-1], w.shape[0])
+        if res is not None:
+            y = y + res
         if fanout:
             # the input again, for its other consumer: its gradient comes back
             # to this node and is added in the dgrad GEMM's epilogue
@@ -111,8 +120,9 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, dres=None):  # type: ignore[override]
         x2, w, bias, saved = ctx.saved_tensors
+        dres_in = dy if ctx.has_res else None  # y = res + f(x): the residual input's gradient is dy
         if dy is None:  # only the fan-out branch carries a gradient
-            return dres, None, None, None, None, None
+            return dres, None, None, None, None, None, None
         k = native_or_none(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
@@ -163,7 +173,7 @@ class _Linear(torch.autograd.Function):
                 _add_or_copy(main, torch.matmul(dpre.t(), x2), w)
             else:
                 dw = torch.matmul(dpre.t(), x2)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, dres_in
 
 
 # ---------------------------------------------------------------- deferred wgrad
@@ -266,6 +276,23 @@ def linear(
         y = F.linear(x, weight)
         return bias_act_reference(y, bias, activation, p, True)
     return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p)
+
+
+def linear_residual(
+    x: Tensor,
+    weight: Tensor,
+    bias: Optional[Tensor],
+    res: Tensor,
+    dropout_p: float = 0.0,
+    training: bool = True,
+) -> Tensor:
+    """``res + dropout(x @ weight.T + bias)`` -- a pre-norm residual branch's
+    output projection with the residual add folded into the GEMM epilogue (no
+    separate add kernel: one fewer read of two activations and write of one)."""
+    p = float(dropout_p) if training else 0.0
+    if not x.is_cuda:
+        return res + linear(x, weight, bias, None, p, True)
+    return _Linear.apply(x, weight, bias, 0, p, False, res)
 
 
 def linear_fanout(

@@ -369,6 +369,36 @@ def test_linear_op_matches_reference(k):
         assert torch.allclose(b.grad.float(), bf.grad, atol=2e-1, rtol=5e-2), act
 
 
+@pytest.mark.parametrize("T,K,N", [(256, 512, 384), (520, 264, 136)])
+def test_linear_residual_epilogue(k, T, K, N):
+    """``res + dropout(x W^T + b)`` with the add in the GEMM epilogue, against fp32
+    (p = 0) and against ``res + linear(...)`` with the same Philox draw (p > 0)."""
+    from mipipe.ops import linear, linear_residual
+
+    torch.manual_seed(6)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=DEV).to(torch.bfloat16).requires_grad_()
+    r = torch.randn(T, N, device=DEV).to(torch.bfloat16).requires_grad_()
+    y = linear_residual(x, w, b, r, 0.0, True)
+    xf, wf, bf, rf = (t.detach().float().requires_grad_() for t in (x, w, b, r))
+    ref = rf + xf @ wf.t() + bf
+    assert torch.allclose(y.float(), ref, atol=3e-2, rtol=3e-2)
+    g = torch.randn_like(ref)
+    y.backward(g.to(torch.bfloat16))
+    ref.backward(g)
+    assert torch.allclose(x.grad.float(), xf.grad, atol=6e-2, rtol=5e-2)
+    assert torch.allclose(w.grad.float(), wf.grad, atol=2e-1, rtol=5e-2)
+    assert torch.allclose(b.grad.float(), bf.grad, atol=2e-1, rtol=5e-2)
+    assert torch.allclose(r.grad.float(), rf.grad, atol=1e-2, rtol=1e-2)
+    with torch.no_grad():
+        torch.manual_seed(9)
+        y1 = linear_residual(x, w, b, r, 0.2, True)
+        torch.manual_seed(9)
+        y2 = r.float() + linear(x, w, b, None, 0.2, True).float()
+    assert torch.allclose(y1.float(), y2, atol=6e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("T,K,N", [(2048, 1600, 4800), (1024, 6400, 1600), (520, 264, 136)])
 def test_linear_edge_shapes_main_grad(k, T, K, N):
     """Non-multiple-of-256 widths (GPT-2-XL) go through the masked edge tiles in all three GEMMs."""
