@@ -123,24 +123,39 @@ __device__ __forceinline__ bf16x8 frag_global(const bf16_t* __restrict__ rowp, i
   return *reinterpret_cast<const bf16x8*>(rowp + 32 * s + 8 * (lane >> 4));
 }
 
-// Per-wave scratch [16][64] bf16 for accumulator -> A-operand relayout.
-// Row stride 136 bytes (64 + 4 elements) keeps both the scattered 2-byte
-// writes and the 16-byte fragment reads spread over the banks.
-constexpr int kScrStride = 68;  // elements
+// Per-wave scratch for the accumulator -> A-operand relayout of a 16 x 64
+// tile M (lane (g = lane >> 4, c = lane & 15) holds M[4g + r][16j + c]).
+// M is stored TRANSPOSED, T[col][row] (64 rows of 16 bf16 = 32 bytes), so a
+// lane's 4 values M[4g .. 4g+3][col] are one contiguous 8-byte ds_write_b64
+// (4 per tile instead of 16 ds_write_b16), and the A fragment (row c, k =
+// 32 s + 8 g + 0..7) is a column of T: two ds_read_b64_tr_b16.
+//   * rows are placed at phi(col) (bits 2 and 3 swapped), so the 8 rows a
+//     32-lane group of a transposing read touches ({0-3, 8-11} + 16 t and
+//     {4-7, 12-15} + 16 t) fill 256 contiguous bytes: all 64 banks once;
+//   * the 8-byte chunk g of row col sits at chunk g ^ ((col >> 2) & 3), so
+//     the 16 lanes of a ds_write_b64 group (cols 16 j + 0..15) hit 16
+//     distinct 8-byte bank pairs of a 128-byte window.
+// 2 KiB per tile (the 16 x 68 regions the kernels allocate hold it).
+constexpr int kScrStride = 68;  // elements (region size unit: 16 * kScrStride per tile)
+__device__ __forceinline__ int scr_row(int col) { return (col & ~12) | ((col & 4) << 1) | ((col & 8) >> 1); }
+__device__ __forceinline__ int scr_off(int col, int chunk) { return scr_row(col) * 32 + ((chunk ^ ((col >> 2) & 3)) << 3); }
 __device__ __forceinline__ void scratch_write(bf16_t* scr, const float (&v)[4][4], int lane) {
-  const int rq = 4 * (lane >> 4), c = lane & 15;
+  const int g = lane >> 4, c = lane & 15;
+  char* base = reinterpret_cast<char*>(scr);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(rq + r) * kScrStride + 16 * j + c] = f2bf(v[j][r]);
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = (uint32_t)f2bf(v[j][0]) | ((uint32_t)f2bf(v[j][1]) << 16);
+    const uint32_t hi = (uint32_t)f2bf(v[j][2]) | ((uint32_t)f2bf(v[j][3]) << 16);
+    *reinterpret_cast<uint2*>(base + scr_off(16 * j + c, g)) = make_uint2(lo, hi);
+  }
 }
 __device__ __forceinline__ bf16x8 scratch_frag(const bf16_t* scr, int s, int lane) {
-  const bf16_t* p = scr + (lane & 15) * kScrStride + 32 * s + 8 * (lane >> 4);
-  // 136-byte rows are 8-byte but not 16-byte aligned: two 8-byte reads.
-  const uint2 a = *reinterpret_cast<const uint2*>(p);
-  const uint2 b = *reinterpret_cast<const uint2*>(p + 4);
-  const uint4 v = make_uint4(a.x, a.y, b.x, b.y);
-  return __builtin_bit_cast(bf16x8, v);
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 32 * s + 8 * g + q;
+  const char* base = reinterpret_cast<const char*>(scr);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + scr_off(r0, p)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + scr_off(r0 + 4, p)));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 __device__ __forceinline__ uint4 attn_mask_words(const AttnArgs& a, int bh, int q4, int key) {
