@@ -500,6 +500,25 @@ void py_column_sum_segments(std::vector<Tensor> xs, Tensor out, bool accumulate)
   auto part = at::empty({total, cols}, xs[0].options().dtype(at::kFloat));
   auto s = cur_stream(out);
   int first = 0;
+  bool uniform = true;
+  for (size_t i = 1; i < xs.size(); ++i) uniform = uniform && rows[i] == rows[0];
+  if (uniform && cols % 8 == 0) {
+    // every segment's stage 1 in one launch per kColsumSegs inputs (grid.z = segment)
+    for (size_t i0 = 0; i0 < xs.size(); i0 += kColsumSegs) {
+      const int n = (int)std::min<size_t>(kColsumSegs, xs.size() - i0);
+      ColsumSegs segs;
+      for (int j = 0; j < n; ++j) segs.p[j] = xs[i0 + j].data_ptr();
+      dispatch_fb(xs[0], "column_sum_segments", [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        MP_CHECK(column_sum_partial_multi<T>(segs, n, rows[0], (int)cols, ptr<float>(part) + (int64_t)first * cols,
+                                             parts[0], s),
+                 "column_sum_segments: multi-segment launch refused");
+      });
+      first += n * parts[0];
+    }
+    reduce_parts(ptr<float>(part), nullptr, total, (int)cols, out.data_ptr(), nullptr, out_f32, accumulate, s);
+    return;
+  }
   for (size_t i = 0; i < xs.size(); ++i) {
     dispatch_fb(xs[i], "column_sum_segments", [&](auto* tag) {
       using T = std::remove_pointer_t<decltype(tag)>;

@@ -97,10 +97,15 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
 // column are folded through LDS and the block writes ONE partial row.  Parts
 // cover >= 256 rows each, so the partial image stays small (<= 64 rows) and
 // the second stage (reduce_parts) is a launch, not a second pass.
+// blockIdx.z picks one of up to kColsumSegs equally shaped inputs (the
+// micro-batch gradients of a deferred bias), each owning gridDim.y part rows:
+// all segments of a step run in ONE launch.
 template <typename T>
-__global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ x, int rows, int cols, int rows_per,
+__global__ void __launch_bounds__(256) colsum_part_kernel(ColsumSegs segs, int rows, int cols, int rows_per,
                                                           float* __restrict__ part) {
   __shared__ float sm[32][65];
+  const T* __restrict__ x = reinterpret_cast<const T*>(segs.p[blockIdx.z]);
+  part += (size_t)blockIdx.z * gridDim.y * cols;
   const int cx = threadIdx.x & 7, ry = threadIdx.x >> 3;
   const int c0 = blockIdx.x * 64 + cx * 8;
   const int r0 = blockIdx.y * rows_per;
@@ -204,11 +209,24 @@ void column_sum_partial(const T* x, int64_t rows, int cols, float* part, int npa
   const int rows_per = (int)((rows + nparts - 1) / nparts);
   if (cols % 8 == 0) {
     dim3 g1((unsigned)((cols + 63) / 64), (unsigned)nparts);
-    hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+    ColsumSegs segs;
+    segs.p[0] = x;
+    hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, segs, (int)rows, cols, rows_per, part);
   } else {
     dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);
     hipLaunchKernelGGL((colsum_part_scalar_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
   }
+}
+
+template <typename T>
+bool column_sum_partial_multi(const ColsumSegs& segs, int nseg, int64_t rows, int cols, float* part, int nparts,
+                              hipStream_t s) {
+  if (cols % 8 != 0 || nseg < 1 || nseg > kColsumSegs) return false;
+  if (rows == 0 || cols == 0) return true;
+  const int rows_per = (int)((rows + nparts - 1) / nparts);
+  dim3 g1((unsigned)((cols + 63) / 64), (unsigned)nparts, (unsigned)nseg);
+  hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, segs, (int)rows, cols, rows_per, part);
+  return true;
 }
 
 template <typename T>
@@ -218,7 +236,9 @@ void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, voi
   const int rows_per = (int)((rows + nparts - 1) / nparts);
   if (cols % 8 == 0) {
     dim3 g1((unsigned)((cols + 63) / 64), (unsigned)nparts);
-    hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
+    ColsumSegs segs;
+    segs.p[0] = x;
+    hipLaunchKernelGGL((colsum_part_kernel<T>), g1, dim3(256), 0, s, segs, (int)rows, cols, rows_per, part);
   } else {
     dim3 g1((unsigned)((cols + 255) / 256), (unsigned)nparts);
     hipLaunchKernelGGL((colsum_part_scalar_kernel<T>), g1, dim3(256), 0, s, x, (int)rows, cols, rows_per, part);
@@ -232,6 +252,8 @@ template void bias_act_dropout_bwd<float>(const float*, const float*, const floa
 template void bias_act_dropout_bwd<bf16_t>(const bf16_t*, const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, int, float, uint64_t, uint64_t, hipStream_t);
 template void column_sum_partial<float>(const float*, int64_t, int, float*, int, hipStream_t);
 template void column_sum_partial<bf16_t>(const bf16_t*, int64_t, int, float*, int, hipStream_t);
+template bool column_sum_partial_multi<float>(const ColsumSegs&, int, int64_t, int, float*, int, hipStream_t);
+template bool column_sum_partial_multi<bf16_t>(const ColsumSegs&, int, int64_t, int, float*, int, hipStream_t);
 template void column_sum<float>(const float*, int64_t, int, float*, int, void*, bool, bool, hipStream_t);
 template void column_sum<bf16_t>(const bf16_t*, int64_t, int, float*, int, void*, bool, bool, hipStream_t);
 

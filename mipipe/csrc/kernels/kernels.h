@@ -69,6 +69,14 @@ template <typename T>
 void bias_act_dropout_bwd(const T* dy, const T* saved, const T* bias, T* dx, int64_t rows, int cols, int act, float p,
                           uint64_t seed, uint64_t offset, hipStream_t s);
 int colsum_parts(int64_t rows, int64_t cols);
+// Up to kColsumSegs equally shaped inputs whose stage-1 column sums run as one launch.
+constexpr int kColsumSegs = 16;
+struct ColsumSegs {
+  const void* p[kColsumSegs] = {};
+};
+template <typename T>
+bool column_sum_partial_multi(const ColsumSegs& segs, int nseg, int64_t rows, int cols, float* part, int nparts,
+                              hipStream_t s);
 // Stage 1 only: per-part column sums of `rows` rows into part[nparts][cols]
 // (several inputs can write disjoint part slices and share one reduce_parts).
 template <typename T>

@@ -644,6 +644,17 @@ def test_column_sum_segments(k, cols):
     assert torch.allclose(out, expect, atol=5e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("cols,rows,nseg", [(4096, 4096, 4), (264, 300, 20), (12288, 512, 3)])
+def test_column_sum_segments_one_launch(k, cols, rows, nseg):
+    """Equally shaped segments: one stage-1 launch per 16 segments (grid.z = segment)."""
+    torch.manual_seed(10)
+    xs = [torch.randn(rows, cols, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    expect = sum(x.float().sum(0) for x in xs)
+    out = torch.empty(cols, device=DEV)
+    k.column_sum_segments(xs, out, False)
+    assert torch.allclose(out, expect, atol=5e-2, rtol=1e-3)
+
+
 def test_deferred_bias_grad(k):
     from mipipe import ops
 
