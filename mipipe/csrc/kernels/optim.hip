@@ -17,6 +17,13 @@ namespace mipipe {
 
 namespace {
 
+// Streaming 16-byte loads (nt bit): the builtins take native vector types.
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+__device__ __forceinline__ float4 nt_load(const float4* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
 __global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
                                                             float* __restrict__ partial) {
   __shared__ float sm[8];
@@ -24,7 +31,7 @@ __global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restr
   const int64_t nvec = n / 4;
   const float4* g4 = reinterpret_cast<const float4*>(g);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 v = g4[i];
+    const float4 v = nt_load(g4 + i);
     acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
   if (blockIdx.x == 0) {
@@ -88,9 +95,12 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
   const float4* G = reinterpret_cast<const float4*>(grad);
   float4* Mo = reinterpret_cast<float4*>(m);
   float4* V = reinterpret_cast<float4*>(v);
+  // Every operand is read exactly once per step: streaming (non-temporal)
+  // loads; stores stay regular (nt stores measured 3% slower on MI355X).
   for (int64_t i = tid; i < n4; i += stride) {
-    float4 p = P[i], mm = Mo[i], vv = V[i];
-    const float4 g = G[i];
+    float4 p = nt_load(P + i), mm = nt_load(Mo + i),
+           vv = nt_load(V + i);
+    const float4 g = nt_load(G + i);
     adam_one(p.x, g.x, mm.x, vv.x, h, c);
     adam_one(p.y, g.y, mm.y, vv.y, h, c);
     adam_one(p.z, g.z, mm.z, vv.z, h, c);
