@@ -113,12 +113,14 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(ColsumSegs segs, int r
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c0 < cols) {
     int r = r0 + ry;
-    for (; r + 96 < r1; r += 128) {
-      float a[4][8];
+    // 8 independent 16-byte loads in flight per lane (a pure read stream:
+    // latency hiding comes from loads in flight, not from occupancy)
+    for (; r + 224 < r1; r += 256) {
+      float a[8][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Io<T>::load8(x + (size_t)(r + 32 * u) * cols + c0, a[u]);
+      for (int u = 0; u < 8; ++u) Io<T>::load8(x + (size_t)(r + 32 * u) * cols + c0, a[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] += a[u][i];
     }
