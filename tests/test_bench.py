@@ -29,7 +29,11 @@ def _json_lines(out):
 
 
 @pytest.mark.parametrize("nproc,extra", [(1, []), (2, []), (2, ["--chunks-per-rank", "1", "--checkpoint", "always"]),
-                                         (3, ["--skips", "unet", "--chunks-per-rank", "1"])])
+                                         (3, ["--skips", "unet", "--chunks-per-rank", "1"]),
+                                         # the full-node plan shape: looping stages, split LM head, except_last
+                                         (4, ["--split-decoder", "on", "--chunks-per-rank", "2",
+                                              "--checkpoint", "except_last"]),
+                                         (8, [])])
 def test_bench_json_contract(nproc, extra):
     args = ["--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--device", "cpu", "--config", "tiny",
             "--micro-batch", "2"] + extra
