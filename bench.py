@@ -20,6 +20,7 @@ and gradient accumulation.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -28,7 +29,18 @@ import time
 import torch
 import torch.distributed as dist
 
-REF_TOKENS_PER_S = 3500.0  # reference, checkpoint='never', 2 GPUs (derived)
+# the reference's derived throughput on ITS config (main.py: fp32,
+# 16 x TransformerEncoderLayer(2048, 32, 2048), V 28,782, batch 32 x 128,
+# chunks 4, 2 GPUs).  vs_baseline is only reported for that same config
+# (--config ref_main --dtype fp32 --chunks 4 --micro-batch 8); any other
+# model / precision is a different workload and gets vs_baseline = null.
+REF_TOKENS_PER_S = {"never": 3500.0, "except_last": 2850.0}
+REF_PEAK_MB = {"never": [6361.6, 7954.0], "except_last": [5051.8, 6254.1]}
+
+
+def matches_reference(cfg, args, m, mb) -> bool:
+    return (cfg.name == "ref_main" and args.dtype == "fp32" and m == 4 and m * mb == 32
+            and cfg.seq_len == 128 and args.checkpoint in REF_TOKENS_PER_S)
 
 
 def parse():
@@ -40,6 +52,7 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=None,
                     help="sequences per micro-batch (default 32 for enc12_d4096 / ref_main, 8 for gpt2_xl)")
     ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--num-layers", type=int, default=None, help="override the model's layer count (tests)")
     ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
     ap.add_argument("--checkpoint", default="auto", choices=["auto", "never", "except_last", "always"],
                     help="auto = the BASELINE.json config for this model and PP: enc12 'except_last' at PP=8 "
@@ -54,6 +67,12 @@ def parse():
                     help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
                     help="model chunks per rank (looping placement); 'auto' = shortest simulated step")
+    ap.add_argument("--impl", default="engine", choices=["engine", "pipe"],
+                    help="engine = one process per GPU over RCCL (default; what torchrun launches); "
+                         "pipe = the single-process mipipe.Pipe driving --gpus devices with peer copies")
+    ap.add_argument("--watchdog", type=float, default=300.0,
+                    help="seconds without pipeline progress before a rank reports its pending transfers and "
+                         "exits (0 = off)")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -62,6 +81,8 @@ def parse():
 
 def main() -> int:
     args = parse()
+    if args.impl == "pipe":
+        return run_pipe(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -90,9 +111,7 @@ def main() -> int:
     from mipipe.parallel import PipelineEngine, plan_stages
     from mipipe.parallel.stage import build_stage, choose_virtual, simulate_step, stage_input_shape
 
-    cfg = CONFIGS[args.config]
-    if args.seq_len:
-        cfg.seq_len = args.seq_len
+    cfg = _config(args)
     S, E, V = cfg.seq_len, cfg.d_model, cfg.vocab
     pp = world
     if cfg.name == "gpt2_xl":
@@ -105,7 +124,7 @@ def main() -> int:
         auto_ckpt = "except_last" if pp == 8 else "never"
     if args.checkpoint == "auto":
         args.checkpoint = auto_ckpt
-    mb = args.micro_batch or {"gpt2_xl": 8, "tiny": 8}.get(cfg.name, 32)
+    mb = args.micro_batch or _default_micro_batch(cfg)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
     splits = {"auto": (False, True), "on": (True,), "off": (False,)}[args.split_decoder]
@@ -134,10 +153,13 @@ def main() -> int:
     def loss_fn(y, t):
         return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
 
+    from mipipe.parallel.watchdog import Watchdog
+
+    wd = Watchdog(args.watchdog) if args.watchdog > 0 else None
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
                             act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device,
-                            skip_shapes={"skip": ((mb, S, E), dtype)})
+                            skip_shapes={"skip": ((mb, S, E), dtype)}, watchdog=wd)
     # explicit recompute (issued before each gradient wait, as the engine does)
     from mipipe.pipeline import checkpoint_stop_for
     sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
@@ -150,24 +172,35 @@ def main() -> int:
     # every rank gets the targets: the vocabulary-split decoder's head stage needs them too
     targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(m)]
 
+    def mark(label):
+        if wd is not None:
+            wd.progress(label)
+
     def train_step():
         opt.zero_grad()
         st = engine.step(inputs, targets)
+        mark("grad-norm all-reduce")
         sq = opt.grad_sumsq()
         if world > 1:
             dist.all_reduce(sq)
         opt.step(sq)
         return st
 
-    for _ in range(args.warmup):
+    armed = wd.watch("bench start") if wd is not None else contextlib.nullcontext()
+    armed.__enter__()
+    for k in range(args.warmup):
+        mark(f"warmup step {k}")
         st = train_step()
+    mark("synchronize after warmup")
     sync()
     if world > 1:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        mark(f"timed step {k}")
         st = train_step()
+    mark("synchronize after the timed steps")
     sync()
     if world > 1:
         dist.barrier()
@@ -178,9 +211,7 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
     ms = float(ms_t.item())
-    peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 2**30 if on_gpu else 0.0], device=device)
-    if world > 1:
-        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+    peaks = _allgather([torch.cuda.max_memory_allocated(device) / 2**30 if on_gpu else 0.0], device, world)
 
     loss_val = None
     if is_last and st.loss is not None:
@@ -188,7 +219,9 @@ def main() -> int:
 
     # Bubble: one extra instrumented step, per-stage GPU busy time vs step time.
     bubble = None
+    stage_busy = None
     if not args.no_bubble and on_gpu:
+        mark("instrumented step")
         engine.measure = True
         sync()
         if world > 1:
@@ -204,6 +237,7 @@ def main() -> int:
         engine.measure = False
         step_ms = max(float(x[1]) for x in gathered)
         busys = [float(x[0]) for x in gathered]
+        stage_busy = [round(b, 3) for b in busys]
         bubble = 100.0 * (1.0 - (sum(busys) / len(busys)) / step_ms) if step_ms > 0 else None
 
     if world > 1:
@@ -211,9 +245,13 @@ def main() -> int:
         dist.broadcast(lt, src=world - 1)
         loss_val = float(lt.item())
 
+    armed.__exit__(None, None, None)
+    if wd is not None:
+        wd.close()
     tokens_per_step = m * mb * S
     value = tokens_per_step / (ms / 1e3)
     total_params = sum(int(x) for x in _allsum([n_params_local], device, world))
+    ref_match = matches_reference(cfg, args, m, mb)
     if rank == 0:
         out = {
             "metric": ("tokens/sec for 12-layer Transformer at PP=N (pipeline-parallel training)"
@@ -226,7 +264,7 @@ def main() -> int:
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / REF_TOKENS_PER_S, 2),
+            "vs_baseline": round(value / REF_TOKENS_PER_S[args.checkpoint], 2) if ref_match else None,
             "dtype": args.dtype,
             "data": "synthetic (random tokens, random-init weights)",
             "config": {
@@ -245,22 +283,151 @@ def main() -> int:
                 "skips": args.skips if not skip_pairs else f"{args.skips}: {len(skip_pairs)} long residuals, "
                                                            f"{len(engine.skip_routes)} cross-stage",
                 "parallelism": f"pp{world}",
+                "impl": "engine (one process per GPU, RCCL send/recv)",
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
             },
             "bubble_pct": None if bubble is None else round(bubble, 2),
             "bubble_theory_pct": round(100.0 * (pp - 1) / (virtual * m + pp - 1), 2),
+            "bubble_gpipe_v1_pct": round(100.0 * (pp - 1) / (m + pp - 1), 2),
+            "stage_busy_ms": stage_busy,
             "bubble_sim_pct": round(100.0 * (1 - sum(sim_busy) / len(sim_busy) / sim_t), 2),
             "loss": loss_val,
-            "peak_hbm_gib_per_gpu": round(float(peak.item()), 2) if on_gpu else None,
-            "baseline_note": "vs_baseline divides by the reference's ~3.5k tokens/s (BASELINE.md, 2 GPUs, fp32, "
-                             "16x d2048 model, checkpoint='never'); see BASELINE.md",
+            "peak_hbm_gib_per_gpu": [round(x, 2) for x in peaks] if on_gpu else None,
+            "baseline_note": _baseline_note(ref_match, args.checkpoint),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def run_pipe(args) -> int:
+    """``--impl pipe``: the single-process :class:`mipipe.Pipe` (the reference's
+    execution model, ``/root/reference/pipeline.py:100-117``) over ``--gpus``
+    devices of this process -- worker thread per device, per-(stage, chunk)
+    copy streams, native peer copies.  Same model, data, optimizer and timing
+    contract as the engine path; the pipeline is the GPipe clock schedule with
+    one partition per device."""
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--impl pipe is one process driving every GPU: run it without torchrun")
+    import mipipe
+    from mipipe import ops
+    from mipipe.optim import FlatAdam
+    from mipipe.parallel.stage import build_stage, plan_stages
+
+    on_gpu = args.device == "cuda"
+    n = args.gpus
+    if on_gpu and torch.cuda.device_count() < n:
+        raise SystemExit(f"--impl pipe --gpus {n}: only {torch.cuda.device_count()} GPU(s) visible")
+    devices = [torch.device("cuda", d) for d in range(n)] if on_gpu else [torch.device("cpu")] * n
+    if not on_gpu:
+        args.dtype = "fp32"
+    cfg = _config(args)
+    S, V = cfg.seq_len, cfg.vocab
+    m = args.chunks or (8 if (cfg.name == "gpt2_xl" and n == 8) else 4 * n)
+    if args.checkpoint == "auto":
+        args.checkpoint = "always" if cfg.name == "gpt2_xl" else ("except_last" if n == 8 else "never")
+    mb = args.micro_batch or _default_micro_batch(cfg)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(1234)
+    plan = plan_stages(cfg, n, 1, m, split_decoder=False)
+    stages = [build_stage(cfg, plan, s, device=devices[s], dtype=dtype).train() for s in range(n)]
+    params = [p for st_ in stages for p in st_.parameters()]
+    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip)
+    pipe = mipipe.Pipe(torch.nn.Sequential(*stages), chunks=m, checkpoint=args.checkpoint)
+
+    g = torch.Generator(device="cpu").manual_seed(0)
+    tokens = torch.randint(0, V, (m * mb, S + 1), generator=g)
+    x = tokens[:, :S].contiguous().to(devices[0])
+    t = tokens[:, 1:].contiguous().to(devices[-1])
+
+    def sync():
+        for d in dict.fromkeys(devices):
+            if d.type == "cuda":
+                torch.cuda.synchronize(d)
+
+    def train_step():
+        opt.zero_grad()
+        out = pipe(x).local_value()
+        loss = ops.cross_entropy(out.reshape(-1, V), t.reshape(-1))
+        loss.backward()
+        opt.step(opt.grad_sumsq())
+        return loss
+
+    for _ in range(args.warmup):
+        loss = train_step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = train_step()
+    sync()
+    ms = (time.perf_counter() - t0) / max(args.steps, 1) * 1e3
+    value = m * mb * S / (ms / 1e3)
+    ref_match = matches_reference(cfg, args, m, mb)
+    peaks = [torch.cuda.max_memory_allocated(d) / 2**30 for d in dict.fromkeys(devices)] if on_gpu else None
+    out = {
+        "metric": ("tokens/sec for 12-layer Transformer at PP=N (pipeline-parallel training)"
+                   if cfg.name == "enc12_d4096" else f"tokens/sec for {cfg.name} at PP=N (pipeline-parallel training)"),
+        "value": round(value, 1), "unit": "tokens/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": round(value / REF_TOKENS_PER_S[args.checkpoint], 2) if ref_match else None,
+        "dtype": args.dtype, "data": "synthetic (random tokens, random-init weights)",
+        "config": {
+            "model": f"{cfg.name}: {cfg.num_layers} layers d_model={cfg.d_model} nhead={cfg.nhead} "
+                     f"dim_feedforward={cfg.dim_feedforward} V={V}",
+            "params": sum(p.numel() for p in params), "global_batch": m * mb, "seq_len": S, "micro_batch": mb,
+            "chunks": m, "checkpoint": args.checkpoint, "schedule": "gpipe", "parallelism": f"pp{n}",
+            "impl": "pipe (single process, worker thread per GPU, peer copies on copy streams)",
+            "balance": plan.balance,
+        },
+        "bubble_gpipe_v1_pct": round(100.0 * (n - 1) / (m + n - 1), 2),
+        "loss": float(loss.item()),
+        "peak_hbm_gib_per_gpu": [round(p, 2) for p in peaks] if peaks else None,
+        "baseline_note": _baseline_note(ref_match, args.checkpoint),
+    }
+    print(json.dumps(out), flush=True)
+    pipe.close()
+    return 0
+
+
+def _config(args):
+    import dataclasses
+
+    from mipipe.models import CONFIGS
+
+    cfg = dataclasses.replace(CONFIGS[args.config])
+    if args.seq_len:
+        cfg.seq_len = args.seq_len
+    if args.num_layers:
+        cfg.num_layers = args.num_layers
+    return cfg
+
+
+def _default_micro_batch(cfg) -> int:
+    # ref_main: the reference's own micro-batch (batch 32 / chunks 4 = 8 sequences)
+    return {"gpt2_xl": 8, "tiny": 8, "ref_main": 8}.get(cfg.name, 32)
+
+
+def _baseline_note(ref_match: bool, checkpoint: str) -> str:
+    if ref_match:
+        return (f"vs_baseline = value / the reference's derived {REF_TOKENS_PER_S[checkpoint]:.0f} tokens/s on the SAME "
+                f"config (BASELINE.md: fp32, 16x d2048, batch 32x128, chunks 4, checkpoint={checkpoint!r}; the "
+                f"reference used 2 GPUs, profiled); reference peak allocated per GPU "
+                f"{REF_PEAK_MB[checkpoint]} MB")
+    return ("vs_baseline = null: the reference published only its own config (BASELINE.md: fp32, 16x d2048, "
+            "chunks 4, ~3.5k tokens/s on 2 GPUs); this run is a different model/precision. The like-for-like "
+            "number is `bench.py --config ref_main --dtype fp32`")
+
+
+def _allgather(vals, device, world):
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    if world == 1:
+        return [float(x) for x in t.tolist()]
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(x) for o in out for x in o.tolist()]
 
 
 def _allsum(vals, device, world):

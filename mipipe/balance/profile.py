@@ -66,8 +66,8 @@ def profile_times(module: nn.Sequential, sample: Union[List[Any], Tensor], timeo
 
     layers = list(layerwise_sandbox(module, device))
     totals = [0.0] * len(layers)
-    begun = time.perf_counter()
-    while time.perf_counter() - begun < timeout:
+
+    def one_pass(record: bool) -> None:
         b = _as_batch(list(batch) if not batch.atomic else batch.tensor)
         for k, layer in enumerate(layers):
             detach(b)
@@ -78,8 +78,16 @@ def profile_times(module: nn.Sequential, sample: Union[List[Any], Tensor], timeo
             if outs:
                 torch.autograd.backward(outs, [torch.ones_like(y) for y in outs])
             _sync(device)
-            totals[k] += time.perf_counter() - t0
+            if record:
+                totals[k] += time.perf_counter() - t0
             b = out
+
+    # One untimed pass first: the first layer would otherwise absorb one-time
+    # costs (autograd engine start-up, kernel loading, allocator growth).
+    one_pass(record=False)
+    begun = time.perf_counter()
+    while time.perf_counter() - begun < timeout:
+        one_pass(record=True)
     return [max(1, int(t * 1e6)) for t in totals]
 
 

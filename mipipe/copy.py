@@ -19,7 +19,7 @@ two devices) issued on the source copy stream and fenced with pooled events
 from __future__ import annotations
 
 from collections import deque
-from typing import Deque, List, Optional, Tuple
+from typing import Deque, List, Optional
 
 import torch
 from torch import Tensor
@@ -122,8 +122,3 @@ class Wait(torch.autograd.Function):
         wait_stream(ctx.prev_stream, ctx.next_stream)
         return (None, None) + grad_inputs
 
-
-def _apply_and_detach_ints(fn, batch_values, prev_stream, next_stream) -> Tuple:
-    out = fn.apply(prev_stream, next_stream, *batch_values)
-    # Gradients exist for floating-point tensors only.
-    return tuple(x.detach() if torch.is_tensor(x) and not x.is_floating_point() else x for x in out)

@@ -29,7 +29,7 @@ from typing import Optional, Tuple
 import torch
 from torch import Tensor, nn
 
-from ..ops._util import native_or_none
+from ..ops._util import kernels_for
 from ..ops.linear import accumulable, accumulate_wgrad, mark_gemm_weight
 
 __all__ = ["DecoderHead", "DecoderTail", "split_point", "split_decoder", "STAT_SLOTS"]
@@ -103,7 +103,7 @@ def _slots_to_stats(slots: Tensor) -> Tuple[Tensor, Tensor]:
 class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, target):  # type: ignore[override]
-        k = native_or_none(x) if x.is_cuda else None
+        k = kernels_for(x) if x.is_cuda else None
         e = x.shape[-1]
         x2 = x.reshape(-1, e).contiguous()
         logits, tile = _tile_linear(k, x2, w, b)
@@ -119,7 +119,7 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):  # type: ignore[override]
         x2, w, b, logits, ta = ctx.saved_tensors
-        k = native_or_none(x2) if x2.is_cuda else None
+        k = kernels_for(x2) if x2.is_cuda else None
         e = x2.shape[1]
         d2 = dout.reshape(-1, e + STAT_SLOTS)
         lse, g_row = _slots_to_stats(d2[:, e:])
@@ -134,7 +134,7 @@ class _HeadFn(torch.autograd.Function):
 class _TailFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, packed, w, b, target, va, vb, ignore_index):  # type: ignore[override]
-        k = native_or_none(packed) if packed.is_cuda else None
+        k = kernels_for(packed) if packed.is_cuda else None
         e = packed.shape[-1] - STAT_SLOTS
         p2 = packed.reshape(-1, e + STAT_SLOTS)
         x2 = p2[:, :e].contiguous()
@@ -157,7 +157,7 @@ class _TailFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):  # type: ignore[override]
         x2, w, b, logits, tb, lse, valid, count = ctx.saved_tensors
-        k = native_or_none(x2) if x2.is_cuda else None
+        k = kernels_for(x2) if x2.is_cuda else None
         g_row = (valid.to(torch.float32) * (g.to(torch.float32) / count)).contiguous()
         dlog = torch.zeros_like(logits)  # padded vocabulary columns stay zero
         _softmax_grad(k, logits[:, : ctx.vb], tb, lse, g_row, dlog)

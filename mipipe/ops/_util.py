@@ -8,7 +8,7 @@ from torch import Tensor
 from .. import _native_loader
 
 
-def native_or_none(t: Tensor) -> ModuleType:
+def kernels_for(t: Tensor) -> ModuleType:
     """The kernel module for a GPU tensor.  Raises when it is not built: on a
     GPU the hot path must run the HIP kernels, never a silent eager fallback."""
     return _native_loader.kernels()

@@ -7,7 +7,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ._util import native_or_none
+from ._util import kernels_for
 
 __all__ = ["bias_act_dropout", "ACTIVATIONS", "bias_act_reference"]
 
@@ -26,7 +26,7 @@ def bias_act_reference(x: Tensor, bias: Optional[Tensor], activation: Optional[s
 class _BiasActDropout(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, act, p):  # type: ignore[override]
-        k = native_or_none(x)
+        k = kernels_for(x)
         xc = x.contiguous()
         y, seed, offset = k.bias_act_fwd(xc, bias, act, p)
         # ReLU/identity backward needs only the output; GELU the pre-activation.
@@ -37,7 +37,7 @@ class _BiasActDropout(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):  # type: ignore[override]
         saved, bias = ctx.saved_tensors
-        k = native_or_none(dy)
+        k = kernels_for(dy)
         dx, db = k.bias_act_bwd(
             dy.contiguous(), saved, bias, ctx.act, ctx.p, ctx.seed, ctx.offset, bias is not None and ctx.needs_input_grad[1]
         )

@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ._util import native_or_none
+from ._util import kernels_for
 
 __all__ = ["attention", "attention_packed", "attention_reference"]
 
@@ -49,7 +49,7 @@ class _AttentionPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qkv, causal, p, scale):  # type: ignore[override]
-        kern = native_or_none(qkv)
+        kern = kernels_for(qkv)
         q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
         o, lse, seed, offset = kern.attention_fwd(q, k, v, causal, p, scale)
         ctx.save_for_backward(qkv, o, lse)
@@ -59,7 +59,7 @@ class _AttentionPacked(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):  # type: ignore[override]
         qkv, o, lse = ctx.saved_tensors
-        kern = native_or_none(do)
+        kern = kernels_for(do)
         if do.stride() != o.stride():
             do = do.contiguous()
         dqkv = torch.empty_like(qkv)
@@ -73,7 +73,7 @@ class _Attention(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q, k, v, causal, p, scale):  # type: ignore[override]
-        kern = native_or_none(q)
+        kern = kernels_for(q)
         o, lse, seed, offset = kern.attention_fwd(q, k, v, causal, p, scale)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
@@ -82,7 +82,7 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):  # type: ignore[override]
         q, k, v, o, lse = ctx.saved_tensors
-        kern = native_or_none(do)
+        kern = kernels_for(do)
         if do.stride() != o.stride():
             do = do.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
@@ -106,7 +106,7 @@ def _note_math_path(S: int, D: int, dtype) -> None:
 
 
 def _gpu_ok(t: Tensor, S: int, D: int) -> bool:
-    return t.dtype == torch.bfloat16 and native_or_none(t).attention_supported(S, D)
+    return t.dtype == torch.bfloat16 and kernels_for(t).attention_supported(S, D)
 
 
 def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, training: bool = True,

@@ -12,7 +12,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ._util import native_or_none
+from ._util import kernels_for
 from .linear import accumulable
 
 __all__ = ["embed_scale_posenc_dropout"]
@@ -21,7 +21,7 @@ __all__ = ["embed_scale_posenc_dropout"]
 class _Embed(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tokens, weight, pe, scale, p):  # type: ignore[override]
-        k = native_or_none(weight)
+        k = kernels_for(weight)
         out, seed, offset = k.embedding_fwd(tokens.contiguous(), weight, pe, scale, p)
         ctx.save_for_backward(tokens)
         ctx.weight = weight
@@ -32,7 +32,7 @@ class _Embed(torch.autograd.Function):
     def backward(ctx, dout):  # type: ignore[override]
         (tokens,) = ctx.saved_tensors
         weight = ctx.weight
-        k = native_or_none(dout)
+        k = kernels_for(dout)
         main = accumulable(weight)
         if main is not None:
             k.embedding_bwd(tokens, dout.contiguous(), main, ctx.scale, ctx.p, ctx.seed, ctx.offset)

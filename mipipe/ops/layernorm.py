@@ -12,7 +12,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ._util import native_or_none
+from ._util import kernels_for
 from .linear import accumulable
 
 __all__ = ["add_dropout_layer_norm", "layer_norm_fanout", "layer_norm_reference"]
@@ -31,7 +31,7 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, eps, p, fanout=False):  # type: ignore[override]
         ctx.set_materialize_grads(False)
-        k = native_or_none(x)
+        k = kernels_for(x)
         xc = x.contiguous()
         rc = residual.contiguous() if residual is not None else None
         y, z, mean, rstd, seed, offset = k.layernorm_fwd(xc, rc, weight, bias, eps, p, True)
@@ -52,7 +52,7 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
         z, mean, rstd, weight = ctx.saved_tensors
         if dy is None:  # only the fan-out branch carries a gradient
             return dfan, None, None, None, None, None, None
-        k = native_or_none(dy)
+        k = kernels_for(dy)
         mg = accumulable(weight)
         mb = accumulable(ctx.bias) if ctx.bias is not None else None
         add = dfan.contiguous() if dfan is not None and dfan.dtype == dy.dtype else None

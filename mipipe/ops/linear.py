@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ._util import native_or_none
+from ._util import kernels_for
 from .activation import ACTIVATIONS, bias_act_reference
 
 __all__ = ["linear", "linear_fanout", "deferred_wgrad", "flush_wgrad", "accumulate_wgrad", "mark_gemm_weight"]
@@ -80,7 +80,7 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act, p, fanout=False, res=None):  # type: ignore[override]
         ctx.set_materialize_grads(False)
-        k = native_or_none(x)
+        k = kernels_for(x)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         w = weight.contiguous()
@@ -123,7 +123,7 @@ class _Linear(torch.autograd.Function):
         dres_in = dy if ctx.has_res else None  # y = res + f(x): the residual input's gradient is dy
         if dy is None:  # only the fan-out branch carries a gradient
             return dres, None, None, None, None, None, None
-        k = native_or_none(dy)
+        k = kernels_for(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
         main_b = accumulable(bias) if need_db else None
@@ -206,7 +206,7 @@ def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
     backward: into ``w.main_grad`` (deferred inside :func:`deferred_wgrad`) when
     it exists, else returned for autograd."""
     main = getattr(w, "main_grad", None)
-    k = native_or_none(dy) if dy.is_cuda else None
+    k = kernels_for(dy) if dy.is_cuda else None
     tile = (k is not None and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
             and k.gemm_supported(w.shape[0], w.shape[1], dy.shape[0]))
     if main is not None and tile:
@@ -229,7 +229,7 @@ def flush_wgrad() -> None:
         return
     queue, _DEFERRED = _DEFERRED, {}
     for w, dys, xs in queue.values():
-        k = native_or_none(dys[0])
+        k = kernels_for(dys[0])
         if xs is None:  # a bias
             k.column_sum_segments(dys, w.main_grad, True)
             continue

@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ._util import native_or_none
+from ._util import kernels_for
 
 __all__ = ["cross_entropy", "mark_zero_padded", "take_zero_padded"]
 
@@ -43,7 +43,7 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, ignore_index):  # type: ignore[override]
         _ZERO_PADDED.clear()  # marks live from a CE backward to the slice backward of the same pass
-        k = native_or_none(logits)
+        k = kernels_for(logits)
         lc = logits if (logits.dim() == 2 and logits.stride(1) == 1) else logits.contiguous()
         loss_rows, lse = k.cross_entropy_fwd(lc, target.contiguous(), ignore_index)
         count = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
@@ -54,7 +54,7 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):  # type: ignore[override]
         logits, target, lse, count = ctx.saved_tensors
-        k = native_or_none(logits)
+        k = kernels_for(logits)
         scale = (dloss.to(torch.float32) / count).reshape(1).contiguous()
         n, v = logits.shape
         ld = logits.stride(0)

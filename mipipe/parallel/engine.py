@@ -42,6 +42,7 @@ compute.  Per-stage busy time is measured with HIP events (bubble %).
 from __future__ import annotations
 
 import time
+from contextlib import contextmanager
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
 
@@ -55,6 +56,7 @@ from ..pipeline import checkpoint_stop_for
 from ..skip.tracker import use_skip_tracker
 from .p2p import Channels, DirectLinks
 from .skips import EngineSkipTracker, SkipRoute, gather_routes
+from .watchdog import Watchdog
 
 __all__ = ["PipelineEngine", "StepStats", "schedule_actions"]
 
@@ -97,6 +99,11 @@ def schedule_actions(kind: str, m: int, n: int, j: int, virtual: int = 1) -> Lis
     raise ValueError(f"unknown schedule {kind!r}")
 
 
+@contextmanager
+def _null():
+    yield
+
+
 class _RNGState:
     __slots__ = ("cpu", "dev")
 
@@ -130,6 +137,11 @@ class PipelineEngine:
             whose tensor is not shaped like the popping stage's input.
         skip_routes: explicit cross-stage routes (default: gathered from every
             rank's ``@skippable`` layers at construction, a collective).
+        watchdog: a :class:`~mipipe.parallel.watchdog.Watchdog` (or a timeout
+            in seconds to create one).  The engine arms it during :meth:`step`,
+            marks every action, and registers every transfer, so a stalled
+            step ends the process with a report naming the transfer that never
+            completed.  Callers can arm it around their own waits too.
     """
 
     def __init__(
@@ -148,6 +160,7 @@ class PipelineEngine:
         defer_wgrad: bool = True,
         skip_shapes: Optional[Dict[str, Tuple[Sequence[int], torch.dtype]]] = None,
         skip_routes: Optional[Dict[str, SkipRoute]] = None,
+        watchdog: Union[None, float, Watchdog] = None,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
             raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
@@ -172,12 +185,17 @@ class PipelineEngine:
         self.defer_wgrad = defer_wgrad
         if schedule == "1f1b" and self.virtual > 1:
             raise ValueError("1f1b supports one chunk per rank")
+        if isinstance(watchdog, (int, float)):
+            watchdog = Watchdog(float(watchdog))
+        self.watchdog: Optional[Watchdog] = watchdog
+        self._action = "construction"
         if isinstance(group, Channels):
             self.chan: Optional[Channels] = group
         elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
             self.chan = Channels(ranks, wrap=self.virtual > 1)
-            self.chan.warmup(device or next(mods[0].parameters()).device)
+            with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
+                self.chan.warmup(device or next(mods[0].parameters()).device)
         else:
             self.chan = None
         if self.chan is not None:
@@ -193,7 +211,26 @@ class PipelineEngine:
         # kept for callers: rank-level first/last of the whole pipeline
         self.is_first = self.rank == 0
         self.is_last = self.rank == n - 1
+        self._action = "idle"
+        if self.watchdog is not None and self.watchdog.describe is None:
+            self.watchdog.describe = self.describe
         self._setup_skips(group, skip_shapes, skip_routes)
+
+    # ------------------------------------------------------------------ watchdog
+    def describe(self) -> str:
+        """One line of engine state for failure reports."""
+        return (f"pipeline rank {self.rank}/{self.world}, virtual stages {self.vstage}, chunks {self.chunks}, "
+                f"schedule {self.schedule}, checkpoint {self.checkpoint}, current action {self._action}")
+
+    def _mark(self, label: str) -> None:
+        self._action = label
+        if self.watchdog is not None:
+            self.watchdog.progress(label)
+
+    def _track(self, label: str, work):
+        if self.watchdog is not None:
+            self.watchdog.pending.add(label, work)
+        return work
 
     # ------------------------------------------------------------------ skips
     def _setup_skips(self, group, skip_shapes, skip_routes) -> None:
@@ -219,7 +256,8 @@ class PipelineEngine:
         self._skip_links: Optional[DirectLinks] = None
         if pairs:
             self._skip_links = DirectLinks(self.chan.ranks, pairs)
-            self._skip_links.warmup(self.device)
+            with (self.watchdog.watch("skip link warm-up") if self.watchdog is not None else _null()):
+                self._skip_links.warmup(self.device)
 
     def _actions_of(self, rank: int, training: bool) -> List[Tuple[str, int, int]]:
         if training:
@@ -246,7 +284,9 @@ class PipelineEngine:
                     if not grad and not (r.stash_vstage == vs and r.pop_vstage % n == self.rank):
                         continue
                     buf = torch.empty(r.shape, dtype=r.dtype, device=self.device)
-                    into[(key, i)] = (buf, self._skip_links.recv(src, self.rank, buf))
+                    what = "skip gradient" if grad else "skip"
+                    into[(key, i)] = (buf, self._track(f"recv {what} '{key}' micro-batch {i} from rank {src}",
+                                                       self._skip_links.recv(src, self.rank, buf)))
 
     # ------------------------------------------------------------------ helpers
     def _first(self, c: int) -> bool:
@@ -300,6 +340,8 @@ class PipelineEngine:
         t0 = time.perf_counter()
         chan = self.chan
         routes = self.skip_routes
+        if self.watchdog is not None:
+            self.watchdog.pending.clear()
 
         # Post every activation receive of the forward phase up front, in the
         # order the upstream rank sends them (chunk-major, micro-batch minor).
@@ -309,7 +351,8 @@ class PipelineEngine:
             if not self._first(c):
                 for i in range(m):
                     recv_x[c][i] = self._new_act(c)
-                    recv_w[c][i] = chan.recv_act(recv_x[c][i])
+                    recv_w[c][i] = self._track(f"recv activation: virtual stage {self.vstage[c]} micro-batch {i} "
+                                               f"from rank {(self.rank - 1) % n}", chan.recv_act(recv_x[c][i]))
         # ... and every skip receive (each skip has its own directed link).
         sk_rx: Dict = {}
         sk_grad_rx: Dict = {}
@@ -364,7 +407,8 @@ class PipelineEngine:
                 if tuple(t.shape) != tuple(r.shape) or t.dtype != r.dtype:
                     raise RuntimeError(f"skip '{key}' is {tuple(t.shape)} {t.dtype}, the popping stage expects "
                                        f"{tuple(r.shape)} {r.dtype} (pass skip_shapes=)")
-                sends.append(self._skip_links.send(self.rank, dst, t))
+                sends.append(self._track(f"send skip '{key}' micro-batch {i} to rank {dst}",
+                                         self._skip_links.send(self.rank, dst, t)))
 
         def forward(c: int, i: int) -> None:
             mod = self.modules[c]
@@ -398,7 +442,8 @@ class PipelineEngine:
             stage_out[c][i] = y if (training and i >= stop) else None
             out_meta[c][i] = torch.empty(y.shape, dtype=y.dtype, device="meta")
             if not last:
-                sends.append(chan.send_act(y.detach()))
+                sends.append(self._track(f"send activation: virtual stage {self.vstage[c]} micro-batch {i} to rank "
+                                         f"{(self.rank + 1) % n}", chan.send_act(y.detach())))
             ship_skips(c, i, tracker)
             if tracker is not None and training and i >= stop:
                 skip_out[c][i] = tracker.outgoing
@@ -406,7 +451,8 @@ class PipelineEngine:
         def post_grad_recv(c: int, i: int) -> None:
             if not self._last(c) and grad_w[c][i] is None:
                 grad_buf[c][i] = self._new_act(c, out_meta[c][i])
-                grad_w[c][i] = chan.recv_grad(grad_buf[c][i])
+                grad_w[c][i] = self._track(f"recv gradient: virtual stage {self.vstage[c]} micro-batch {i} from rank "
+                                           f"{(self.rank + 1) % n}", chan.recv_grad(grad_buf[c][i]))
 
         def backward(c: int, i: int) -> None:
             mod = self.modules[c]
@@ -470,7 +516,8 @@ class PipelineEngine:
                 events.append(("B", tm))
             stage_out[c][i] = grad_buf[c][i] = grad_w[c][i] = None
             if not self._first(c):
-                sends.append(chan.send_grad(x.grad))
+                sends.append(self._track(f"send gradient: virtual stage {self.vstage[c]} micro-batch {i} to rank "
+                                         f"{(self.rank - 1) % n}", chan.send_grad(x.grad)))
             for key in self._pops[c]:
                 r = routes[key]
                 if not r.has_grad:
@@ -481,14 +528,21 @@ class PipelineEngine:
                 if src == self.rank:
                     sk_local_grad[(key, i)] = g
                 else:
-                    sends.append(self._skip_links.send(self.rank, src, g))
+                    sends.append(self._track(f"send skip gradient '{key}' micro-batch {i} to rank {src}",
+                                             self._skip_links.send(self.rank, src, g)))
             stage_in[c][i] = rng[c][i] = skip_in[c][i] = skip_out[c][i] = None
 
         actions = self._actions_of(self.rank, training)
         started_backward = False
         defer = ops.deferred_wgrad() if (training and self.defer_wgrad) else None
+        wd = self.watchdog
+        armed = wd.watch("step start") if wd is not None else None
+        if armed is not None:
+            armed.__enter__()
         try:
             for kind, c, i in actions:
+                self._mark(f"{'forward' if kind == 'F' else 'backward'} virtual stage {self.vstage[c]} "
+                           f"micro-batch {i}")
                 if kind == "F":
                     with torch.set_grad_enabled(training):
                         forward(c, i)
@@ -508,6 +562,7 @@ class PipelineEngine:
                     post_grad_recv(c, i)
                     backward(c, i)
             if defer is not None and started_backward:
+                self._mark("deferred weight gradients")
                 tm = self._timer()
                 if tm:
                     tm[0].record()
@@ -516,12 +571,18 @@ class PipelineEngine:
                 if tm:
                     tm[1].record()
                     events.append(("B", tm))
+            self._mark("waiting for this step's sends")
+            for w in sends:
+                w.wait()
+        except BaseException as exc:
+            self._on_error(exc)
+            raise
         finally:
             if defer is not None and started_backward:
                 defer.__exit__(RuntimeError, None, None)
-
-        for w in sends:
-            w.wait()
+            if armed is not None:
+                armed.__exit__(None, None, None)
+        self._mark("step done")
 
         if losses:
             stats.loss = torch.stack(losses).float().mean()
@@ -533,3 +594,18 @@ class PipelineEngine:
             stats.busy_ms = sum(stats.forward_ms) + sum(stats.backward_ms)
         stats.step_ms = (time.perf_counter() - t0) * 1e3
         return stats
+
+    def _on_error(self, exc: BaseException) -> None:
+        """An action raised: say where, list the transfers left in flight.
+
+        The exception then propagates (the process ends and ``torchrun`` stops
+        the peers, which would otherwise wait for this rank's sends)."""
+        import sys
+
+        lines = [f"[mipipe engine] rank {self.rank}: {type(exc).__name__} during {self._action}: {exc}"]
+        if self.watchdog is not None:
+            left = self.watchdog.pending.unfinished()
+            if left:
+                lines.append(f"[mipipe engine] rank {self.rank}: {len(left)} transfer(s) left in flight:")
+                lines.extend(f"[mipipe engine]   {u}" for u in left[:32])
+        print("\n".join(lines), file=sys.stderr, flush=True)

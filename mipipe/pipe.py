@@ -152,6 +152,24 @@ def _verify_splitting(module: nn.Sequential, partitions: List[nn.Sequential], de
             owner.setdefault(id(p), idx)
 
 
+def _enable_peer_access(devices: List[torch.device]) -> None:
+    """Direct xGMI access between every pair of the pipeline's GPUs.
+
+    Without it a ``hipMemcpyPeerAsync`` between two devices may be staged
+    through host memory; with it the SDMA engine (or a kernel) reads/writes the
+    peer's HBM over the link that joins them.  Idempotent; a no-op without the
+    native runtime or with fewer than two GPUs."""
+    indices = sorted({d.index if d.index is not None else torch.cuda.current_device()
+                      for d in devices if d.type == "cuda"})
+    if len(indices) < 2:
+        return
+    from .stream import _native
+
+    rt = _native()
+    if rt is not None:
+        rt.enable_peer_access(indices)
+
+
 _MOVING_DENIED = "denied to move parameters and buffers, because Pipe should manage device placement"
 MOVING_DENIED = TypeError(_MOVING_DENIED)
 
@@ -166,6 +184,13 @@ class Pipe(nn.Module):
         checkpoint: ``"always"``, ``"except_last"`` or ``"never"``.
         deferred_batch_norm: track BatchNorm statistics over the whole mini-batch.
         return_rref: return an RRef (upstream behaviour, default) or the output.
+        copy_streams: copy streams per partition.  ``None`` (default) keeps the
+            reference's one stream per (partition, micro-batch)
+            (``/root/reference/pipe.py:417-429``); an integer ``k`` gives each
+            partition ``k`` streams shared round-robin by the micro-batches.
+            A HIP process has few hardware queues (``GPU_MAX_HW_QUEUES``, 4 by
+            default), so ``chunks x partitions`` streams alias onto the same
+            queues anyway; see ``profiles/copy_streams_ab.txt``.
     """
 
     def __init__(
@@ -176,6 +201,7 @@ class Pipe(nn.Module):
         deferred_batch_norm: bool = False,
         *,
         return_rref: bool = True,
+        copy_streams: Optional[int] = None,
     ) -> None:
         super().__init__()
         chunks = int(chunks)
@@ -188,15 +214,19 @@ class Pipe(nn.Module):
         _verify_module(module)
         verify_skippables(module)
 
+        if copy_streams is not None and int(copy_streams) <= 0:
+            raise ValueError("copy_streams must be a positive integer or None")
         self.chunks = chunks
         self.checkpoint = checkpoint
         self.return_rref = return_rref
+        self.copy_streams_per_partition = None if copy_streams is None else int(copy_streams)
 
         if deferred_batch_norm:
             module = DeferredBatchNorm.convert_deferred_batch_norm(module, chunks)
 
         self.partitions, self.devices = _split_module(module)
         _verify_splitting(module, self.partitions, self.devices)
+        _enable_peer_access(self.devices)
 
         self._copy_streams: List[List[AbstractStream]] = []
         self._skip_layout: SkipLayout = inspect_skip_layout(self.partitions)
@@ -241,8 +271,13 @@ class Pipe(nn.Module):
         cached -- reusing streams keeps the caching allocator's per-stream pools
         small (``/root/reference/pipe.py:417-424``)."""
         if not self._copy_streams:
+            k = self.copy_streams_per_partition
             for device in self.devices:
-                self._copy_streams.append([new_stream(device) for _ in range(self.chunks)])
+                if k is None:
+                    self._copy_streams.append([new_stream(device) for _ in range(self.chunks)])
+                else:
+                    pool = [new_stream(device) for _ in range(min(k, self.chunks))]
+                    self._copy_streams.append([pool[i % len(pool)] for i in range(self.chunks)])
         return self._copy_streams
 
     def close(self) -> None:

@@ -28,13 +28,37 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
-@pytest.mark.parametrize("nproc,extra", [(1, []), (2, []), (2, ["--chunks-per-rank", "1", "--checkpoint", "always"]),
-                                         (3, ["--skips", "unet", "--chunks-per-rank", "1"]),
-                                         # the full-node plan shape: looping stages, split LM head, except_last
-                                         (4, ["--split-decoder", "on", "--chunks-per-rank", "2",
-                                              "--checkpoint", "except_last"]),
-                                         (8, [])])
-def test_bench_json_contract(nproc, extra):
+# (extra args, expected plan fields)
+CASES = [
+    (1, [], {}),
+    (2, [], {}),
+    (2, ["--chunks-per-rank", "1", "--checkpoint", "always"], {"virtual_chunks_per_rank": 1, "checkpoint": "always"}),
+    (3, ["--skips", "unet", "--chunks-per-rank", "1"], {"virtual_chunks_per_rank": 1}),
+    # the full-node plan shape forced on 4 ranks: looping stages, split LM head, except_last
+    (4, ["--split-decoder", "on", "--chunks-per-rank", "2", "--checkpoint", "except_last"],
+     {"virtual_chunks_per_rank": 2, "vocab_split_decoder": True, "checkpoint": "except_last"}),
+    # 8 ranks with the DEFAULT plan choice: with >= 4 layers the planner must pick what it picks for
+    # enc12_d4096 at PP=8 (2 chunks per rank, split head, except_last at 32 micro-batches)
+    (8, ["--num-layers", "4"], {"virtual_chunks_per_rank": 2, "vocab_split_decoder": True,
+                                "checkpoint": "except_last", "chunks": 32}),
+]
+
+
+def test_default_pp8_plan_matches_enc12():
+    """The 8-rank contract case stands for the enc12_d4096 PP=8 plan."""
+    import dataclasses
+
+    from mipipe.models import CONFIGS
+    from mipipe.parallel.stage import choose_virtual
+
+    ck = 2.0 + 31 / 32
+    v, plan = choose_virtual(CONFIGS["enc12_d4096"], 8, 32, bwd_ratio=ck)
+    tv, tplan = choose_virtual(dataclasses.replace(CONFIGS["tiny"], num_layers=4), 8, 32, bwd_ratio=ck)
+    assert (v, plan.split_decoder) == (tv, tplan.split_decoder) == (2, True)
+
+
+@pytest.mark.parametrize("nproc,extra,expect", CASES)
+def test_bench_json_contract(nproc, extra, expect):
     args = ["--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--device", "cpu", "--config", "tiny",
             "--micro-batch", "2"] + extra
     if nproc == 1:
@@ -58,3 +82,39 @@ def test_bench_json_contract(nproc, extra):
     tokens = cfg["global_batch"] * cfg["seq_len"]
     assert abs(rec["value"] - tokens / (rec["ms_per_step"] / 1e3)) / rec["value"] < 0.01
     assert rec["loss"] is not None and rec["loss"] > 0
+    for k, v in expect.items():
+        assert cfg[k] == v, (k, cfg[k], v)
+    # metrics: per-GPU / per-stage lists (None on the CPU plumbing run), both bubble models
+    assert rec["peak_hbm_gib_per_gpu"] is None and rec["stage_busy_ms"] is None
+    assert rec["bubble_gpipe_v1_pct"] == pytest.approx(100.0 * (nproc - 1) / (cfg["chunks"] + nproc - 1), abs=0.01)
+    v = cfg["virtual_chunks_per_rank"]
+    assert rec["bubble_theory_pct"] == pytest.approx(100.0 * (nproc - 1) / (v * cfg["chunks"] + nproc - 1), abs=0.01)
+    assert rec["vs_baseline"] is None  # not the reference's config
+
+
+def test_bench_pipe_impl_cpu():
+    """--impl pipe: the single-process Pipe path emits the same contract."""
+    args = ["--impl", "pipe", "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--config", "tiny",
+            "--micro-batch", "2"]
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                         timeout=600, cwd="/tmp", env={**os.environ, "CUDA_VISIBLE_DEVICES": ""})
+    assert out.returncode == 0, out.stderr[-3000:]
+    (rec,) = _json_lines(out.stdout)
+    assert REQUIRED <= set(rec) and rec["config"]["impl"].startswith("pipe")
+    assert rec["n_gpus"] == 2 and rec["config"]["chunks"] == 8 and rec["value"] > 0
+
+
+def test_vs_baseline_only_on_reference_config():
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from mipipe.models import CONFIGS
+
+    ns = argparse.Namespace(dtype="fp32", checkpoint="never")
+    assert bench.matches_reference(CONFIGS["ref_main"], ns, 4, 8)
+    assert not bench.matches_reference(CONFIGS["ref_main"], argparse.Namespace(dtype="bf16", checkpoint="never"), 4, 8)
+    assert not bench.matches_reference(CONFIGS["enc12_d4096"], ns, 4, 8)
+    assert not bench.matches_reference(CONFIGS["ref_main"], ns, 8, 4)

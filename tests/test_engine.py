@@ -20,6 +20,8 @@ from mipipe.parallel import PipelineEngine, plan_stages, schedule_actions
 from mipipe.models.transformer import merge_units, pipeline_units
 from mipipe.parallel.stage import block_costs, stage_input_shape
 
+from helpers.engine_cases import ENGINE_CASES, run_engine_case
+
 
 def _pairs(acts):
     return [(k, i) for k, c, i in acts]
@@ -341,3 +343,11 @@ def test_engine_deferred_wgrad_same_gradients():
     for n, g in grads[False].items():
         scale = g.abs().max().item() + 1e-6
         assert (grads[True][n] - g).abs().max().item() < 1e-2 * scale, n
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("checkpoint,virtual,split,skips", ENGINE_CASES)
+def test_engine_cases_gloo_emulation(world, checkpoint, virtual, split, skips):
+    """The cases tests/test_gpu_pipeline.py runs over RCCL on 2 / 4 GPUs, here
+    rank-for-rank over gloo on CPU (fp32, exact comparison)."""
+    run_engine_case("cpu", world, checkpoint, virtual, split, skips)

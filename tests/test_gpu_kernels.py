@@ -602,10 +602,31 @@ def test_transformer_layer_bf16_kernels_vs_torch(k):
     ref = nn.TransformerEncoderLayer(E, H, F_, dropout=0.0, batch_first=True).to(DEV)
     ours = TransformerEncoderLayer(E, H, F_, dropout=0.0, device=DEV).load_from_torch(ref).to(torch.bfloat16)
     x = torch.randn(B, S, E, device=DEV)
-    y = ours(x.to(torch.bfloat16).requires_grad_())
-    yr = ref(x)
+    xb = x.to(torch.bfloat16).requires_grad_()
+    xr = x.clone().requires_grad_()
+    y = ours(xb)
+    yr = ref(xr)
     err = (y.float() - yr).abs().max().item()
     assert err < 0.1, err
+    # backward: input and every parameter gradient, relative to the fp32 gradient's scale
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+
+    def rel(a, b):
+        return (a.float() - b.float()).abs().max().item() / (b.float().abs().max().item() + 1e-6)
+
+    assert rel(xb.grad, xr.grad) < 3e-2, rel(xb.grad, xr.grad)
+    attn, ff = ours[0], ours[1]
+    pairs = [(attn.core.in_proj_weight, ref.self_attn.in_proj_weight), (attn.core.in_proj_bias, ref.self_attn.in_proj_bias),
+             (attn.out.out_proj_weight, ref.self_attn.out_proj.weight), (attn.out.out_proj_bias, ref.self_attn.out_proj.bias),
+             (attn.out.norm_weight, ref.norm1.weight), (attn.out.norm_bias, ref.norm1.bias),
+             (ff.fc_in.linear1_weight, ref.linear1.weight), (ff.fc_in.linear1_bias, ref.linear1.bias),
+             (ff.fc_out.linear2_weight, ref.linear2.weight), (ff.fc_out.linear2_bias, ref.linear2.bias),
+             (ff.fc_out.norm_weight, ref.norm2.weight), (ff.fc_out.norm_bias, ref.norm2.bias)]
+    for ours_p, ref_p in pairs:
+        got = ours_p.main_grad if getattr(ours_p, "main_grad", None) is not None else ours_p.grad
+        assert got is not None and rel(got, ref_p.grad) < 3e-2, (tuple(ref_p.shape), rel(got, ref_p.grad))
 
 
 def test_vocab_split_decoder_gpu(k):

@@ -1,0 +1,203 @@
+"""The pipeline on MI355X with the HIP kernels: Pipe and engine end to end.
+
+* ``mipipe.Pipe`` running the bf16 LM blocks (MFMA GEMMs, flash attention,
+  fused LN, FlatAdam) against the same blocks as one ``nn.Sequential``
+  (SURVEY §4 transparency, on our kernels, not ``nn.Linear``);
+* activation-checkpoint recompute replays dropout bit-exactly on our kernels
+  (LN / GEMM-epilogue / attention / embedding dropout): ``always`` and
+  ``except_last`` gradients are BIT-IDENTICAL to ``never``, for the engine and
+  for ``Pipe`` (``/root/reference/README.md:517-537``);
+* multi-GPU: ``Pipe`` over ``cuda:0..N-1`` (native peer copies over xGMI) and
+  the engine over RCCL (``nccl`` backend, one rank per GPU) against the
+  single-rank engine -- skipped on a one-GPU box (``multigpu``).
+"""
+import copy
+import dataclasses
+
+import pytest
+import torch
+
+from mipipe import Pipe, ops
+from mipipe.models import CONFIGS, build_lm_blocks
+from mipipe.optim import FlatAdam
+from mipipe.parallel import PipelineEngine
+
+from helpers.engine_cases import ENGINE_CASES, run_engine_case
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _cfg(dropout=0.0, layers=2):
+    base = CONFIGS["tiny"]
+    cfg = dataclasses.replace(base, dropout=dropout, num_layers=layers, d_model=256, nhead=4, dim_feedforward=512,
+                              vocab=512, seq_len=64)
+    return cfg
+
+
+def _data(cfg, m, mb, seed=7):
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(0, cfg.vocab, (m, mb, cfg.seq_len + 1), generator=g)
+    return [tok[i, :, :-1] for i in range(m)], [tok[i, :, 1:].contiguous() for i in range(m)]
+
+
+def _loss_fn(cfg):
+    return lambda y, t: ops.cross_entropy(y.reshape(-1, cfg.vocab), t.reshape(-1))
+
+
+def _ngpu():
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+# ------------------------------------------------------------------ Pipe on our kernels
+def _pipe_vs_sequential(devices, checkpoint, copy_streams=None, dropout=0.0):
+    cfg = _cfg(dropout=dropout)
+    m, mb = 4, 2
+    torch.manual_seed(0)
+    blocks = build_lm_blocks(cfg, dtype=torch.bfloat16)
+    ref_blocks = copy.deepcopy(blocks)
+    # reference: one device, the whole mini-batch in one pass
+    ref = torch.nn.Sequential(*ref_blocks).to(DEV).train()
+    ref_opt = FlatAdam(ref.parameters(), lr=1e-3)
+    inputs, targets = _data(cfg, m, mb)
+    x = torch.cat(inputs).to(DEV)
+    t = torch.cat(targets)
+    ref_opt.zero_grad()
+    loss_ref = _loss_fn(cfg)(ref(x), t.to(DEV))
+    loss_ref.backward()
+    ref_opt.fold_grads()
+
+    # pipe: blocks spread evenly over the devices
+    n = len(devices)
+    per = (len(blocks) + n - 1) // n
+    parts = [torch.nn.Sequential(*blocks[i * per:(i + 1) * per]).to(devices[i]) for i in range(n)
+             if blocks[i * per:(i + 1) * per]]
+    model = torch.nn.Sequential(*parts).train()
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    pipe = Pipe(model, chunks=m, checkpoint=checkpoint, copy_streams=copy_streams)
+    try:
+        opt.zero_grad()
+        out = pipe(x).local_value()
+        loss = _loss_fn(cfg)(out, t.to(out.device))
+        loss.backward()
+        opt.fold_grads()
+    finally:
+        pipe.close()
+    assert abs(float(loss) - float(loss_ref)) < 2e-3 * abs(float(loss_ref))
+    for (name, p), q in zip(model.named_parameters(), ref.parameters()):
+        g, gr = p.main_grad.float().cpu(), q.main_grad.float().cpu()
+        scale = gr.abs().max().item() + 1e-6
+        assert (g - gr).abs().max().item() < 2e-2 * scale, name
+    return pipe
+
+
+@pytest.mark.parametrize("checkpoint", ["never", "except_last", "always"])
+def test_pipe_lm_bf16_one_gpu(checkpoint):
+    """Pipe on one MI355X (one partition: scatter, worker thread, checkpoint /
+    recompute, gather) with the HIP-kernel LM blocks == nn.Sequential."""
+    _pipe_vs_sequential([DEV], checkpoint)
+
+
+@pytest.mark.multigpu
+@pytest.mark.parametrize("ngpu", [2, 4, 8])
+@pytest.mark.parametrize("checkpoint,copy_streams", [("never", None), ("except_last", None), ("always", 2),
+                                                     ("except_last", 1)])
+def test_pipe_lm_bf16_multi_gpu(ngpu, checkpoint, copy_streams):
+    """Pipe over cuda:0..N-1 (peer copies over xGMI on copy streams) == nn.Sequential on one GPU."""
+    if _ngpu() < ngpu:
+        pytest.skip(f"needs {ngpu} GPUs")
+    pipe = _pipe_vs_sequential([torch.device("cuda", d) for d in range(ngpu)], checkpoint, copy_streams)
+    assert len(pipe.devices) == ngpu
+
+
+def test_pipe_copy_stream_pool():
+    """copy_streams=k: each partition gets k distinct streams shared round-robin."""
+    lin = torch.nn.Linear(8, 8).to(DEV)
+    pipe = Pipe(torch.nn.Sequential(lin), chunks=5, copy_streams=2)
+    (row,) = pipe._copy_streams
+    assert len(row) == 5 and len({id(s) for s in row}) == 2 and row[0] is row[2] is row[4]
+    pipe.close()
+    pipe = Pipe(torch.nn.Sequential(lin), chunks=5)
+    assert len({id(s) for s in pipe._copy_streams[0]}) == 5
+    pipe.close()
+    with pytest.raises(ValueError):
+        Pipe(torch.nn.Sequential(lin), chunks=2, copy_streams=0)
+
+
+# ------------------------------------------------------------------ bit-exact recompute
+def _engine_grads(checkpoint, cfg, m, mb, seed=99):
+    torch.manual_seed(0)
+    full = torch.nn.Sequential(*build_lm_blocks(cfg)).train().to(DEV, torch.bfloat16)
+    opt = FlatAdam(full.parameters(), lr=1e-3)
+    eng = PipelineEngine(full, chunks=m, checkpoint=checkpoint, act_shape=(mb, cfg.seq_len),
+                         act_dtype=torch.bfloat16, loss_fn=_loss_fn(cfg), device=DEV)
+    inputs, targets = _data(cfg, m, mb)
+    opt.zero_grad()
+    torch.manual_seed(seed)
+    st = eng.step([x.to(DEV) for x in inputs], [t.to(DEV) for t in targets])
+    opt.fold_grads()
+    torch.cuda.synchronize()
+    return float(st.loss), {n: p.main_grad.clone() for n, p in full.named_parameters()}
+
+
+def test_engine_recompute_bit_identical_with_dropout():
+    """Engine, dropout 0.2 everywhere (embedding, attention, GEMM epilogues, LN):
+    recomputed micro-batches regenerate the same Philox masks, so the gradients
+    of 'always' / 'except_last' equal 'never' bit for bit."""
+    cfg = _cfg(dropout=0.2)
+    m, mb = 4, 2
+    loss0, g0 = _engine_grads("never", cfg, m, mb)
+    # dropout is live: a different RNG seed gives different gradients
+    _, g_other = _engine_grads("never", cfg, m, mb, seed=100)
+    assert any(not torch.equal(g0[n], g_other[n]) for n in g0)
+    for mode in ("except_last", "always"):
+        loss, g = _engine_grads(mode, cfg, m, mb)
+        assert loss == loss0, mode
+        for n in g0:
+            assert torch.equal(g[n], g0[n]), (mode, n, (g[n] - g0[n]).abs().max().item())
+
+
+def _pipe_grads(checkpoint, cfg, m, mb, seed=99):
+    torch.manual_seed(0)
+    blocks = build_lm_blocks(cfg, dtype=torch.bfloat16)
+    model = torch.nn.Sequential(torch.nn.Sequential(*blocks).to(DEV)).train()
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    pipe = Pipe(model, chunks=m, checkpoint=checkpoint)
+    inputs, targets = _data(cfg, m, mb)
+    try:
+        opt.zero_grad()
+        torch.manual_seed(seed)
+        out = pipe(torch.cat(inputs).to(DEV)).local_value()
+        loss = _loss_fn(cfg)(out, torch.cat(targets).to(DEV))
+        loss.backward()
+        opt.fold_grads()
+        torch.cuda.synchronize()
+    finally:
+        pipe.close()
+    return float(loss), {n: p.main_grad.clone() for n, p in model.named_parameters()}
+
+
+def test_pipe_recompute_bit_identical_with_dropout():
+    """Same property through the single-process Pipe's Checkpoint/Recompute."""
+    cfg = _cfg(dropout=0.2)
+    m, mb = 4, 2
+    loss0, g0 = _pipe_grads("never", cfg, m, mb)
+    for mode in ("except_last", "always"):
+        loss, g = _pipe_grads(mode, cfg, m, mb)
+        assert loss == loss0, mode
+        for n in g0:
+            assert torch.equal(g[n], g0[n]), (mode, n, (g[n] - g0[n]).abs().max().item())
+
+
+# ------------------------------------------------------------------ engine over RCCL
+@pytest.mark.multigpu
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("checkpoint,virtual,split,skips", ENGINE_CASES)
+def test_engine_nccl_matches_single_rank(world, checkpoint, virtual, split, skips):
+    """One rank per GPU over RCCL (isend/irecv on per-direction communicators)
+    vs the single-rank engine; the same cases run over gloo on CPU in
+    tests/test_engine.py::test_engine_cases_gloo_emulation."""
+    if _ngpu() < world:
+        pytest.skip(f"needs {world} GPUs")
+    run_engine_case("nccl", world, checkpoint, virtual, split, skips)

@@ -150,6 +150,27 @@ def test_balance_by_time_cpu():
     assert balance == [5, 1]
 
 
+def test_balance_by_size_mocked_profile(monkeypatch):
+    """balance_by_size forwards its arguments to profile_sizes and balances the
+    returned per-layer sizes (no GPU: the profiler is mocked)."""
+    import mipipe.balance as B
+
+    seen = {}
+
+    def fake_profile_sizes(module, input, chunks, param_scale, device):
+        seen.update(n=len(module), chunks=chunks, param_scale=param_scale, device=device)
+        return [10, 10, 10, 10, 40, 40][: len(module)]
+
+    monkeypatch.setattr(B, "profile_sizes", fake_profile_sizes)
+    model = nn.Sequential(*[nn.Linear(2, 2) for _ in range(6)])
+    balance = B.balance_by_size(2, model, torch.rand(4, 2), chunks=4, param_scale=4.0, device="cpu")
+    assert balance == [5, 1] or balance == [4, 2]
+    assert sum(balance) == 6
+    # the largest partition cost is minimal: [4,2] -> max(40,80)=80; [5,1] -> max(80,40)=80
+    assert seen == {"n": 6, "chunks": 4, "param_scale": 4.0, "device": torch.device("cpu")}
+    assert B.balance_by_size(3, model, torch.rand(4, 2), device="cpu") == [4, 1, 1]
+
+
 def test_partition_model():
     model = nn.Sequential(*[nn.Linear(2, 2) for _ in range(5)])
     grouped = partition_model(model, [2, 3], devices=["cpu", "cpu"])
