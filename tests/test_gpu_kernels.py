@@ -624,9 +624,14 @@ def test_transformer_layer_bf16_kernels_vs_torch(k):
              (ff.fc_in.linear1_weight, ref.linear1.weight), (ff.fc_in.linear1_bias, ref.linear1.bias),
              (ff.fc_out.linear2_weight, ref.linear2.weight), (ff.fc_out.linear2_bias, ref.linear2.bias),
              (ff.fc_out.norm_weight, ref.norm2.weight), (ff.fc_out.norm_bias, ref.norm2.bias)]
+    def rel_fro(a, b):
+        # norm-wise: a ReLU whose bf16 pre-activation lands on the other side of 0
+        # moves single elements of the weight gradient by a whole token's share
+        return (a.float() - b.float()).norm().item() / (b.float().norm().item() + 1e-6)
+
     for ours_p, ref_p in pairs:
         got = ours_p.main_grad if getattr(ours_p, "main_grad", None) is not None else ours_p.grad
-        assert got is not None and rel(got, ref_p.grad) < 3e-2, (tuple(ref_p.shape), rel(got, ref_p.grad))
+        assert got is not None and rel_fro(got, ref_p.grad) < 2e-2, (tuple(ref_p.shape), rel_fro(got, ref_p.grad))
 
 
 def test_vocab_split_decoder_gpu(k):
