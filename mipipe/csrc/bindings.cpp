@@ -390,31 +390,49 @@ void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, doub
 }
 
 // ------------------------------------------------------------------ GEMM
-void check_bf16_2d(const Tensor& t, const char* name) {
+// GEMM operands: bf16 (v_mfma_f32_16x16x32_bf16 kernel) or fp32 (v_mfma_f32_32x32x2_f32 kernel).
+void check_gemm_2d(const Tensor& t, const char* name) {
   check_cuda(t, name);
-  MP_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  MP_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name, " must be bf16 or fp32");
   MP_CHECK(t.dim() == 2, name, " must be 2-D");
 }
 
+void check_same_dtype(const Tensor& a, const Tensor& b, const char* what) {
+  MP_CHECK(a.scalar_type() == b.scalar_type(), what, ": operand dtypes differ");
+}
+
+bool gemm_ok(at::ScalarType t, int64_t M, int64_t N, int64_t K) {
+  return t == at::kFloat ? gemm_f32_supported(M, N, K) : gemm_supported(M, N, K);
+}
+
+void gemm_run(at::ScalarType t, const GemmArgs& g, hipStream_t s) {
+  if (t == at::kFloat) gemm_f32(g, s);
+  else gemm_bf16(g, s);
+}
+
 bool py_gemm_supported(int64_t M, int64_t N, int64_t K) { return gemm_supported(M, N, K); }
+bool py_gemm_f32_supported(int64_t M, int64_t N, int64_t K) { return gemm_f32_supported(M, N, K); }
 
 // y[M,N] = act(x[M,K] . w[N,K]^T + bias) with dropout; optional pre-activation.
 std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor x, Tensor w,
                                                                            std::optional<Tensor> bias, int64_t act,
                                                                            double p, bool save_preact,
                                                                            std::optional<Tensor> res) {
-  check_bf16_2d(x, "x");
-  check_bf16_2d(w, "w");
+  check_gemm_2d(x, "x");
+  check_gemm_2d(w, "w");
+  check_same_dtype(x, w, "linear_fwd");
+  const auto dt = x.scalar_type();
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   MP_CHECK(w.size(1) == K, "linear_fwd: inner dims differ");
-  MP_CHECK(gemm_supported(M, N, K), "linear_fwd: unsupported shape ", M, "x", N, "x", K);
+  MP_CHECK(gemm_ok(dt, M, N, K), "linear_fwd: unsupported shape ", M, "x", N, "x", K);
   MP_CHECK(act >= 0 && act <= 2 && p >= 0.0 && p < 1.0, "linear_fwd: bad act/p");
   if (bias) {
     check_cuda(*bias, "bias");
-    MP_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N, "linear_fwd: bad bias");
+    MP_CHECK(bias->scalar_type() == dt && bias->numel() == N, "linear_fwd: bad bias");
   }
   if (res) {
-    check_bf16_2d(*res, "res");
+    check_gemm_2d(*res, "res");
+    check_same_dtype(x, *res, "linear_fwd res");
     MP_CHECK(res->size(0) == M && res->size(1) == N && res->is_contiguous(), "linear_fwd: res must be contiguous [M, N]");
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -428,9 +446,9 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   g.bias = bias ? bias->data_ptr() : nullptr; g.aux = pre ? pre->data_ptr() : nullptr;
   if (res) g.res = res->data_ptr();  // y = res + dropout(act(x . w^T + b)): the residual add in the epilogue
   g.lda = K; g.ldb = K; g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
-  g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreBf16; g.act = (int)act; g.p = (float)p;
+  g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreAct; g.act = (int)act; g.p = (float)p;
   g.seed = seed; g.offset = offset;
-  gemm_bf16(g, cur_stream(x));
+  gemm_run(dt, g, cur_stream(x));
   return {y, pre, (int64_t)seed, (int64_t)offset};
 }
 
@@ -438,13 +456,16 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
 // dx = dy . w (+ res): `res` is the gradient the input receives from its
 // other consumer (a residual branch), added in the epilogue.
 Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
-  check_bf16_2d(dy, "dy");
-  check_bf16_2d(w, "w");
+  check_gemm_2d(dy, "dy");
+  check_gemm_2d(w, "w");
+  check_same_dtype(dy, w, "linear_dgrad");
+  const auto dt = dy.scalar_type();
   const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
   MP_CHECK(w.size(0) == N, "linear_dgrad: inner dims differ");
-  MP_CHECK(gemm_supported(M, K, N), "linear_dgrad: unsupported shape");
+  MP_CHECK(gemm_ok(dt, M, K, N), "linear_dgrad: unsupported shape");
   if (res) {
-    check_bf16_2d(*res, "res");
+    check_gemm_2d(*res, "res");
+    check_same_dtype(dy, *res, "linear_dgrad res");
     MP_CHECK(res->size(0) == M && res->size(1) == K && res->is_contiguous(), "linear_dgrad: res must be contiguous [M, K]");
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
@@ -453,26 +474,28 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
   g.A = dy.data_ptr(); g.B = w.data_ptr(); g.C = dx.data_ptr();
   if (res) g.res = res->data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)M; g.N = (int)K; g.K = (int)N;
-  g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreBf16;
-  gemm_bf16(g, cur_stream(dy));
+  g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreAct;
+  gemm_run(dt, g, cur_stream(dy));
   return dx;
 }
 
 // main_grad[N,K] (fp32) += dy[T,N]^T . x[T,K]   (= when !accumulate)
 void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad, bool accumulate) {
-  check_bf16_2d(dy, "dy");
-  check_bf16_2d(x, "x");
+  check_gemm_2d(dy, "dy");
+  check_gemm_2d(x, "x");
+  check_same_dtype(dy, x, "linear_wgrad");
+  const auto dt = dy.scalar_type();
   check_cuda(main_grad, "main_grad");
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
   MP_CHECK(x.size(0) == T, "linear_wgrad: token dims differ");
   MP_CHECK(main_grad.scalar_type() == at::kFloat && main_grad.numel() == N * K, "linear_wgrad: bad main_grad");
-  MP_CHECK(gemm_supported(N, K, T), "linear_wgrad: unsupported shape");
+  MP_CHECK(gemm_ok(dt, N, K, T), "linear_wgrad: unsupported shape");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = x.data_ptr(); g.C = main_grad.data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)T;
   g.a_kc = false; g.b_kc = false; g.epi = accumulate ? kEpiAccumF32 : kEpiStoreF32;
-  gemm_bf16(g, cur_stream(dy));
+  gemm_run(dt, g, cur_stream(dy));
 }
 
 // Deferred bias gradient over the micro-batches of a step: out (+)= column sums
@@ -541,13 +564,15 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
   check_cuda(main_grad, "main_grad");
   const int64_t T = dys[0].size(0), N = dys[0].size(1), K = xs[0].size(1);
   MP_CHECK(main_grad.scalar_type() == at::kFloat && main_grad.numel() == N * K, "linear_wgrad_segments: bad main_grad");
+  const auto dt = dys[0].scalar_type();
   for (size_t i = 0; i < dys.size(); ++i) {
-    check_bf16_2d(dys[i], "dy");
-    check_bf16_2d(xs[i], "x");
+    check_gemm_2d(dys[i], "dy");
+    check_gemm_2d(xs[i], "x");
+    MP_CHECK(dys[i].scalar_type() == dt && xs[i].scalar_type() == dt, "linear_wgrad_segments: mixed dtypes");
     MP_CHECK(dys[i].size(0) == T && dys[i].size(1) == N && xs[i].size(0) == T && xs[i].size(1) == K,
              "linear_wgrad_segments: every micro-batch needs the same [T, N] / [T, K] shapes");
   }
-  MP_CHECK(T % 64 == 0 && gemm_supported(N, K, T), "linear_wgrad_segments: unsupported shape");
+  MP_CHECK(T % 64 == 0 && gemm_ok(dt, N, K, T), "linear_wgrad_segments: unsupported shape");
   at::hip::HIPGuardMasqueradingAsCUDA guard(main_grad.device());
   const int total = (int)dys.size();
   for (int first = 0; first < total; first += GemmArgs::kMaxSegs) {
@@ -562,38 +587,47 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
       g.b_seg[i] = xs[first + i].data_ptr();
     }
     g.A = g.a_seg[0]; g.B = g.b_seg[0];
-    gemm_bf16(g, cur_stream(main_grad));
+    gemm_run(dt, g, cur_stream(main_grad));
   }
 }
 
 // Generic test entry: C[M,N] (fp32) = A . B with A given [M,K] (a_kc) or [K,M],
 // B given [N,K] (b_kc) or [K,N].
 Tensor py_gemm_f32(Tensor a, Tensor b, bool a_kc, bool b_kc) {
-  check_bf16_2d(a, "a");
-  check_bf16_2d(b, "b");
+  check_gemm_2d(a, "a");
+  check_gemm_2d(b, "b");
+  check_same_dtype(a, b, "gemm");
+  const auto dt = a.scalar_type();
   const int64_t M = a_kc ? a.size(0) : a.size(1);
   const int64_t K = a_kc ? a.size(1) : a.size(0);
   const int64_t N = b_kc ? b.size(0) : b.size(1);
   MP_CHECK((b_kc ? b.size(1) : b.size(0)) == K, "gemm: inner dims differ");
-  MP_CHECK(gemm_supported(M, N, K), "gemm: unsupported shape");
+  MP_CHECK(gemm_ok(dt, M, N, K), "gemm: unsupported shape");
   at::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   auto c = at::empty({M, N}, a.options().dtype(at::kFloat));
   GemmArgs g;
   g.A = a.data_ptr(); g.B = b.data_ptr(); g.C = c.data_ptr();
   g.lda = a.size(1); g.ldb = b.size(1); g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.a_kc = a_kc; g.b_kc = b_kc; g.epi = kEpiStoreF32;
-  gemm_bf16(g, cur_stream(a));
+  gemm_run(dt, g, cur_stream(a));
   return c;
 }
 
 // ------------------------------------------------------------------ attention
 // q, k, v: [B, S, H, D] views (unit stride on D, identical strides), bf16.
+// q, k, v: bf16 (attention.hip) or fp32 (attention_f32.hip).
 void check_bshd(const Tensor& t, const char* name) {
-  MP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
+  MP_CHECK(t.is_cuda() && (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat), name,
+           " must be a bf16 or fp32 GPU tensor");
   MP_CHECK(t.dim() == 4 && t.stride(3) == 1, name, " must be [B, S, H, D] with unit stride on D");
-  MP_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+  const int64_t v = 16 / t.element_size();  // elements per 16 bytes
+  MP_CHECK(t.stride(0) % v == 0 && t.stride(1) % v == 0 && t.stride(2) % v == 0 &&
                reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
            name, ": strides must keep 16-byte alignment");
+}
+
+bool attn_ok(at::ScalarType t, int S, int D) {
+  return t == at::kFloat ? attention_f32_supported(S, D) : attention_supported(S, D);
 }
 
 void fill_qkv(AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
@@ -602,11 +636,12 @@ void fill_qkv(AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
   check_bshd(v, "v");
   MP_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes(), "attention: q, k, v shapes differ");
   MP_CHECK(q.strides() == k.strides() && q.strides() == v.strides(), "attention: q, k, v strides differ");
+  MP_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attention: q, k, v dtypes differ");
   a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr();
   a.B = (int)q.size(0); a.S = (int)q.size(1); a.H = (int)q.size(2); a.D = (int)q.size(3);
   a.sb_qkv = q.stride(0); a.ld_qkv = q.stride(1); a.sh_qkv = q.stride(2);
-  MP_CHECK(attention_supported(a.S, a.D), "attention: unsupported S=", a.S, " D=", a.D,
-           " (S % 64 == 0, D in {64,128,256})");
+  MP_CHECK(attn_ok(q.scalar_type(), a.S, a.D), "attention: unsupported S=", a.S, " D=", a.D, " for ",
+           q.scalar_type(), " (bf16: S % 64 == 0, D in {64,128,256}; fp32: S % 32 == 0, D == 64)");
 }
 
 std::tuple<Tensor, Tensor, int64_t, int64_t> py_attention_fwd(Tensor q, Tensor k, Tensor v, bool causal, double p,
@@ -622,7 +657,8 @@ std::tuple<Tensor, Tensor, int64_t, int64_t> py_attention_fwd(Tensor q, Tensor k
   a.o = o.data_ptr(); a.sb_o = o.stride(0); a.ld_o = o.stride(1); a.sh_o = o.stride(2);
   a.lse = ptr<float>(lse);
   a.scale = (float)scale; a.p = (float)p; a.seed = seed; a.offset = offset; a.causal = causal;
-  attention_fwd(a, cur_stream(q));
+  if (q.scalar_type() == at::kFloat) attention_f32_fwd(a, cur_stream(q));
+  else attention_fwd(a, cur_stream(q));
   return {o, lse, (int64_t)seed, (int64_t)offset};
 }
 
@@ -633,6 +669,8 @@ void py_attention_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tenso
   check_bshd(o, "o");
   check_bshd(dout, "dout");
   MP_CHECK(o.strides() == dout.strides() && o.sizes() == dout.sizes(), "attention_bwd: o/dout layout differs");
+  MP_CHECK(o.scalar_type() == q.scalar_type() && dout.scalar_type() == q.scalar_type() &&
+               dq.scalar_type() == q.scalar_type(), "attention_bwd: dtypes differ");
   MP_CHECK(dq.strides() == q.strides() && dk.strides() == q.strides() && dv.strides() == q.strides(),
            "attention_bwd: gradient buffers must share q's layout");
   MP_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)a.B * a.H * a.S, "attention_bwd: bad lse");
@@ -643,7 +681,8 @@ void py_attention_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tenso
   a.dq = dq.data_ptr(); a.dk = dk.data_ptr(); a.dv = dv.data_ptr();
   a.lse = ptr<float>(lse); a.delta = ptr<float>(delta);
   a.scale = (float)scale; a.p = (float)p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset; a.causal = causal;
-  attention_bwd(a, cur_stream(q));
+  if (q.scalar_type() == at::kFloat) attention_f32_bwd(a, cur_stream(q));
+  else attention_bwd(a, cur_stream(q));
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -728,9 +767,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &py_embed_fwd);
   m.def("embedding_bwd", &py_embed_bwd);
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });
+  m.def("attention_f32_supported", [](int64_t S, int64_t D) { return attention_f32_supported((int)S, (int)D); });
   m.def("attention_fwd", &py_attention_fwd);
   m.def("attention_bwd", &py_attention_bwd);
   m.def("gemm_supported", &py_gemm_supported);
+  m.def("gemm_f32_supported", &py_gemm_f32_supported);
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);
   m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 auto (default)");
   m.def("gemm_get_schedule", &gemm_get_schedule);

@@ -60,9 +60,11 @@ __device__ __forceinline__ int ic_rk(int r) { return (r & 3) | (((r >> 3) & 1) <
 __device__ __forceinline__ int ic_off(int r, int c8) { return r * 256 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
 
 // ---- global -> registers -> LDS staging ------------------------------------------
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
 template <bool KC>
 struct Stager {
-  uint4 v[4];
+  u32x4 v[4];  // native vector: HIP's uint4 struct copies become memcpys that pin the array in scratch
   // Loads the tile whose first element is (i0, k0) of an operand of leading
   // dimension ld.
   __device__ __forceinline__ void load(const bf16_t* __restrict__ base, int64_t ld, int i0, int k0, int tid) {
@@ -77,7 +79,7 @@ struct Stager {
         const int r = id >> 4, c = id & 15;
         p = base + (int64_t)(k0 + r) * ld + i0 + c * 8;
       }
-      v[u] = *reinterpret_cast<const uint4*>(p);
+      v[u] = *reinterpret_cast<const u32x4*>(p);
     }
   }
   __device__ __forceinline__ void store(char* tile, int tid) const {
@@ -90,7 +92,7 @@ struct Stager {
       } else {
         off = ic_off(id >> 4, (id & 15) * 2);
       }
-      *reinterpret_cast<uint4*>(tile + off) = v[u];
+      *reinterpret_cast<u32x4*>(tile + off) = v[u];
     }
   }
 };

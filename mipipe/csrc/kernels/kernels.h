@@ -86,7 +86,9 @@ void column_sum(const T* x, int64_t rows, int cols, float* part, int nparts, voi
                 hipStream_t s);
 
 // ------------------------------------------------------------------ GEMM
-enum GemmEpilogue : int { kEpiStoreBf16 = 0, kEpiAccumF32 = 1, kEpiStoreF32 = 2 };
+// kEpiStoreBf16 / kEpiStoreAct: the activation epilogue (bias, act, dropout,
+// residual, aux) stored in the operand dtype (bf16 for gemm_bf16, fp32 for gemm_f32).
+enum GemmEpilogue : int { kEpiStoreBf16 = 0, kEpiAccumF32 = 1, kEpiStoreF32 = 2, kEpiStoreAct = 0 };
 
 struct GemmArgs {
   const void* A = nullptr;  // bf16
@@ -119,6 +121,9 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K);
 void gemm_set_schedule(int mode);
 int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
+// Same interface with fp32 operands (and fp32 bias / res / aux / C): v_mfma_f32_32x32x2_f32.
+bool gemm_f32_supported(int64_t M, int64_t N, int64_t K);
+void gemm_f32(const GemmArgs& g, hipStream_t s);
 
 // ------------------------------------------------------------------ attention
 struct AttnArgs {
@@ -146,6 +151,10 @@ bool attention_supported(int S, int D);
 void attention_set_fused_bwd(int on);
 void attention_fwd(const AttnArgs& a, hipStream_t s);
 void attention_bwd(const AttnArgs& a, hipStream_t s);
+// fp32 q/k/v/o (v_mfma_f32_32x32x2_f32): S % 32 == 0, D == 64; "key-quad" dropout layout.
+bool attention_f32_supported(int S, int D);
+void attention_f32_fwd(const AttnArgs& a, hipStream_t s);
+void attention_f32_bwd(const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ loss
 template <typename T>

@@ -11,8 +11,10 @@ Two entry points:
 
 Causal masking and attention dropout are supported; the dropout mask is
 regenerated from Philox (seed, offset) in backward, so checkpoint recompute
-replays it exactly.  Supported on the GPU path: ``S % 64 == 0`` and
-``D in {64, 128, 256}``; the CPU path is eager math.
+replays it exactly.  Supported on the GPU path: bf16 with ``S % 64 == 0`` and
+``D in {64, 128, 256}`` (attention.hip), fp32 with ``S % 32 == 0`` and
+``D == 64`` (attention_f32.hip, the reference's own precision); the
+CPU path is eager math.
 """
 from __future__ import annotations
 
@@ -94,19 +96,22 @@ _noted = set()
 
 
 def _note_math_path(S: int, D: int, dtype) -> None:
-    """fp32 models and shapes outside the kernel's tiling (S % 64, D in
-    {64,128,256}) use the eager math path; say so once per shape."""
+    """Shapes outside the kernels' tiling use the eager math path; say so once per shape."""
     key = (S, D, dtype)
     if key not in _noted:
         _noted.add(key)
         import warnings
 
-        warnings.warn(f"mipipe attention: S={S} D={D} {dtype} runs the eager math path (HIP kernel: bf16, "
-                      "S % 64 == 0, D in {64, 128, 256})", stacklevel=3)
+        warnings.warn(f"mipipe attention: S={S} D={D} {dtype} runs the eager math path (HIP kernels: bf16 with "
+                      "S % 64 == 0, D in {64, 128, 256}; fp32 with S % 32 == 0, D == 64)", stacklevel=3)
 
 
 def _gpu_ok(t: Tensor, S: int, D: int) -> bool:
-    return t.dtype == torch.bfloat16 and kernels_for(t).attention_supported(S, D)
+    if t.dtype == torch.bfloat16:
+        return kernels_for(t).attention_supported(S, D)
+    if t.dtype == torch.float32:
+        return kernels_for(t).attention_f32_supported(S, D)
+    return False
 
 
 def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, training: bool = True,

@@ -10,9 +10,11 @@ Backward: the activation/dropout backward is one elementwise pass
           fp32 straight into ``weight.main_grad`` when the flat optimizer owns
           the parameter, so micro-batch accumulation never rounds to bf16.
 
-Shapes the tile kernel does not cover (dims not multiples of 128/64) and
-non-bf16 GPU tensors run the plain GEMM through hipBLASLt (torch.matmul) with
-the same fused elementwise kernels.
+bf16 runs the v_mfma_f32_16x16x32_bf16 kernel (gemm.hip), fp32 -- the
+reference's own precision -- the v_mfma_f32_32x32x2_f32 kernel (gemm_f32.hip)
+with the same epilogues and main_grad path.  Only shapes neither kernel covers
+(e.g. a width that is not a multiple of 8 / 4) run the plain GEMM through
+torch.matmul with the same fused elementwise kernels.
 """
 from __future__ import annotations
 
@@ -64,15 +66,23 @@ def _add_or_copy(main: Tensor, g: Tensor, p: Tensor) -> None:
         main.copy_(g)
 
 
+def _gemm_supported(k, dtype: torch.dtype, m: int, n: int, kk: int) -> bool:
+    if dtype == torch.bfloat16:
+        return k.gemm_supported(m, n, kk)
+    if dtype == torch.float32:
+        return k.gemm_f32_supported(m, n, kk)
+    return False
+
+
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
     """All three GEMMs of the layer (fwd [T,N,K], dgrad [T,K,N], wgrad [N,K,T]) fit the tile kernel."""
     t, (n, kk) = x2.shape[0], weight.shape
+    dt = x2.dtype
     return (
-        x2.dtype == torch.bfloat16
-        and weight.dtype == torch.bfloat16
-        and k.gemm_supported(t, n, kk)
-        and k.gemm_supported(t, kk, n)
-        and k.gemm_supported(n, kk, t)
+        weight.dtype == dt
+        and _gemm_supported(k, dt, t, n, kk)
+        and _gemm_supported(k, dt, t, kk, n)
+        and _gemm_supported(k, dt, n, kk, t)
     )
 
 
@@ -92,8 +102,8 @@ class _Linear(torch.autograd.Function):
             r2 = None
             if res is not None:
                 r2 = res.reshape(-1, w.shape[0])
-                if r2.dtype != torch.bfloat16 or not r2.is_contiguous():
-                    r2 = r2.to(torch.bfloat16).contiguous()
+                if r2.dtype != x2.dtype or not r2.is_contiguous():
+                    r2 = r2.to(x2.dtype).contiguous()
             y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2, r2)
             res = None  # added in the epilogue
         else:
@@ -152,7 +162,7 @@ class _Linear(torch.autograd.Function):
             r2 = None
             if dres is not None:
                 r2 = dres.reshape(-1, dres.shape[-1])
-                if not (ctx.fused_tile and r2.dtype == torch.bfloat16 and r2.is_contiguous()):
+                if not (ctx.fused_tile and r2.dtype == dpre.dtype and r2.is_contiguous()):
                     r2 = None
             if ctx.fused_tile:
                 dx = k.linear_dgrad(dpre, w, r2)
@@ -207,8 +217,7 @@ def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
     it exists, else returned for autograd."""
     main = getattr(w, "main_grad", None)
     k = kernels_for(dy) if dy.is_cuda else None
-    tile = (k is not None and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
-            and k.gemm_supported(w.shape[0], w.shape[1], dy.shape[0]))
+    tile = (k is not None and dy.dtype == x.dtype and _gemm_supported(k, dy.dtype, w.shape[0], w.shape[1], dy.shape[0]))
     if main is not None and tile:
         if _DEFERRED is not None:
             _defer(w, dy.contiguous(), x.contiguous())

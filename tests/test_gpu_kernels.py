@@ -281,8 +281,10 @@ def test_peer_copy_two_gpus(k):
 
 
 # ------------------------------------------------------------------ model / engine
-def test_transformer_layer_matches_torch(k):
-    """Post-norm TransformerEncoderLayer on mipipe ops vs nn.TransformerEncoderLayer (fp32, no dropout)."""
+def test_transformer_layer_eager_fallback_shape(k):
+    """A shape outside both attention kernels' tiling (S = 40) falls back to eager
+    attention math (with a warning) and still matches nn.TransformerEncoderLayer
+    (fp32, no dropout).  The fp32 kernel path is tests/test_gpu_fp32.py."""
     from torch import nn
 
     from mipipe.models import TransformerEncoderLayer
