@@ -10,9 +10,12 @@
 // the kernel is compute-bound for any tile >= 64x64, so the design goal is
 // only to keep one MFMA chain per accumulator issuing back to back:
 //
-// * 256 threads = 4 waves (2 x 2), each wave TM x TN tiles of 32x32 (block
-//   tile 64..128 x 64..128), BK = 32, two LDS buffers, register-staged
-//   global loads one K-tile ahead (fp32 rows are 16-byte float4 loads).
+// * 8 waves per block, each TM x TN tiles of 32x32: 128x128 blocks (waves of
+//   32x64) for grids that fill the chip, 64x128 / 128x64 blocks (waves of
+//   32x32) for the T = 1024 shapes of the reference config; BK = 32, two LDS
+//   buffers, and two sets of staging registers, so a K-tile's global loads
+//   (16-byte float4s) are issued two K-tiles before they are needed;
+//   fragments are read one k-quad ahead of the MFMAs.
 // * The MFMA sums over k, so k may be permuted inside a K-tile as long as A
 //   and B agree: in k-step s lane half h (= lane >> 5) uses physical k =
 //   16h + 4(s >> 2) + (s & 3).  Then a K-contiguous operand hands each lane 4
@@ -21,8 +24,8 @@
 //   I-contiguous operand is one ds_read_b32 per step whose two lane halves
 //   (rows k and k + 16) are 128 bytes apart after an XOR of the chunk index
 //   (all 64 banks distinct).
-// * Two blocks per CU (2 x 64 KiB LDS): while one block waits at its barrier
-//   the other's MFMAs run.
+// * Two or three blocks per CU (LDS 48-64 KiB each): while one block waits
+//   at its barrier the others' MFMAs run.
 // * Epilogues as gemm.hip: bias + ReLU/GELU + dropout (same Philox
 //   column-quad mask layout as the elementwise backward) + residual addend +
 //   pre-activation aux output, all fp32; fp32 += (weight gradients into
@@ -32,12 +35,13 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdlib.h>
+
 namespace mipipe {
 
 namespace {
 
 constexpr int BK = 32;
-constexpr int kThreads = 256;
 
 // K-contiguous image [rows][32 floats]: 128-byte rows, 16-byte chunk c of row
 // r stored at chunk c ^ ((r >> 1) & 7).
@@ -79,15 +83,17 @@ __device__ __forceinline__ const float* seg_base(const GemmArgs& g, bool is_a, i
   return reinterpret_cast<const float*>(is_a ? g.a_seg[s] : g.b_seg[s]);
 }
 
-// Register staging of one operand tile (ROWS x 32 of the operand's M or N rows).
-template <int ROWS, bool KC>
+// Register staging of one operand tile (ROWS x 32 of the operand's M or N rows)
+// by NT threads.
+template <int ROWS, bool KC, int NT>
 struct Stage {
-  static constexpr int kN = ROWS * BK / 4 / kThreads;  // float4s per thread
+  static constexpr int kN = ROWS * BK / 4 / NT;  // float4s per thread
+  static_assert(kN >= 1 && ROWS * BK / 4 % NT == 0, "tile / thread count mismatch");
   f32x4 v[kN];  // native vector type: HIP's float4 struct copies become memcpys that pin the array in scratch
   __device__ __forceinline__ void load(const float* base, int64_t ld, int i0, int lim, int k0, int tid) {
 #pragma unroll
     for (int u = 0; u < kN; ++u) {
-      const int id = tid + u * kThreads;
+      const int id = tid + u * NT;
       const float* p;
       if (KC) {
         const int r = id >> 3, c = id & 7;
@@ -105,7 +111,7 @@ struct Stage {
   __device__ __forceinline__ void store(char* tile, int tid) const {
 #pragma unroll
     for (int u = 0; u < kN; ++u) {
-      const int id = tid + u * kThreads;
+      const int id = tid + u * NT;
       int off;
       if (KC) {
         off = kc_off(id >> 3, id & 7);
@@ -120,30 +126,37 @@ struct Stage {
 
 // The 4 k-steps 4q..4q+3 of rows [ib, ib+32): element e = k-step 4q + e.
 template <int ROWS, bool KC>
-__device__ __forceinline__ float4 frag4(const char* tile, int ib, int q, int lane) {
+__device__ __forceinline__ f32x4 frag4(const char* tile, int ib, int q, int lane) {
   const int i = ib + (lane & 31), h = lane >> 5;
-  if (KC) return *reinterpret_cast<const float4*>(tile + kc_off(i, 4 * h + q));
-  float4 r;
+  if (KC) return *reinterpret_cast<const f32x4*>(tile + kc_off(i, 4 * h + q));
+  f32x4 r;
   const int k0 = 16 * h + 4 * q;
   const int c = i >> 2, w = (i & 3) * 4;
-  r.x = *reinterpret_cast<const float*>(tile + ic_off<ROWS>(k0 + 0, c) + w);
-  r.y = *reinterpret_cast<const float*>(tile + ic_off<ROWS>(k0 + 1, c) + w);
-  r.z = *reinterpret_cast<const float*>(tile + ic_off<ROWS>(k0 + 2, c) + w);
-  r.w = *reinterpret_cast<const float*>(tile + ic_off<ROWS>(k0 + 3, c) + w);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = *reinterpret_cast<const float*>(tile + ic_off<ROWS>(k0 + e, c) + w);
   return r;
 }
 
-__device__ __forceinline__ float f4(const float4& v, int e) { return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w)); }
+// WM x WN waves, each TM x TN tiles of 32x32: block tile (32 WM TM) x (32 WN TN).
+template <int WM, int WN, int TM, int TN>
+struct Cfg {
+  static constexpr int kWaves = WM * WN, kThreads = 64 * WM * WN;
+  static constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
+  static constexpr int kLds = 2 * (BM + BN) * BK * 4;
+  // blocks per CU the LDS admits (160 KiB), capped by 8 waves per SIMD
+  static constexpr int kBlocksPerCu = (160 * 1024 / kLds) < (32 / kWaves) ? (160 * 1024 / kLds) : (32 / kWaves);
+};
 
-template <int TM, int TN, bool A_KC, bool B_KC, int EPI, int ACT>
-__global__ void __launch_bounds__(kThreads, 2) gemm_f32_kernel(GemmArgs g) {
-  constexpr int BM = 2 * 32 * TM, BN = 2 * 32 * TN;
+template <int WM, int WN, int TM, int TN, bool A_KC, bool B_KC, int EPI, int ACT>
+__global__ void __launch_bounds__(64 * WM * WN, (Cfg<WM, WN, TM, TN>::kBlocksPerCu)) gemm_f32_kernel(GemmArgs g) {
+  using C_ = Cfg<WM, WN, TM, TN>;
+  constexpr int NT = C_::kThreads, BM = C_::BM, BN = C_::BN;
   constexpr int kA = BM * BK * 4, kB = BN * BK * 4, kBuf = kA + kB;
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
 
   int tm, tn;
   tile_coords((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, tm, tn);
@@ -157,51 +170,64 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
 
-  Stage<BM, A_KC> sa;
-  Stage<BN, B_KC> sb;
+  // Two register staging sets: the global loads of tile kt+2 are issued
+  // while tile kt computes and tile kt+1 waits in registers, so a load has
+  // two K-tiles of MFMA time (>= 4000 cycles) to return from L2 / MALL.
+  Stage<BM, A_KC, NT> sa0, sa1;
+  Stage<BN, B_KC, NT> sb0, sb1;
   const int nk = g.K / BK;
-  {
+  auto gload = [&](int kt, Stage<BM, A_KC, NT>& sa, Stage<BN, B_KC, NT>& sb) {
+    const int kn = min(kt, nk - 1) * BK;  // clamped: past the end reloads the last tile (unused)
     int kl;
-    const float* A = seg_base(g, true, 0, kl);
+    const float* A = seg_base(g, true, kn, kl);
     sa.load(A, g.lda, m0, g.M, kl, tid);
-    const float* B = seg_base(g, false, 0, kl);
+    const float* B = seg_base(g, false, kn, kl);
     sb.load(B, g.ldb, n0, g.N, kl, tid);
-  }
-  sa.store(smem, tid);
-  sb.store(smem + kA, tid);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * kBuf;
-    // Next tile's loads, unconditionally (the last iteration reloads its own
-    // tile into the idle buffer): staging registers written under a branch
-    // are demoted to scratch by the compiler.
-    {
-      const int kn = min(kt + 1, nk - 1) * BK;
-      int kl;
-      const float* A = seg_base(g, true, kn, kl);
-      sa.load(A, g.lda, m0, g.M, kl, tid);
-      const float* B = seg_base(g, false, kn, kl);
-      sb.load(B, g.ldb, n0, g.N, kl, tid);
-    }
+  };
+  auto compute = [&](const char* cur) {
+    // Fragments one k-quad ahead: the reads of quad q+1 are in flight while
+    // the MFMAs of quad q issue.
+    f32x4 af[2][TM], bf[2][TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) af[0][t] = frag4<BM, A_KC>(cur, (wm * TM + t) * 32, 0, lane);
+#pragma unroll
+    for (int u = 0; u < TN; ++u) bf[0][u] = frag4<BN, B_KC>(cur + kA, (wn * TN + u) * 32, 0, lane);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float4 af[TM], bf[TN];
+      const int cq = q & 1;
+      if (q < 3) {
 #pragma unroll
-      for (int t = 0; t < TM; ++t) af[t] = frag4<BM, A_KC>(cur, wm * 32 * TM + 32 * t, q, lane);
+        for (int t = 0; t < TM; ++t) af[cq ^ 1][t] = frag4<BM, A_KC>(cur, (wm * TM + t) * 32, q + 1, lane);
 #pragma unroll
-      for (int u = 0; u < TN; ++u) bf[u] = frag4<BN, B_KC>(cur + kA, wn * 32 * TN + 32 * u, q, lane);
+        for (int u = 0; u < TN; ++u) bf[cq ^ 1][u] = frag4<BN, B_KC>(cur + kA, (wn * TN + u) * 32, q + 1, lane);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int t = 0; t < TM; ++t)
 #pragma unroll
           for (int u = 0; u < TN; ++u)
-            acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4(af[t], e), f4(bf[u], e), acc[t][u], 0, 0, 0);
+            acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cq][t][e], bf[cq][u][e], acc[t][u], 0, 0, 0);
     }
-    char* nxt = smem + ((kt + 1) & 1) * kBuf;
-    sa.store(nxt, tid);
-    sb.store(nxt + kA, tid);
+  };
+  gload(0, sa0, sb0);
+  gload(1, sa1, sb1);
+  sa0.store(smem, tid);
+  sb0.store(smem + kA, tid);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // even tile kt in buffer 0, tile kt+1 in registers set 1
+    gload(kt + 2, sa0, sb0);
+    compute(smem);
+    sa1.store(smem + kBuf, tid);
+    sb1.store(smem + kBuf + kA, tid);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    // odd tile kt+1 in buffer 1, tile kt+2 in registers set 0
+    gload(kt + 3, sa1, sb1);
+    compute(smem + kBuf);
+    sa0.store(smem, tid);
+    sb0.store(smem + kA, tid);
     __syncthreads();
   }
 
@@ -213,13 +239,13 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_f32_kernel(GemmArgs g) {
   for (int t = 0; t < TM; ++t) {
 #pragma unroll
     for (int u = 0; u < TN; ++u) {
-      const int col = n0 + wn * 32 * TN + 32 * u + cl;
+      const int col = n0 + (wn * TN + u) * 32 + cl;
       const bool col_ok = col < g.N;
       const float b = (EPI == kEpiStoreAct && g.bias != nullptr && col_ok)
                           ? reinterpret_cast<const float*>(g.bias)[col] : 0.f;
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const int row0 = m0 + wm * 32 * TM + 32 * t + 8 * gq + 4 * h;
+        const int row0 = m0 + (wm * TM + t) * 32 + 8 * gq + 4 * h;
         if (EPI == kEpiStoreAct) {
           uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
           if (g.p > 0.f) {
@@ -257,23 +283,64 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_f32_kernel(GemmArgs g) {
   }
 }
 
-template <int TM, int TN>
+template <int WM, int WN, int TM, int TN>
 int tiles(const GemmArgs& g) {
-  return ((g.M + 64 * TM - 1) / (64 * TM)) * ((g.N + 64 * TN - 1) / (64 * TN));
+  using C_ = Cfg<WM, WN, TM, TN>;
+  return ((g.M + C_::BM - 1) / C_::BM) * ((g.N + C_::BN - 1) / C_::BN);
 }
 
-template <int TM, int TN, bool A_KC, bool B_KC, int EPI, int ACT>
-void launch_tile(const GemmArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_f32_kernel<TM, TN, A_KC, B_KC, EPI, ACT>), dim3(tiles<TM, TN>(g)), dim3(kThreads), 0, s, g);
+// Share of the CU slots (256 CUs x resident blocks) the grid keeps busy over
+// its whole run: a grid of 384 tiles on 512 slots leaves a quarter idle.
+template <int WM, int WN, int TM, int TN>
+double fill(const GemmArgs& g) {
+  const int slots = 256 * Cfg<WM, WN, TM, TN>::kBlocksPerCu;
+  const int t = tiles<WM, WN, TM, TN>(g);
+  const int rounds = (t + slots - 1) / slots;
+  return (double)t / ((double)rounds * slots);
 }
 
-// Largest tile that still gives >= 256 workgroups (one per CU; two fit per
-// CU): 128x128, then 64x128, then 64x64.
+template <int WM, int WN, int TM, int TN, bool A_KC, bool B_KC, int EPI, int ACT>
+void launch_cfg(const GemmArgs& g, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, TN, A_KC, B_KC, EPI, ACT>), dim3(tiles<WM, WN, TM, TN>(g)),
+                     dim3(64 * WM * WN), 0, s, g);
+}
+
+// MIPIPE_GEMM_F32_CFG: 0 auto; 1: 128x128 (4 waves, 2x2 tiles each); 2: 64x128
+// (8 waves, 1 tile each); 3: 128x64 (8 waves); 4: 64x128 (4 waves, 1x2 tiles);
+// 5: 128x128 (8 waves, 1x2 tiles); 6: 128x128 (8 waves, 2x1); 7: 256x128 and
+// 8: 128x256 (8 waves, 2x2 tiles).
+int g_f32_cfg = -1;
+
+int f32_cfg() {
+  if (g_f32_cfg < 0) {
+    const char* e = getenv("MIPIPE_GEMM_F32_CFG");
+    g_f32_cfg = e ? atoi(e) : 0;
+  }
+  return g_f32_cfg;
+}
+
 template <bool A_KC, bool B_KC, int EPI, int ACT>
 void launch(const GemmArgs& g, hipStream_t s) {
-  if (tiles<2, 2>(g) >= 256) launch_tile<2, 2, A_KC, B_KC, EPI, ACT>(g, s);
-  else if (tiles<1, 2>(g) >= 256) launch_tile<1, 2, A_KC, B_KC, EPI, ACT>(g, s);
-  else launch_tile<1, 1, A_KC, B_KC, EPI, ACT>(g, s);
+  int c = f32_cfg();
+  if (c == 0) {
+    // the big tile when it fills the machine as well as the small ones (fewer
+    // operand bytes per FLOP), else the best-filling 64-row / 64-column tile
+    // (profiles/gemm_f32_vs_hipblaslt.txt: 128x128 with 8 waves of 32x64 is the
+    // best big tile; 64x128 / 128x64 with 8 waves of 32x32 the best small ones)
+    const double f5 = fill<4, 2, 1, 2>(g), f2 = fill<2, 4, 1, 1>(g), f3 = fill<4, 2, 1, 1>(g);
+    if (f5 >= 0.95 * f2 && f5 >= 0.95 * f3) c = 5;
+    else c = f2 >= f3 ? 2 : 3;
+  }
+  switch (c) {
+    case 2: launch_cfg<2, 4, 1, 1, A_KC, B_KC, EPI, ACT>(g, s); break;
+    case 3: launch_cfg<4, 2, 1, 1, A_KC, B_KC, EPI, ACT>(g, s); break;
+    case 4: launch_cfg<2, 2, 1, 2, A_KC, B_KC, EPI, ACT>(g, s); break;
+    case 5: launch_cfg<4, 2, 1, 2, A_KC, B_KC, EPI, ACT>(g, s); break;
+    case 6: launch_cfg<2, 4, 2, 1, A_KC, B_KC, EPI, ACT>(g, s); break;
+    case 7: launch_cfg<4, 2, 2, 2, A_KC, B_KC, EPI, ACT>(g, s); break;
+    case 8: launch_cfg<2, 4, 2, 2, A_KC, B_KC, EPI, ACT>(g, s); break;
+    default: launch_cfg<2, 2, 2, 2, A_KC, B_KC, EPI, ACT>(g, s); break;
+  }
 }
 
 template <bool A_KC, bool B_KC, int EPI>
