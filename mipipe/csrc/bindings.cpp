@@ -644,8 +644,21 @@ void fill_qkv(AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
            q.scalar_type(), " (bf16: S % 64 == 0, D in {64,128,256}; fp32: S % 32 == 0, D == 64)");
 }
 
-std::tuple<Tensor, Tensor, int64_t, int64_t> py_attention_fwd(Tensor q, Tensor k, Tensor v, bool causal, double p,
-                                                              double scale) {
+// bf16 D = 64, S >= 256 run the long-sequence kernels (attention_long.hip);
+// MIPIPE_ATTN_LONG=0 selects the previous kernels (A/B runs).
+bool use_long(const Tensor& q, int S, int D) {
+  static const int on = [] {
+    const char* e = getenv("MIPIPE_ATTN_LONG");
+    return e == nullptr ? 1 : atoi(e);
+  }();
+  return on && q.scalar_type() == at::kBFloat16 && attention_long_supported(S, D);
+}
+
+// Returns (o, lse, seed, offset, dropout keep bits): the bits tensor (int32
+// [B*H, S/32, S]) is non-empty only for the long-sequence kernels with p > 0
+// and must be handed back to attention_bwd.
+std::tuple<Tensor, Tensor, int64_t, int64_t, Tensor> py_attention_fwd(Tensor q, Tensor k, Tensor v, bool causal,
+                                                                      double p, double scale) {
   AttnArgs a;
   fill_qkv(a, q, k, v);
   MP_CHECK(p >= 0.0 && p < 1.0, "attention: bad dropout p");
@@ -657,13 +670,24 @@ std::tuple<Tensor, Tensor, int64_t, int64_t> py_attention_fwd(Tensor q, Tensor k
   a.o = o.data_ptr(); a.sb_o = o.stride(0); a.ld_o = o.stride(1); a.sh_o = o.stride(2);
   a.lse = ptr<float>(lse);
   a.scale = (float)scale; a.p = (float)p; a.seed = seed; a.offset = offset; a.causal = causal;
-  if (q.scalar_type() == at::kFloat) attention_f32_fwd(a, cur_stream(q));
-  else attention_fwd(a, cur_stream(q));
-  return {o, lse, (int64_t)seed, (int64_t)offset};
+  Tensor bits = at::empty({0}, q.options().dtype(at::kInt));
+  if (q.scalar_type() == at::kFloat) {
+    attention_f32_fwd(a, cur_stream(q));
+  } else if (use_long(q, a.S, a.D)) {
+    if (p > 0.0) {
+      bits = at::empty({(int64_t)a.B * a.H, a.S / 32, a.S}, q.options().dtype(at::kInt));
+      a.dmask = reinterpret_cast<uint32_t*>(bits.data_ptr());
+    }
+    attention_long_fwd(a, cur_stream(q));
+  } else {
+    attention_fwd(a, cur_stream(q));
+  }
+  return {o, lse, (int64_t)seed, (int64_t)offset, bits};
 }
 
 void py_attention_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, double p,
-                      double scale, int64_t seed, int64_t offset, Tensor dq, Tensor dk, Tensor dv) {
+                      double scale, int64_t seed, int64_t offset, Tensor dq, Tensor dk, Tensor dv,
+                      std::optional<Tensor> bits) {
   AttnArgs a;
   fill_qkv(a, q, k, v);
   check_bshd(o, "o");
@@ -681,8 +705,19 @@ void py_attention_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tenso
   a.dq = dq.data_ptr(); a.dk = dk.data_ptr(); a.dv = dv.data_ptr();
   a.lse = ptr<float>(lse); a.delta = ptr<float>(delta);
   a.scale = (float)scale; a.p = (float)p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset; a.causal = causal;
-  if (q.scalar_type() == at::kFloat) attention_f32_bwd(a, cur_stream(q));
-  else attention_bwd(a, cur_stream(q));
+  if (q.scalar_type() == at::kFloat) {
+    attention_f32_bwd(a, cur_stream(q));
+  } else if (use_long(q, a.S, a.D)) {
+    if (p > 0.0) {
+      MP_CHECK(bits && bits->is_cuda() && bits->scalar_type() == at::kInt &&
+                   bits->numel() == (int64_t)a.B * a.H * (a.S / 32) * a.S,
+               "attention_bwd: the long-sequence kernels need the forward's dropout bits");
+      a.dmask = reinterpret_cast<uint32_t*>(bits->data_ptr());
+    }
+    attention_long_bwd(a, cur_stream(q));
+  } else {
+    attention_bwd(a, cur_stream(q));
+  }
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -769,7 +804,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });
   m.def("attention_f32_supported", [](int64_t S, int64_t D) { return attention_f32_supported((int)S, (int)D); });
   m.def("attention_fwd", &py_attention_fwd);
-  m.def("attention_bwd", &py_attention_bwd);
+  m.def("attention_bwd", &py_attention_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("causal"), py::arg("p"), py::arg("scale"), py::arg("seed"), py::arg("offset"),
+        py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none());
+  m.def("attention_long_supported", [](int64_t S, int64_t D) { return attention_long_supported((int)S, (int)D); });
   m.def("gemm_supported", &py_gemm_supported);
   m.def("gemm_f32_supported", &py_gemm_f32_supported);
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);

@@ -1,0 +1,662 @@
+// Long-sequence flash attention for gfx950, head dim 64, bf16 (SURVEY §2.3
+// K2/K3 at GPT-2-XL's shape: B 8, H 25, S 1024, D 64, causal, dropout 0.1).
+//
+// Built on v_mfma_f32_32x32x16_bf16 and its accumulator layout: register r of
+// lane l holds (row (r&3) + 8(r>>2) + 4(l>>5), column l&31), and an
+// accumulator tile is directly the A or B operand of a following MFMA that
+// sums over its ROW index (k-step half h, element j <-> row 8t + j of the
+// tile's k-step t; the other operand reads its k index in that same order).
+// So no probability or gradient tile ever goes through LDS:
+//
+//   forward (a wave = 64 queries):  S^T = K Q^T   (keys in registers, query on the lane)
+//                                   O  += P V     (P^T registers are the A operand)
+//   dK, dV  (a wave = 64 keys):     S = Q K^T, dP = dO V^T   (key on the lane)
+//                                   dV^T += dO^T P_drop,  dK^T += Q^T dS
+//   dQ      (a wave = 64 queries):  S^T, dP^T = V dO^T, dQ += dS K
+//
+// Each wave owns two 32-row blocks of its own dimension, so every K/V (Q/dO)
+// fragment read from LDS feeds two MFMAs.  64-row operand tiles are staged in
+// LDS ([64][64] bf16, 128-byte rows) through registers one tile ahead, with
+// 16-byte chunk c of row r at c ^ f(r), f(r) = 4((r>>1)&1) | ((r>>2)&3): the
+// row reads (ds_read_b128, 16 lanes on 16 rows) and the transposing column
+// reads (ds_read_b64_tr_b16, 32 lanes on 4 rows x 4 chunks) are both free of
+// bank conflicts.
+//
+// Softmax: exp2 with the scale folded into one FMA; the running max is only
+// raised when a tile's max exceeds it by more than 2^8 (then O and l are
+// rescaled: a lane's query sits in the registers of the O layout, so the
+// rescale factors move by ds_bpermute -- rare, not per tile); l is a per-lane
+// partial sum reduced once.
+//
+// Dropout: the keep bits are made by their own kernel (pure VALU at full
+// occupancy: the RNG no longer competes with the softmax for issue slots in
+// the MFMA kernels) and stored as one 32-bit word per (head, 32-query block,
+// key), bit = query % 32.  Philox4x32-10 with 16-bit uniforms: the uniform of
+// (q, key) of head bh is 16-bit half (q & 1) of word (q >> 1) & 3 of the block
+// for counter (((bh * S/32 + q/32) * S + key) * 4 + (q >> 3) & 3).  Forward,
+// dQ and dK/dV read the bits; checkpoint recompute regenerates them.
+#include "common.h"
+#include "kernels.h"
+
+namespace mipipe {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int D = 64;
+constexpr int kThreads = 256;   // 4 waves
+constexpr int kWaveRows = 64;   // rows of its own dimension per wave
+constexpr int kBlockRows = 256; // per workgroup
+constexpr int kTile = 64;       // streamed tile rows
+constexpr int kImg = kTile * D * 2;  // 8 KiB per [64][64] bf16 image
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kRescale = 8.f;  // log2 headroom before the running max is raised
+
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int ioff(int r, int c16) { return r * 128 + ((c16 ^ swz(r)) << 4); }
+__device__ __forceinline__ int arow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+// Register staging of a [64][64] bf16 tile (token stride ld): 2 x 16 B per thread.
+struct Stage {
+  u32x4 v0, v1;
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int t0, int tid) {
+    const int r0 = tid >> 3, c = tid & 7;
+    v0 = *reinterpret_cast<const u32x4*>(base + (int64_t)(t0 + r0) * ld + 8 * c);
+    v1 = *reinterpret_cast<const u32x4*>(base + (int64_t)(t0 + r0 + 32) * ld + 8 * c);
+  }
+  __device__ __forceinline__ void store(char* img, int tid) const {
+    const int r0 = tid >> 3, c = tid & 7;
+    *reinterpret_cast<u32x4*>(img + ioff(r0, c)) = v0;
+    *reinterpret_cast<u32x4*>(img + ioff(r0 + 32, c)) = v1;
+  }
+};
+
+// Row operand (A or B) of a 32x32x16 MFMA whose k index is d: row `row` of
+// the image, k-step s (d = 16 s + 8 h + 0..7).
+__device__ __forceinline__ bf16x8 row_frag(const char* img, int row, int s, int h) {
+  return *reinterpret_cast<const bf16x8*>(img + ioff(row, 2 * s + h));
+}
+
+// Column operand whose k index runs over image rows: column `col` (= d),
+// rows r0 + (j & 3) + 8 (j >> 2), j = 0..7 (r0 = block row + 16 t + 4 h):
+// two transposing reads of 4 rows x 16 columns per 16-lane group.
+__device__ __forceinline__ bf16x8 col_frag(const char* img, int r0, int col0, int lane) {
+  const int i = lane & 15;
+  const int row = r0 + (i >> 2);
+  const int col = col0 + 4 * (i & 3);  // the 16-lane group's column base + this lane's 4-column piece
+  const int o0 = ioff(row, col >> 3) + (col & 7) * 2;
+  const int o1 = ioff(row + 8, col >> 3) + (col & 7) * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// 8 registers of an accumulator tile (k-step t) as a bf16 operand.
+__device__ __forceinline__ bf16x8 pack8(const f32x16& v, int t) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[8 * t + j];
+  return o;
+}
+
+// The 16 keep words of the keys a lane holds in the query-on-lane layout (keys
+// kk0 + arow(r, h)): 4 runs of 4 consecutive words.
+__device__ __forceinline__ void load_keep_words(const uint32_t* mw, uint32_t (&wds)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 w4 = *reinterpret_cast<const u32x4*>(mw + 8 * g);
+    wds[4 * g] = w4[0]; wds[4 * g + 1] = w4[1]; wds[4 * g + 2] = w4[2]; wds[4 * g + 3] = w4[3];
+  }
+}
+
+__device__ __forceinline__ float bperm(float v, int src_lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, v)));
+}
+
+// ------------------------------------------------------------------ keep bits
+// One thread per (head, 32-query block, key) word; causal: only words with a
+// query >= the key somewhere in the block.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
+  const int nqb = a.S >> 5;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over (bh, qblk, key)
+  if (idx >= (int64_t)a.B * a.H * nqb * a.S) return;
+  const int key = (int)(idx % a.S);
+  const int qblk = (int)((idx / a.S) % nqb);
+  if (CAUSAL && key > 32 * qblk + 31) return;
+  const uint32_t t16 = a.threshold >> 16;
+  uint32_t word = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint4 w = Philox(a.seed, (uint64_t)idx * 4 + (uint64_t)c, a.offset).next4();
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      word |= (uint32_t)((ws[i] & 0xFFFFu) >= t16) << (8 * c + 2 * i);
+      word |= (uint32_t)((ws[i] >> 16) >= t16) << (8 * c + 2 * i + 1);
+    }
+  }
+  a.dmask[idx] = word;
+}
+
+// ------------------------------------------------------------------ forward
+// Per 64-key tile: two 32-key sub-tiles, each S^T (both query blocks share the
+// K fragments), softmax, P V (both share the V fragments).  K/V tiles are
+// double-buffered in LDS and staged through registers one tile ahead: one
+// barrier per tile.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg];  // K, V double-buffered
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // grid (B*H, query tiles): the query tile is the SLOW grid dimension, so under
+  // causal masking every head's longest tile is dispatched before any shorter one
+  const int nqt = (a.S + kBlockRows - 1) / kBlockRows;
+  const int qt = CAUSAL ? nqt - 1 - (int)blockIdx.y : (int)blockIdx.y;
+  const int bh = blockIdx.x, b = bh / a.H, hh = bh % a.H;
+  const int q0w = qt * kBlockRows + wave * kWaveRows;  // this wave's queries q0w .. q0w + 63
+  const bool active = q0w < a.S;
+  const int64_t hoff = (int64_t)b * a.sb_qkv + (int64_t)hh * a.sh_qkv;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + hoff;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + hoff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + hoff;
+  const bool drop = a.p > 0.f;
+  const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
+  const float sl2 = a.scale * kLog2e;
+
+  // Q^T fragments (B operand of S^T = K Q^T): query q0w + 32 qb + li, d = 16 s + 8 h + j
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = min(q0w + 32 * qb + li, a.S - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[qb][s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)q * a.ld_qkv + 16 * s + 8 * h);
+  }
+  f32x16 o[2][2];
+  float m[2], l[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    o[qb][0] = zero16();
+    o[qb][1] = zero16();
+    m[qb] = -INFINITY;
+    l[qb] = 0.f;
+  }
+
+  const int kend = CAUSAL ? min(a.S, (qt + 1) * kBlockRows) : a.S;
+  const int ntiles = kend / kTile;
+  Stage sk, sv;
+  sk.load(K, a.ld_qkv, 0, tid);
+  sv.load(V, a.ld_qkv, 0, tid);
+  sk.store(lds, tid);
+  sv.store(lds + kImg, tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const char* kimg = lds + (t & 1) * 2 * kImg;
+    const char* vimg = kimg + kImg;
+    const int k0 = t * kTile;
+    {  // next tile in flight (clamped: the last iteration reloads its own tile, unused)
+      const int tn = min(t + 1, ntiles - 1) * kTile;
+      sk.load(K, a.ld_qkv, tn, tid);
+      sv.load(V, a.ld_qkv, tn, tid);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int kk0 = k0 + 32 * kb;
+      if (!active || (CAUSAL && kk0 > q0w + kWaveRows - 1)) continue;  // wave-uniform
+      f32x16 st[2] = {zero16(), zero16()};  // [qb]: rows keys, columns queries
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = row_frag(kimg, 32 * kb + li, s, h);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) st[qb] = mfma(kf, qf[qb][s], st[qb]);
+      }
+      bf16x8 pf[2][2];  // [qb][k-step]
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int qrow = q0w + 32 * qb;  // block's first query
+        const int q = qrow + li;
+        if (CAUSAL && kk0 > qrow + 31) {  // wholly above this block's diagonal: P = 0
+          pf[qb][0] = bf16x8{};
+          pf[qb][1] = bf16x8{};
+          continue;
+        }
+        uint32_t wds[16] = {};
+        if (drop) load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
+        const bool diag = CAUSAL && kk0 + 31 > qrow;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (diag && kk0 + arow(r, h) > q) st[qb][r] = -INFINITY;
+          mx = fmaxf(mx, st[qb][r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+        if (__ballot(mx > m[qb] + kRescale)) {
+          // raise the running max; rescale O (queries in registers there) and l
+          const float mn = fmaxf(m[qb], mx);
+          const float alpha = m[qb] == -INFINITY ? 0.f : exp2f(m[qb] - mn);
+          m[qb] = mn;
+          l[qb] *= alpha;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float ar = bperm(alpha, arow(r, h));
+            o[qb][0][r] *= ar;
+            o[qb][1][r] *= ar;
+          }
+        }
+        const float mq = m[qb];
+        float ps = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(fmaf(st[qb][r], sl2, -mq));
+          ps += p;
+          if (drop) p = ((wds[r] >> li) & 1u) ? p * pscale : 0.f;
+          st[qb][r] = p;
+        }
+        l[qb] += ps;
+        pf[qb][0] = pack8(st[qb], 0);
+        pf[qb][1] = pack8(st[qb], 1);
+      }
+      // ---- O += P V for this 32-key sub-tile
+#pragma unroll
+      for (int st_ = 0; st_ < 2; ++st_)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16x8 vf = col_frag(vimg, 32 * kb + 16 * st_ + 4 * h, 32 * dt + 16 * ((lane >> 4) & 1), lane);
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) o[qb][dt] = mfma(pf[qb][st_], vf, o[qb][dt]);
+        }
+    }
+    char* nxt = lds + ((t + 1) & 1) * 2 * kImg;
+    sk.store(nxt, tid);
+    sv.store(nxt + kImg, tid);
+    __syncthreads();
+  }
+  if (!active) return;
+  bf16_t* O = reinterpret_cast<bf16_t*>(a.o) + (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const float lt = l[qb] + __shfl_xor(l[qb], 32, 64);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    const int qrow = q0w + 32 * qb;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float ir = bperm(inv, arow(r, h));
+      const int q = qrow + arow(r, h);
+      O[(int64_t)q * a.ld_o + li] = f2bf(o[qb][0][r] * ir);
+      O[(int64_t)q * a.ld_o + 32 + li] = f2bf(o[qb][1][r] * ir);
+    }
+    if (h == 0) a.lse[(int64_t)bh * a.S + qrow + li] = (m[qb] + log2f(lt > 0.f ? lt : 1.f)) / kLog2e;
+  }
+}
+
+// ------------------------------------------------------------------ delta = rowsum(dO * O)
+__global__ void __launch_bounds__(256) attn_long_delta_kernel(AttnArgs a) {
+  // 8 lanes per row (8 bf16 each)
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;  // over (b, s, h)
+  const int part = threadIdx.x & 7;
+  const int64_t rows = (int64_t)a.B * a.S * a.H;
+  float acc = 0.f;
+  int64_t bh_s = 0;
+  if (row < rows) {
+    const int hh = (int)(row % a.H);
+    const int64_t bs = row / a.H;
+    const int s = (int)(bs % a.S), b = (int)(bs / a.S);
+    const int64_t off = (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o + (int64_t)s * a.ld_o + 8 * part;
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.o) + off);
+    const bf16x8 y = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.dout) + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += (float)x[j] * (float)y[j];
+    bh_s = ((int64_t)b * a.H + hh) * a.S + s;
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (row < rows && part == 0) a.delta[bh_s] = acc;
+}
+
+// ------------------------------------------------------------------ dK, dV
+template <bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 2 * 2 * kTile * 4];  // Q, dO (x2) + lse2, delta (x2)
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nkt = (a.S + kBlockRows - 1) / kBlockRows;
+  // grid (B*H, key tiles), key tile slow: under causal masking the first key
+  // tiles see the most queries and are dispatched first
+  const int kt = (int)blockIdx.y;
+  const int bh = blockIdx.x, b = bh / a.H, hh = bh % a.H;
+  const int k0w = kt * kBlockRows + wave * kWaveRows;  // this wave's keys
+  const bool active = k0w < a.S;
+  const int64_t hoff = (int64_t)b * a.sb_qkv + (int64_t)hh * a.sh_qkv;
+  const int64_t ooff = (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + hoff;
+  const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + ooff;
+  const bool drop = a.p > 0.f;
+  const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
+  const float sl2 = a.scale * kLog2e;
+  (void)nkt;
+
+  // K^T and V^T fragments (B operands of S = Q K^T and dP = dO V^T): key k0w + 32 kb + li
+  bf16x8 kf[2][4], vf[2][4];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = min(k0w + 32 * kb + li, a.S - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[kb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.k) + hoff +
+                                                   (int64_t)key * a.ld_qkv + 16 * s + 8 * h);
+      vf[kb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.v) + hoff +
+                                                   (int64_t)key * a.ld_qkv + 16 * s + 8 * h);
+    }
+  }
+  f32x16 dk[2][2], dv[2][2];  // [kb][dt]: rows d, columns keys
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      dk[kb][dt] = zero16();
+      dv[kb][dt] = zero16();
+    }
+
+  const int qstart = CAUSAL ? (kt * kBlockRows) / kTile : 0;  // first query tile with q >= the block's first key
+  const int ntiles = a.S / kTile;
+  Stage sq, so;
+  float st_l = 0.f;
+  auto gload = [&](int t) {
+    sq.load(Q, a.ld_qkv, t * kTile, tid);
+    so.load(dO, a.ld_o, t * kTile, tid);
+    if (tid < 2 * kTile) {
+      const int64_t i = (int64_t)bh * a.S + t * kTile + (tid & (kTile - 1));
+      st_l = tid < kTile ? a.lse[i] * kLog2e : a.delta[i];
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* base = lds + buf * 2 * kImg;
+    sq.store(base, tid);
+    so.store(base + kImg, tid);
+    if (tid < 2 * kTile) reinterpret_cast<float*>(lds + 4 * kImg)[buf * 2 * kTile + tid] = st_l;
+  };
+  if (qstart < ntiles) {
+    gload(qstart);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int t = qstart; t < ntiles; ++t) {
+    const int buf = (t - qstart) & 1;
+    const char* qimg = lds + buf * 2 * kImg;
+    const char* oimg = qimg + kImg;
+    const float* lse2 = reinterpret_cast<const float*>(lds + 4 * kImg) + buf * 2 * kTile;
+    const float* dlt = lse2 + kTile;
+    const int q0 = t * kTile;
+    gload(min(t + 1, ntiles - 1));
+    if (active && !(CAUSAL && q0 + kTile - 1 < k0w)) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int qrow = q0 + 32 * qb;
+        if (CAUSAL && qrow + 31 < k0w) continue;  // every query of the block precedes every key
+        f32x16 sacc[2], dpacc[2];
+        sacc[0] = sacc[1] = dpacc[0] = dpacc[1] = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 qa = row_frag(qimg, 32 * qb + li, s, h);
+          const bf16x8 oa = row_frag(oimg, 32 * qb + li, s, h);
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            sacc[kb] = mfma(qa, kf[kb][s], sacc[kb]);
+            dpacc[kb] = mfma(oa, vf[kb][s], dpacc[kb]);
+          }
+        }
+        bf16x8 pb[2][2], sb[2][2];  // [kb][step]
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int key = k0w + 32 * kb + li;
+          uint32_t word = 0xFFFFFFFFu;
+          if (drop) word = a.dmask[((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + key];
+          const bool diag = CAUSAL && k0w + 32 * kb + 31 > qrow;
+          // row constants (lse, delta) of the 16 query rows this lane holds: LDS broadcasts
+          float lr[16], dr[16];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2 + 32 * qb + 8 * g + 4 * h);
+            const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dlt + 32 * qb + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              lr[4 * g + j] = lv[j];
+              dr[4 * g + j] = dv4[j];
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int qr = arow(r, h);
+            float p = exp2f(fmaf(sacc[kb][r], sl2, -lr[r]));
+            if (diag && key > qrow + qr) p = 0.f;
+            const float keep = drop ? (((word >> qr) & 1u) ? pscale : 0.f) : 1.f;
+            const float pd = p * keep;
+            sacc[kb][r] = pd;                              // P with dropout (for dV)
+            dpacc[kb][r] = p * (dpacc[kb][r] * keep - dr[r]);  // dS
+          }
+          pb[kb][0] = pack8(sacc[kb], 0);
+          pb[kb][1] = pack8(sacc[kb], 1);
+          sb[kb][0] = pack8(dpacc[kb], 0);
+          sb[kb][1] = pack8(dpacc[kb], 1);
+        }
+#pragma unroll
+        for (int st_ = 0; st_ < 2; ++st_)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int r0 = 32 * qb + 16 * st_ + 4 * h, c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+            const bf16x8 oc = col_frag(oimg, r0, c0, lane);
+            const bf16x8 qc = col_frag(qimg, r0, c0, lane);
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+              dv[kb][dt] = mfma(oc, pb[kb][st_], dv[kb][dt]);
+              dk[kb][dt] = mfma(qc, sb[kb][st_], dk[kb][dt]);
+            }
+          }
+      }
+    }
+    lstore(buf ^ 1);  // the other buffer: every wave left it behind the previous barrier
+    __syncthreads();
+  }
+  if (!active) return;
+  // dK^T / dV^T tiles: register r = d (32 dt + arow(r, h)), lane = key -> 4 consecutive d per 8-byte store
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = k0w + 32 * kb + li;
+    bf16_t* dK = reinterpret_cast<bf16_t*>(a.dk) + hoff + (int64_t)key * a.ld_qkv;
+    bf16_t* dV = reinterpret_cast<bf16_t*>(a.dv) + hoff + (int64_t)key * a.ld_qkv;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * dt + 8 * g + 4 * h;
+        bf16x4 kv, vv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          kv[j] = (__bf16)(dk[kb][dt][4 * g + j] * a.scale);
+          vv[j] = (__bf16)dv[kb][dt][4 * g + j];
+        }
+        *reinterpret_cast<bf16x4*>(dK + d0) = kv;
+        *reinterpret_cast<bf16x4*>(dV + d0) = vv;
+      }
+  }
+}
+
+// ------------------------------------------------------------------ dQ
+template <bool CAUSAL>
+__global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg];  // K, V double-buffered
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // grid (B*H, query tiles): the query tile is the SLOW grid dimension, so under
+  // causal masking every head's longest tile is dispatched before any shorter one
+  const int nqt = (a.S + kBlockRows - 1) / kBlockRows;
+  const int qt = CAUSAL ? nqt - 1 - (int)blockIdx.y : (int)blockIdx.y;
+  const int bh = blockIdx.x, b = bh / a.H, hh = bh % a.H;
+  const int q0w = qt * kBlockRows + wave * kWaveRows;
+  const bool active = q0w < a.S;
+  const int64_t hoff = (int64_t)b * a.sb_qkv + (int64_t)hh * a.sh_qkv;
+  const int64_t ooff = (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o;
+  const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + hoff;
+  const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + hoff;
+  const bool drop = a.p > 0.f;
+  const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
+  const float sl2 = a.scale * kLog2e;
+
+  bf16x8 qf[2][4], of[2][4];
+  float lse2[2], dlt[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = min(q0w + 32 * qb + li, a.S - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[qb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.q) + hoff +
+                                                   (int64_t)q * a.ld_qkv + 16 * s + 8 * h);
+      of[qb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.dout) + ooff +
+                                                   (int64_t)q * a.ld_o + 16 * s + 8 * h);
+    }
+    lse2[qb] = a.lse[(int64_t)bh * a.S + q] * kLog2e;
+    dlt[qb] = a.delta[(int64_t)bh * a.S + q];
+  }
+  f32x16 dq[2][2];  // [qb][dt]: rows = queries, columns = d
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    dq[qb][0] = zero16();
+    dq[qb][1] = zero16();
+  }
+
+  const int kend = CAUSAL ? min(a.S, (qt + 1) * kBlockRows) : a.S;
+  const int ntiles = kend / kTile;
+  Stage sk, sv;
+  sk.load(K, a.ld_qkv, 0, tid);
+  sv.load(V, a.ld_qkv, 0, tid);
+  sk.store(lds, tid);
+  sv.store(lds + kImg, tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const char* kimg = lds + (t & 1) * 2 * kImg;
+    const char* vimg = kimg + kImg;
+    const int k0 = t * kTile;
+    {
+      const int tn = min(t + 1, ntiles - 1) * kTile;
+      sk.load(K, a.ld_qkv, tn, tid);
+      sv.load(V, a.ld_qkv, tn, tid);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int kk0 = k0 + 32 * kb;
+      if (!active || (CAUSAL && kk0 > q0w + kWaveRows - 1)) continue;  // wave-uniform
+      f32x16 st[2] = {zero16(), zero16()}, dpt[2] = {zero16(), zero16()};  // [qb]: rows keys, columns queries
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = row_frag(kimg, 32 * kb + li, s, h);
+        const bf16x8 vfr = row_frag(vimg, 32 * kb + li, s, h);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          st[qb] = mfma(kf, qf[qb][s], st[qb]);
+          dpt[qb] = mfma(vfr, of[qb][s], dpt[qb]);
+        }
+      }
+      bf16x8 sb[2][2];  // [qb][k-step]: dS^T as the A operand of dQ += dS K
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int qrow = q0w + 32 * qb;
+        const int q = qrow + li;
+        if (CAUSAL && kk0 > qrow + 31) {
+          sb[qb][0] = bf16x8{};
+          sb[qb][1] = bf16x8{};
+          continue;
+        }
+        uint32_t wds[16] = {};
+        if (drop) load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
+        const bool diag = CAUSAL && kk0 + 31 > qrow;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(fmaf(st[qb][r], sl2, -lse2[qb]));
+          if (diag && kk0 + arow(r, h) > q) p = 0.f;
+          float d = dpt[qb][r];
+          if (drop) d = ((wds[r] >> li) & 1u) ? d * pscale : 0.f;
+          st[qb][r] = p * (d - dlt[qb]);
+        }
+        sb[qb][0] = pack8(st[qb], 0);
+        sb[qb][1] = pack8(st[qb], 1);
+      }
+#pragma unroll
+      for (int st_ = 0; st_ < 2; ++st_)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16x8 kc = col_frag(kimg, 32 * kb + 16 * st_ + 4 * h, 32 * dt + 16 * ((lane >> 4) & 1), lane);
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) dq[qb][dt] = mfma(sb[qb][st_], kc, dq[qb][dt]);
+        }
+    }
+    char* nxt = lds + ((t + 1) & 1) * 2 * kImg;
+    sk.store(nxt, tid);
+    sv.store(nxt + kImg, tid);
+    __syncthreads();
+  }
+  if (!active) return;
+  bf16_t* dQ = reinterpret_cast<bf16_t*>(a.dq) + hoff;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = q0w + 32 * qb + arow(r, h);
+      dQ[(int64_t)q * a.ld_qkv + li] = f2bf(dq[qb][0][r] * a.scale);
+      dQ[(int64_t)q * a.ld_qkv + 32 + li] = f2bf(dq[qb][1][r] * a.scale);
+    }
+}
+
+template <bool CAUSAL>
+void run_fwd(const AttnArgs& a, hipStream_t s) {
+  if (a.p > 0.f) {
+    const int64_t words = (int64_t)a.B * a.H * (a.S / 32) * a.S;
+    hipLaunchKernelGGL((attn_long_mask_kernel<CAUSAL>), dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, a);
+  }
+  const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
+  hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
+}
+
+template <bool CAUSAL>
+void run_bwd(const AttnArgs& a, hipStream_t s) {
+  const int64_t rows = (int64_t)a.B * a.S * a.H;
+  hipLaunchKernelGGL(attn_long_delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, a);
+  const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
+  hipLaunchKernelGGL((attn_long_dkdv_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
+}
+
+}  // namespace
+
+bool attention_long_supported(int S, int Dh) { return Dh == D && S >= kBlockRows && S % kTile == 0; }
+
+void attention_long_fwd(const AttnArgs& ai, hipStream_t s) {
+  AttnArgs a = ai;
+  a.threshold = dropout_threshold(a.p);
+  if (a.causal) run_fwd<true>(a, s);
+  else run_fwd<false>(a, s);
+}
+
+void attention_long_bwd(const AttnArgs& ai, hipStream_t s) {
+  AttnArgs a = ai;
+  a.threshold = dropout_threshold(a.p);
+  if (a.causal) run_bwd<true>(a, s);
+  else run_bwd<false>(a, s);
+}
+
+}  // namespace mipipe

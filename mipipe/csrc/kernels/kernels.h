@@ -145,6 +145,9 @@ struct AttnArgs {
   uint32_t threshold = 0;
   uint64_t seed = 0, offset = 0;
   bool causal = false;
+  // long-sequence kernels with dropout: keep bits, one uint32 per (b*h, 32-query
+  // block, key) written by the forward and read by the backward
+  uint32_t* dmask = nullptr;
 };
 bool attention_supported(int S, int D);
 // S == 128 backward: fused one-pass kernel (1, default) or delta + dK/dV + dQ kernels (0).
@@ -153,6 +156,10 @@ void attention_fwd(const AttnArgs& a, hipStream_t s);
 void attention_bwd(const AttnArgs& a, hipStream_t s);
 // fp32 q/k/v/o (v_mfma_f32_32x32x2_f32): S % 32 == 0, D == 64; "key-quad" dropout layout.
 bool attention_f32_supported(int S, int D);
+// bf16, D == 64, S >= 256, S % 64 == 0 (attention_long.hip): 32x32x16 MFMA, stored dropout bits.
+bool attention_long_supported(int S, int D);
+void attention_long_fwd(const AttnArgs& a, hipStream_t s);
+void attention_long_bwd(const AttnArgs& a, hipStream_t s);
 void attention_f32_fwd(const AttnArgs& a, hipStream_t s);
 void attention_f32_bwd(const AttnArgs& a, hipStream_t s);
 

@@ -53,20 +53,21 @@ class _AttentionPacked(torch.autograd.Function):
     def forward(ctx, qkv, causal, p, scale):  # type: ignore[override]
         kern = kernels_for(qkv)
         q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
-        o, lse, seed, offset = kern.attention_fwd(q, k, v, causal, p, scale)
-        ctx.save_for_backward(qkv, o, lse)
+        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale)
+        ctx.save_for_backward(qkv, o, lse, bits)
         ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
         return o
 
     @staticmethod
     def backward(ctx, do):  # type: ignore[override]
-        qkv, o, lse = ctx.saved_tensors
+        qkv, o, lse, bits = ctx.saved_tensors
         kern = kernels_for(do)
         if do.stride() != o.stride():
             do = do.contiguous()
         dqkv = torch.empty_like(qkv)
         kern.attention_bwd(do, qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2), o, lse, ctx.causal, ctx.p,
-                           ctx.scale, ctx.seed, ctx.offset, dqkv.select(2, 0), dqkv.select(2, 1), dqkv.select(2, 2))
+                           ctx.scale, ctx.seed, ctx.offset, dqkv.select(2, 0), dqkv.select(2, 1), dqkv.select(2, 2),
+                           bits if bits.numel() else None)
         return dqkv, None, None, None
 
 
@@ -76,19 +77,20 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, p, scale):  # type: ignore[override]
         kern = kernels_for(q)
-        o, lse, seed, offset = kern.attention_fwd(q, k, v, causal, p, scale)
-        ctx.save_for_backward(q, k, v, o, lse)
+        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale)
+        ctx.save_for_backward(q, k, v, o, lse, bits)
         ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
         return o
 
     @staticmethod
     def backward(ctx, do):  # type: ignore[override]
-        q, k, v, o, lse = ctx.saved_tensors
+        q, k, v, o, lse, bits = ctx.saved_tensors
         kern = kernels_for(do)
         if do.stride() != o.stride():
             do = do.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        kern.attention_bwd(do, q, k, v, o, lse, ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, dq, dk, dv)
+        kern.attention_bwd(do, q, k, v, o, lse, ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, dq, dk, dv,
+                           bits if bits.numel() else None)
         return dq, dk, dv, None, None, None
 
 

@@ -158,7 +158,7 @@ def test_attention_f32(k, causal, p, S):
     keep = None
     if p > 0:
         torch.manual_seed(11)  # the op's draw, replayed to read its (seed, offset)
-        _, _, seed, offset = k.attention_fwd(*(qkv.detach().select(2, i) for i in range(3)), causal, p, scale)
+        _, _, seed, offset, _ = k.attention_fwd(*(qkv.detach().select(2, i) for i in range(3)), causal, p, scale)
         keep = _keyquad_keep(B, H, S, p, seed, offset).to(DEV)
         assert abs(keep.double().mean().item() - (1 - p)) < 0.03
     qf = qkv.detach().double().requires_grad_()
@@ -183,9 +183,9 @@ def test_attention_f32_recompute_replays_mask(k):
     B, S, H, D = 2, 128, 4, 64
     q, kk, v = (torch.randn(B, S, H, D, device=DEV) for _ in range(3))
     torch.manual_seed(7)
-    o1, lse1, s1, off1 = k.attention_fwd(q, kk, v, False, 0.2, 0.125)
+    o1, lse1, s1, off1, _ = k.attention_fwd(q, kk, v, False, 0.2, 0.125)
     torch.manual_seed(7)
-    o2, lse2, s2, off2 = k.attention_fwd(q, kk, v, False, 0.2, 0.125)
+    o2, lse2, s2, off2, _ = k.attention_fwd(q, kk, v, False, 0.2, 0.125)
     assert (s1, off1) == (s2, off2) and torch.equal(o1, o2) and torch.equal(lse1, lse2)
 
 

@@ -524,6 +524,35 @@ def _attn_keep_mask(B, H, S, p, seed, offset):
     return torch.from_numpy((w >= thr).reshape(B, H, S, S))
 
 
+def _long_keep_mask(B, H, S, p, seed, offset):
+    """Dropout mask of the long-sequence kernels (attention_long.hip): the uniform of
+    (q, key) of head bh is 16-bit half (q & 1) of word (q >> 1) & 3 of Philox counter
+    ((bh * S/32 + q/32) * S + key) * 4 + (q >> 3) & 3."""
+    import numpy as np
+
+    bh, q, key = np.meshgrid(np.arange(B * H), np.arange(S), np.arange(S), indexing="ij")
+    qq = q % 32
+    sub = ((bh.astype(np.uint64) * np.uint64(S // 32) + (q // 32).astype(np.uint64)) * np.uint64(S)
+           + key.astype(np.uint64)) * np.uint64(4) + (qq >> 3).astype(np.uint64)
+    seed &= 0xFFFFFFFFFFFFFFFF
+    offset &= 0xFFFFFFFFFFFFFFFF
+    m32 = np.uint64(0xFFFFFFFF)
+    words = _philox4x32_10(sub & m32, sub >> np.uint64(32), np.uint64(offset) & m32, np.uint64(offset) >> np.uint64(32),
+                           seed & 0xFFFFFFFF, seed >> 32)
+    w = np.choose((qq >> 1) & 3, words)
+    u16 = (w >> (np.uint64(16) * (qq & 1).astype(np.uint64))) & np.uint64(0xFFFF)
+    thr = min(int(p * 4294967296.0), 0xFFFFFFFF) >> 16
+    return torch.from_numpy((u16 >= thr).reshape(B, H, S, S))
+
+
+def _bits_to_mask(bits, B, H, S):
+    """Keep bits stored by the long-sequence forward: word [bh, q // 32, key], bit q % 32."""
+    w = bits.view(B * H, S // 32, S).to(torch.int64) & 0xFFFFFFFF
+    shifts = torch.arange(32, device=bits.device, dtype=torch.int64)
+    m = (w.unsqueeze(2) >> shifts.view(1, 1, 32, 1)) & 1  # [bh, qblk, 32, key]
+    return m.reshape(B, H, S, S).bool().cpu()
+
+
 def _ref_attention_masked(q, k, v, causal, keep, p, scale):
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if causal:
@@ -538,7 +567,7 @@ def _ref_attention_masked(q, k, v, causal, keep, p, scale):
 @pytest.mark.parametrize("D", [64, 128, 256])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("p", [0.0, 0.25])
-@pytest.mark.parametrize("S,fused", [(128, 1), (128, 0), (256, 1)])
+@pytest.mark.parametrize("S,fused", [(128, 1), (128, 0), (256, 1), (512, 1), (320, 1)])
 def test_attention_packed(k, D, causal, p, S, fused):
     """S = 128 runs the fused one-pass backward (fused=1) or the general
     delta + dK/dV + dQ kernels (fused=0); S = 256 always the general ones."""
@@ -556,10 +585,21 @@ def _check_attention_packed(k, D, causal, p, S):
     B, H = 2, 2
     qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16).requires_grad_()
     scale = 1.0 / math.sqrt(D)
+    long = k.attention_long_supported(S, D)
     if p > 0:
         q, kk, v = (qkv.detach().select(2, i) for i in range(3))
-        o, lse, seed, offset = k.attention_fwd(q, kk, v, causal, p, scale)
-        keep = _attn_keep_mask(B, H, S, p, seed, offset)
+        o, lse, seed, offset, bits = k.attention_fwd(q, kk, v, causal, p, scale)
+        if long:
+            keep = _long_keep_mask(B, H, S, p, seed, offset)
+            stored = _bits_to_mask(bits, B, H, S)
+            if causal:  # blocks wholly above the diagonal are never written
+                tri = torch.ones(S, S, dtype=torch.bool).tril()
+                assert torch.equal(stored & tri, keep & tri)
+            else:
+                assert torch.equal(stored, keep)
+        else:
+            assert bits.numel() == 0
+            keep = _attn_keep_mask(B, H, S, p, seed, offset)
         assert abs(keep.float().mean().item() - (1 - p)) < 0.02
     else:
         keep = None
@@ -568,8 +608,8 @@ def _check_attention_packed(k, D, causal, p, S):
     if p > 0:
         # the op drew its own seed: rebuild the mask from the generator state it used
         torch.manual_seed(11)
-        _, _, seed2, offset2 = k.attention_fwd(*(qkv.detach().select(2, i) for i in range(3)), causal, p, scale)
-        keep = _attn_keep_mask(B, H, S, p, seed2, offset2)
+        _, _, seed2, offset2, _ = k.attention_fwd(*(qkv.detach().select(2, i) for i in range(3)), causal, p, scale)
+        keep = (_long_keep_mask if long else _attn_keep_mask)(B, H, S, p, seed2, offset2)
     qf = qkv.detach().float().requires_grad_()
     qh, kh, vh = (qf.select(2, i).transpose(1, 2) for i in range(3))
     ref = _ref_attention_masked(qh, kh, vh, causal, keep, p, scale).transpose(1, 2)

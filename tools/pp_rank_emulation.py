@@ -1,0 +1,138 @@
+"""One pipeline rank of a PP=8 enc12_d4096 run, emulated on ONE MI355X without transport.
+
+The rank's two looping chunks (the plan bench.py builds at PP=8: chunks=32,
+micro-batch 32 x 128, except_last) run through the real PipelineEngine with a
+loopback channel (sends and receives complete immediately; receive buffers
+hold random activations / gradients), so the GPU executes exactly the rank's
+kernels in the rank's schedule.  Reported:
+
+* wall   -- host wall time of one step (host issue + GPU);
+* gpu    -- the same step issued behind a long GPU sleep kernel, so the host
+            finishes enqueueing before the GPU reaches it: GPU time with no
+            host gaps (= kernel busy + inter-kernel dependency latency);
+* busy   -- gpu / wall: the share of the step the GPU is not waiting for the host.
+
+    python tools/pp_rank_emulation.py [--rank R] [--steps N] [--graphs]
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+
+from mipipe import ops  # noqa: E402
+from mipipe._native_loader import kernels  # noqa: E402
+from mipipe.models import CONFIGS  # noqa: E402
+from mipipe.optim import FlatAdam  # noqa: E402
+from mipipe.parallel import PipelineEngine  # noqa: E402
+from mipipe.parallel.p2p import Channels  # noqa: E402
+from mipipe.parallel.stage import build_stage, choose_virtual, stage_input_shape  # noqa: E402
+
+
+class _Done:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+class Loopback(Channels):
+    """Channels stand-in: every transfer completes at once (no bytes move)."""
+
+    def __init__(self, rank: int, world: int) -> None:  # no process groups
+        self.rank, self.world, self.ranks = rank, world, list(range(world))
+        self.host_staged = False
+
+    def send_act(self, t):
+        return _Done()
+
+    def recv_act(self, t):
+        return _Done()
+
+    def send_grad(self, t):
+        return _Done()
+
+    def recv_grad(self, t):
+        return _Done()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, default=-1, help="pipeline rank to emulate (default: the most loaded)")
+    ap.add_argument("--pp", type=int, default=8)
+    ap.add_argument("--chunks", type=int, default=32)
+    ap.add_argument("--micro-batch", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--checkpoint", default="except_last")
+    args = ap.parse_args()
+
+    dev = torch.device("cuda", 0)
+    cfg = CONFIGS["enc12_d4096"]
+    pp, m, mb = args.pp, args.chunks, args.micro_batch
+    recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
+    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute)
+    rank = args.rank if args.rank >= 0 else max(range(pp), key=plan.rank_cost)
+    torch.manual_seed(0)
+    stages = [build_stage(cfg, plan, vs, device=dev, dtype=torch.bfloat16).train() for vs in plan.vstages(rank)]
+    shapes = [stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)]
+    opt = FlatAdam([p for s in stages for p in s.parameters()], lr=1e-4, max_grad_norm=0.5)
+    last = any(vs == pp * virtual - 1 for vs in plan.vstages(rank))
+    V = cfg.vocab
+
+    def loss_fn(y, t):
+        return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
+
+    engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint, act_shape=shapes, act_dtype=torch.bfloat16,
+                            loss_fn=loss_fn if last else None, group=Loopback(rank, pp), device=dev,
+                            skip_routes={})
+    g = torch.Generator(device="cpu").manual_seed(0)
+    tokens = torch.randint(0, V, (m, mb, cfg.seq_len + 1), generator=g)
+    inputs = [tokens[i, :, :cfg.seq_len].to(dev) for i in range(m)] if rank == 0 else None
+    targets = [tokens[i, :, 1:].contiguous().to(dev) for i in range(m)]
+    params = sum(p.numel() for p in opt.params)
+    print(f"# PP={pp} rank {rank} of enc12_d4096 (plan v={virtual}, split head {plan.split_decoder}, "
+          f"vstages {plan.vstages(rank)}, units {[len(plan.slice(v)) for v in plan.vstages(rank)]}), "
+          f"{params / 1e6:.1f}M params, chunks {m} x micro-batch {mb} x {cfg.seq_len}, {args.checkpoint}")
+
+    def step():
+        opt.zero_grad()
+        engine.step(inputs, targets)
+        opt.step(opt.grad_sumsq())
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    walls, gpus = [], []
+    k = kernels()
+    for _ in range(args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+        walls.append(wall)
+        # the same step behind a GPU sleep that outlasts the host's enqueueing
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k.gpu_sleep(int(wall * 1.5 * 1e3) + 20000)
+        e0.record()
+        h0 = time.perf_counter()
+        step()
+        e1.record()
+        host = (time.perf_counter() - h0) * 1e3
+        torch.cuda.synchronize()
+        gpu = e0.elapsed_time(e1)
+        if host > wall * 1.5:
+            print(f"  warning: host enqueue {host:.1f} ms outlasted the sleep; gpu time includes host gaps")
+        gpus.append(gpu)
+    wall, gpu = statistics.median(walls), statistics.median(gpus)
+    print(f"wall {wall:.2f} ms/step   gpu (no host gaps) {gpu:.2f} ms/step   busy = gpu/wall = {100 * gpu / wall:.1f} %")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
