@@ -13,6 +13,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdlib.h>
+
 namespace mipipe {
 
 namespace {
@@ -24,6 +26,9 @@ __device__ __forceinline__ float4 nt_load(const float4* p) {
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// NT: streaming loads (default) or regular ones (MIPIPE_SUMSQ_NT=0, for A/B runs:
+// profiles/optim_nt_pp8_ab.txt).
+template <bool NT>
 __global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
                                                             float* __restrict__ partial) {
   __shared__ float sm[8];
@@ -31,7 +36,7 @@ __global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restr
   const int64_t nvec = n / 4;
   const float4* g4 = reinterpret_cast<const float4*>(g);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 v = nt_load(g4 + i);
+    const float4 v = NT ? nt_load(g4 + i) : g4[i];
     acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
   if (blockIdx.x == 0) {
@@ -95,8 +100,13 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
   const float4* G = reinterpret_cast<const float4*>(grad);
   float4* Mo = reinterpret_cast<float4*>(m);
   float4* V = reinterpret_cast<float4*>(v);
-  // Every operand is read exactly once per step: streaming (non-temporal)
-  // loads; stores stay regular (nt stores measured 3% slower on MI355X).
+  // master, m and v are read once per step here; main_grad was read once
+  // before, by sumsq_partial_kernel (grad-norm), also with streaming loads.
+  // Streaming (non-temporal) loads measured faster at enc12 PP=1, where the
+  // gradients (GBs) are far larger than L2 + MALL; a PP=8 slice (~180M
+  // parameters) could keep main_grad cache-resident between the two passes --
+  // see profiles/optim_nt_pp8_ab.txt.  Stores stay regular (nt stores
+  // measured 3% slower on MI355X).
   for (int64_t i = tid; i < n4; i += stride) {
     float4 p = nt_load(P + i), mm = nt_load(Mo + i),
            vv = nt_load(V + i);
@@ -136,7 +146,12 @@ int sumsq_parts(int64_t n) {
 }
 
 void sumsq(const float* g, int64_t n, float* partial, int nparts, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(nparts), dim3(256), 0, s, g, n, partial);
+  static const bool nt = [] {
+    const char* e = getenv("MIPIPE_SUMSQ_NT");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (nt) hipLaunchKernelGGL(sumsq_partial_kernel<true>, dim3(nparts), dim3(256), 0, s, g, n, partial);
+  else hipLaunchKernelGGL(sumsq_partial_kernel<false>, dim3(nparts), dim3(256), 0, s, g, n, partial);
   hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, s, partial, nparts, out);
 }
 

@@ -6,16 +6,16 @@ loopback channel (sends and receives complete immediately; receive buffers
 hold random activations / gradients), so the GPU executes exactly the rank's
 kernels in the rank's schedule.  Reported:
 
-* wall   -- host wall time of one step (host issue + GPU);
-* gpu    -- the same step issued behind a long GPU sleep kernel, so the host
-            finishes enqueueing before the GPU reaches it: GPU time with no
-            host gaps (= kernel busy + inter-kernel dependency latency);
-* busy   -- gpu / wall: the share of the step the GPU is not waiting for the host.
+* wall   -- host wall time of one step (host issue + GPU), synchronised.
+Run it under ``rocprofv3 --kernel-trace --stats``: total kernel time divided by
+the steps executed is the GPU busy time per step; busy / wall is the share of
+the step the GPU spends in kernels (the rest is launch gaps and host waits).
+(Issuing a step behind a long sleep kernel does not isolate the GPU time: the
+host blocks once the queue holds a few thousand packets.)
 
-    python tools/pp_rank_emulation.py [--rank R] [--steps N] [--graphs]
+    python tools/pp_rank_emulation.py [--rank R] [--steps N]
 """
 import argparse
-import os
 import statistics
 import sys
 import time
@@ -25,7 +25,6 @@ import torch
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 
 from mipipe import ops  # noqa: E402
-from mipipe._native_loader import kernels  # noqa: E402
 from mipipe.models import CONFIGS  # noqa: E402
 from mipipe.optim import FlatAdam  # noqa: E402
 from mipipe.parallel import PipelineEngine  # noqa: E402
@@ -107,30 +106,17 @@ def main() -> int:
     for _ in range(2):
         step()
     torch.cuda.synchronize()
-    walls, gpus = [], []
-    k = kernels()
+    walls = []
     for _ in range(args.steps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         step()
         torch.cuda.synchronize()
-        wall = (time.perf_counter() - t0) * 1e3
-        walls.append(wall)
-        # the same step behind a GPU sleep that outlasts the host's enqueueing
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        k.gpu_sleep(int(wall * 1.5 * 1e3) + 20000)
-        e0.record()
-        h0 = time.perf_counter()
-        step()
-        e1.record()
-        host = (time.perf_counter() - h0) * 1e3
-        torch.cuda.synchronize()
-        gpu = e0.elapsed_time(e1)
-        if host > wall * 1.5:
-            print(f"  warning: host enqueue {host:.1f} ms outlasted the sleep; gpu time includes host gaps")
-        gpus.append(gpu)
-    wall, gpu = statistics.median(walls), statistics.median(gpus)
-    print(f"wall {wall:.2f} ms/step   gpu (no host gaps) {gpu:.2f} ms/step   busy = gpu/wall = {100 * gpu / wall:.1f} %")
+        walls.append((time.perf_counter() - t0) * 1e3)
+    wall = statistics.median(walls)
+    total = 2 + args.steps
+    print(f"wall {wall:.2f} ms/step (median of {args.steps}); {total} steps executed in all -- GPU busy per step = "
+          f"rocprofv3 total kernel time / {total}")
     return 0
 
 
