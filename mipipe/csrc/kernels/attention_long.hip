@@ -130,15 +130,15 @@ __device__ __forceinline__ float bperm(float v, int src_lane) {
 
 // ------------------------------------------------------------------ keep bits
 // One thread per (head, 32-query block, key) word; causal: only words with a
-// query >= the key somewhere in the block.
+// query >= the key somewhere in the block.  Grid (S / 256, S / 32, B * H): no
+// 64-bit division in the index math.
 template <bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
-  const int nqb = a.S >> 5;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over (bh, qblk, key)
-  if (idx >= (int64_t)a.B * a.H * nqb * a.S) return;
-  const int key = (int)(idx % a.S);
-  const int qblk = (int)((idx / a.S) % nqb);
-  if (CAUSAL && key > 32 * qblk + 31) return;
+  const int key = blockIdx.x * 256 + threadIdx.x;
+  const int qblk = blockIdx.y;
+  if (CAUSAL && (int)blockIdx.x * 256 > 32 * qblk + 31) return;  // whole block above the diagonal
+  if (key >= a.S || (CAUSAL && key > 32 * qblk + 31)) return;
+  const int64_t idx = ((int64_t)blockIdx.z * gridDim.y + qblk) * a.S + key;
   const uint32_t t16 = a.threshold >> 16;
   uint32_t word = 0;
 #pragma unroll
@@ -624,10 +624,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
 
 template <bool CAUSAL>
 void run_fwd(const AttnArgs& a, hipStream_t s) {
-  if (a.p > 0.f) {
-    const int64_t words = (int64_t)a.B * a.H * (a.S / 32) * a.S;
-    hipLaunchKernelGGL((attn_long_mask_kernel<CAUSAL>), dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, a);
-  }
+  if (a.p > 0.f)
+    hipLaunchKernelGGL((attn_long_mask_kernel<CAUSAL>), dim3((a.S + 255) / 256, a.S / 32, a.B * a.H), dim3(256), 0, s, a);
   const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
   hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
 }
