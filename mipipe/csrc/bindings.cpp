@@ -395,6 +395,7 @@ void check_gemm_2d(const Tensor& t, const char* name) {
   check_cuda(t, name);
   MP_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name, " must be bf16 or fp32");
   MP_CHECK(t.dim() == 2, name, " must be 2-D");
+  MP_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 
 void check_same_dtype(const Tensor& a, const Tensor& b, const char* what) {
@@ -811,8 +812,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_supported", &py_gemm_supported);
   m.def("gemm_f32_supported", &py_gemm_f32_supported);
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);
-  m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 auto (default)");
+  m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 ping-pong except wgrad (default)");
   m.def("gemm_get_schedule", &gemm_get_schedule);
+  m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none());
   m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none());

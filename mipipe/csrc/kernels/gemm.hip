@@ -32,6 +32,8 @@
 //                    autograd add kernel folded into the dgrad), bf16 store;
 //   kEpiAccumF32  -- C(fp32) += acc  (weight gradients straight into main_grad);
 //   kEpiStoreF32  -- fp32 store.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -117,7 +119,18 @@ __device__ __forceinline__ bf16x8 read_frag(const char* tile, int ib, int s, int
   }
 }
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU with erf from Abramowitz & Stegun 7.1.26 (|error| < 1.5e-7,
+// far below the bf16 output rounding): one rcp + one exp and a handful of
+// registers, where ocml's erff keeps so many values live that the 16-value
+// epilogue row blocks spilled (1.2 KB scratch per lane).
+__device__ __forceinline__ float erf_as(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float y = 1.f - poly * __expf(-ax * ax);
+  return copysignf(y, x);
+}
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
 
 // Bijective XCD-aware remap + grouped (8 tile-rows) ordering.
 __device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
@@ -256,36 +269,38 @@ namespace big {
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int kThreads = 512;
 constexpr int kTileBytes = BM * BK * 2;      // 32 KiB per operand tile
-constexpr int kBufBytes = 2 * kTileBytes;    // A + B
 constexpr int kSmemBytes = 128 * 260 * 4;    // 130 KiB: 2 x 64 KiB operand buffers, reused by the epilogue
 
-// I-contiguous image with 512-byte rows (256 i values).
-__device__ __forceinline__ int ic_off(int r, int c8) { return r * 512 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
+// I-contiguous image with 2W-byte rows (W = 256 or 128 i values; the B tile of
+// the 256x128 variant is 128 wide).
+template <int W>
+__device__ __forceinline__ int ic_off_w(int r, int c8) { return r * (2 * W) + ((c8 ^ (ic_rk(r) << 2)) << 3); }
 
 // LDS-DMA staging (global_load_lds_dwordx4: 16 bytes per lane, lane-linear
 // 1 KiB per wave-instruction; the bank swizzle is applied to the per-lane
 // SOURCE address).
 //
-// Loop-invariant per-lane byte offsets of the 4 pieces a wave stages per
-// operand tile; the K position lives in the scalar base, so each LDS-DMA is
+// Loop-invariant per-lane byte offsets of the W/64 pieces a wave stages per
+// W-wide operand tile; the K position lives in the scalar base, so each LDS-DMA is
 // issued in SADDR form (SGPR base + 32-bit VGPR offset) with no per-tile
 // address arithmetic.  gemm_supported() keeps rows * ld * 2 bytes < 4 GiB.
 // Edge tiles: i indices past `lim` (M for A, N for B) are clamped onto the last
 // valid row / 8-column chunk, so every DMA reads mapped memory; the garbage
 // they produce lands only in accumulator rows/columns the epilogue masks off.
-template <bool KC>
-__device__ __forceinline__ void stage_offsets(int64_t ld, int i0, int lim, int wave, int lane, uint32_t (&off)[4]) {
+template <bool KC, int W>
+__device__ __forceinline__ void stage_offsets(int64_t ld, int i0, int lim, int wave, int lane, uint32_t (&off)[W / 64]) {
+  constexpr int NU = W / 64, LPR = W / 8;  // DMAs per wave; 16-byte chunks per I-contiguous row
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int inst = wave * 4 + u;
+  for (int u = 0; u < NU; ++u) {
+    const int inst = wave * NU + u;
     if (KC) {
       const int row = 8 * inst + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       const int gi = min(i0 + row, lim - 1);
       off[u] = (uint32_t)(((int64_t)gi * ld + 8 * c) * 2);
     } else {
-      const int row = 2 * inst + (lane >> 5);
-      const int c16 = (lane & 31) ^ (ic_rk(row) << 1);
+      const int row = (64 / LPR) * inst + lane / LPR;
+      const int c16 = (lane % LPR) ^ (ic_rk(row) << 1);
       const int gi = min(i0 + 8 * c16, lim - 8);
       off[u] = (uint32_t)(((int64_t)row * ld + gi) * 2);
     }
@@ -309,12 +324,13 @@ __device__ __forceinline__ void glds16_saddr(const char* base, uint32_t off, con
       : "memory", "m0");
 }
 
-template <bool KC>
-__device__ __forceinline__ void stage_fast(const bf16_t* base, int64_t ld, int k0, const uint32_t (&off)[4], char* tile,
-                                           int wave) {
+template <bool KC, int W>
+__device__ __forceinline__ void stage_fast(const bf16_t* base, int64_t ld, int k0, const uint32_t (&off)[W / 64],
+                                           char* tile, int wave) {
+  constexpr int NU = W / 64;
   const char* b = reinterpret_cast<const char*>(base) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * ld * 2);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) glds16_saddr(b, off[u], tile + (wave * 4 + u) * 1024);
+  for (int u = 0; u < NU; ++u) glds16_saddr(b, off[u], tile + (wave * NU + u) * 1024);
 }
 
 // Operand base and local k of K-tile k0 (K-segmented operands, GemmArgs::seg_k).
@@ -328,7 +344,7 @@ __device__ __forceinline__ const bf16_t* seg_base(const GemmArgs& g, bool is_a, 
   return reinterpret_cast<const bf16_t*>(is_a ? g.a_seg[s] : g.b_seg[s]);
 }
 
-template <bool KC>
+template <bool KC, int W>
 __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane) {
   if (KC) {
     const int r = ib + (lane & 15);
@@ -338,9 +354,65 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
     const int r0 = 32 * s + 8 * g + q;
     const int c8 = (ib >> 2) + p;
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0, c8)));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0 + 4, c8)));
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off_w<W>(r0, c8)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off_w<W>(r0 + 4, c8)));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+// Epilogue parameters as plain values: read from the kernel arguments once.
+// (Reached through a GemmArgs reference, every field was re-loaded -- an
+// s_load plus its wait -- after each 2-byte aux store, which may alias it.)
+struct EpiParams {
+  bf16_t* aux;
+  int64_t ldc;
+  uint64_t seed, offset;
+  int M, N;
+  float p, pscale;
+  uint32_t threshold;
+};
+
+// Register-phase bf16 epilogue of accumulator row block i (16 rows x 16 NJ
+// cols of the wave's tile): bias, activation, dropout in place, aux (pre-activation)
+// stores.  One instantiation per i: as a loop, the Philox-heavy body is not
+// unrolled and a runtime i demotes the whole accumulator array to scratch.
+// Predicated throughout (no continue/break, for the same reason).
+// EXTRA = false: bias + activation only (no dropout, no aux) -- straight-line
+// code; with the dropout / aux branches merely present, the compiler's
+// per-element control flow cost ~5 us per 256x256 tile round (K = 64 sweep).
+template <int I, int ACT, int NJ, bool EXTRA>
+__device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ], int nrow, int ncol,
+                                         const float (&bias)[NJ]) {
+  if constexpr (!EXTRA) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pre = acc[I][j][r] + bias[j];
+        acc[I][j][r] = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
+      }
+    return;
+  }
+  const int row0 = nrow + 16 * I;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = ncol + 16 * j;
+    const bool col_ok = col < ep.N;
+    const float b = bias[j];
+    uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (ep.p > 0.f) {
+      const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)ep.N + (uint64_t)col;
+      const uint4 w = Philox(ep.seed, sub, ep.offset).next4();
+      ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float pre = acc[I][j][r] + b;
+      float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
+      if (ep.p > 0.f) out = ws[r] >= ep.threshold ? out * ep.pscale : 0.f;
+      acc[I][j][r] = out;
+      if (ep.aux != nullptr && col_ok && row0 + r < ep.M) ep.aux[(int64_t)(row0 + r) * ep.ldc + col] = f2bf(pre);
+    }
   }
 }
 
@@ -362,13 +434,25 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane
 //     the last interval of tile u -- group 0 after its phase-3 MFMAs, group 1
 //     in its phase-3 load interval -- so every wave's reads of tile u+1 start
 //     after a barrier all DMAs of the tile have landed behind.
+//
 // 0: one barrier per K-tile everywhere, 1: ping-pong everywhere, 2 (default):
 // ping-pong except the weight-gradient layout (both operands I-contiguous),
 // where the per-tile loop measured 1-4 % faster (profiles/gemm_saddr_ab.txt).
+// (A piece-staged variant -- each half-tile re-staged as soon as its own last
+// reader was 2 phases behind, 6 phases of DMA lead, counted vmcnt -- measured
+// 1-8 % slower than ping-pong: profiles/gemm_schedules_ab.txt.)
 int g_gemm_sched = 2;
 
-template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP>
+// W: block tile width along N -- 256, or 128 for grids where 256x256 tiles
+// would leave CUs idle (256x128 block, 128x32 per wave).
+// EXTRA: the bf16 epilogue also applies dropout and/or stores the
+// pre-activation (otherwise it is branch-free bias + activation).
+template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP, int W, bool EXTRA>
 __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
+  constexpr int NJ = W / 64;          // 16-wide MFMA column tiles per wave
+  constexpr int JJ = NJ / 2;          // ... per ping-pong quadrant
+  constexpr int WN = W / 4;           // wave tile width
+  constexpr int kBuf = kTileBytes + W * BK * 2;  // A + B tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -376,34 +460,34 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
 
   int tm, tn;
-  tile_coords((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  f32x4 acc[8][4];
+  tile_coords((g.M + BM - 1) / BM, (g.N + W - 1) / W, tm, tn);
+  const int m0 = tm * BM, n0 = tn * W;
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BK;
-  uint32_t offA[4], offB[4];
-  stage_offsets<A_KC>(g.lda, m0, g.M, wave, lane, offA);
-  stage_offsets<B_KC>(g.ldb, n0, g.N, wave, lane, offB);
+  uint32_t offA[4], offB[NJ];
+  stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave, lane, offA);
+  stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave, lane, offB);
   {
     int kl;
     const bf16_t* A = seg_base(g, true, 0, kl);
-    stage_fast<A_KC>(A, g.lda, kl, offA, smem, wave);
+    stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem, wave);
     const bf16_t* B = seg_base(g, false, 0, kl);
-    stage_fast<B_KC>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
+    stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
   }
 
   if constexpr (PP) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
-    bf16x8 af[4][2], bf[2][2][2];
+    bf16x8 af[4][2], bf[2][JJ][2];
     for (int u = 0; u < nk; ++u) {
-      const char* cur = smem + (u & 1) * kBufBytes;
-      char* nxt = smem + ((u + 1) & 1) * kBufBytes;
+      const char* cur = smem + (u & 1) * kBuf;
+      char* nxt = smem + ((u + 1) & 1) * kBuf;
       const bool more = u + 1 < nk;
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph) {
@@ -414,24 +498,24 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
           for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC>(cur, wm * 128 + qm * 64 + 16 * ii, s, lane);
+            for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC, 256>(cur, wm * 128 + qm * 64 + 16 * ii, s, lane);
         }
         if (ph == 0 || ph == 1) {
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
+          for (int jj = 0; jj < JJ; ++jj)
 #pragma unroll
             for (int s = 0; s < 2; ++s)
-              bf[qn][jj][s] = frag<B_KC>(cur + kTileBytes, wn * 64 + qn * 32 + 16 * jj, s, lane);
+              bf[qn][jj][s] = frag<B_KC, W>(cur + kTileBytes, wn * WN + qn * (WN / 2) + 16 * jj, s, lane);
         }
         if (ph == 0 && more) {
           int kl;
           const bf16_t* A = seg_base(g, true, (u + 1) * BK, kl);
-          stage_fast<A_KC>(A, g.lda, kl, offA, nxt, wave);
+          stage_fast<A_KC, 256>(A, g.lda, kl, offA, nxt, wave);
         }
         if (ph == 1 && more) {
           int kl;
           const bf16_t* B = seg_base(g, false, (u + 1) * BK, kl);
-          stage_fast<B_KC>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
+          stage_fast<B_KC, W>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
         }
         if (ph == 3 && wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -445,9 +529,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
           for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-              acc[qm * 4 + ii][qn * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  af[ii][s], bf[qn][jj][s], acc[qm * 4 + ii][qn * 2 + jj], 0, 0, 0);
+            for (int jj = 0; jj < JJ; ++jj)
+              acc[qm * 4 + ii][qn * JJ + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  af[ii][s], bf[qn][jj][s], acc[qm * 4 + ii][qn * JJ + jj], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
         if (ph == 3 && wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -463,96 +547,61 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * kBufBytes;
+      char* nxt = smem + ((kt + 1) & 1) * kBuf;
       int kl;
       const bf16_t* A = seg_base(g, true, (kt + 1) * BK, kl);
-      stage_fast<A_KC>(A, g.lda, kl, offA, nxt, wave);
+      stage_fast<A_KC, 256>(A, g.lda, kl, offA, nxt, wave);
       const bf16_t* B = seg_base(g, false, (kt + 1) * BK, kl);
-      stage_fast<B_KC>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
+      stage_fast<B_KC, W>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
     }
-    const char* cur = smem + (kt & 1) * kBufBytes;
+    const char* cur = smem + (kt & 1) * kBuf;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 bfr[4];
+      bf16x8 bfr[NJ];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bfr[t] = frag<B_KC>(cur + kTileBytes, wn * 64 + 16 * t, s, lane);
+      for (int t = 0; t < NJ; ++t) bfr[t] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * t, s, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const bf16x8 af = frag<A_KC>(cur, wm * 128 + 16 * i, s, lane);
+        const bf16x8 af = frag<A_KC, 256>(cur, wm * 128 + 16 * i, s, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
     }
   }
   }
 
   // ---- epilogue ----
-  // 1) element-wise epilogue in registers (accumulator layout);
+  // 1) element-wise epilogue in registers (accumulator layout): bias,
+  //    activation, dropout (the mask is tied to this layout), the optional
+  //    pre-activation aux output;
   // 2) the block's 256 x 256 result is written out through LDS in two halves
   //    (waves wm = 0, then wm = 1): each wave spills its 128 x 64 tile into a
   //    [128][260] fp32 image (the 4-float row pad makes the scattered 4-byte
-  //    writes conflict-free), then all 512 threads stream whole 1 KiB rows
-  //    back with 16-byte accesses -- fp32 read-modify-write for an
-  //    accumulated weight gradient, plain 16-byte fp32 stores for the first
-  //    write of a step (kEpiStoreF32).
+  //    writes conflict-free), then all 512 threads stream whole rows back with
+  //    16-byte accesses -- 8 bf16 per store (+ the residual addend, read as
+  //    16-byte row chunks), fp32 read-modify-write for an accumulated weight
+  //    gradient, plain fp32 stores for the first write of a step.
+  //    (The earlier direct 2-byte bf16 stores cost ~5 us per 256x256 tile at
+  //    K = 64 more than this path: tools/gemm_k_sweep.py.)
   const int quad = lane >> 4, col_in = lane & 15;
   const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
-  if (EPI == kEpiStoreBf16) {
-    // With a residual addend, the addend values of half the lane's rows (64)
-    // are loaded before that half's first store (in program order, so no
-    // aliasing question serialises them): 64 loads in flight instead of one
-    // per store, within the 256-VGPR budget of 2 waves/SIMD.
-    const bool has_res = g.res != nullptr;
+  if (EPI == kEpiStoreBf16 && (EXTRA || ACT != kActNone || g.bias != nullptr)) {
+    const int ncol = n0 + wn * WN + col_in, nrow = m0 + wm * 128 + 4 * quad;
+    const EpiParams ep{reinterpret_cast<bf16_t*>(g.aux), g.ldc, g.seed, g.offset, g.M, g.N, g.p, pscale, g.threshold};
+    float bias[NJ];  // the lane's NJ columns: loaded once, all in flight together
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      bf16_t rv[4][4][4];
-      if (has_res) {
-        const bf16_t* R = reinterpret_cast<const bf16_t*>(g.res);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = m0 + wm * 128 + 16 * (4 * half + ii) + 4 * quad + r;
-              const int col = n0 + wn * 64 + 16 * j + col_in;
-              rv[ii][j][r] = (col < g.N && row < g.M) ? R[(int64_t)row * g.ldc + col] : (bf16_t)0;
-            }
-      }
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = 4 * half + ii;
-        const int row0 = m0 + wm * 128 + 16 * i + 4 * quad;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          // Predicated (never continue/break: the accumulator array must stay
-          // fully unrolled in registers -- an early exit spills it to scratch).
-          const int col = n0 + wn * 64 + 16 * j + col_in;
-          const bool col_ok = col < g.N;
-          const float b = (g.bias != nullptr && col_ok) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[col]) : 0.f;
-          uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-          if (g.p > 0.f) {
-            const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
-            const uint4 w = Philox(g.seed, sub, g.offset).next4();
-            ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pre = acc[i][j][r] + b;
-            float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
-            if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
-            if (has_res) out += bf2f(rv[ii][j][r]);
-            if (col_ok && row0 + r < g.M) {
-              reinterpret_cast<bf16_t*>(g.C)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out);
-              if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre);
-            }
-          }
-        }
-      }
-    }
-    return;  // direct 2-byte stores measured faster than staging for bf16 (profiles/gemm_ablation.txt)
+    for (int j = 0; j < NJ; ++j)
+      bias[j] = (g.bias != nullptr && ncol + 16 * j < g.N) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[ncol + 16 * j]) : 0.f;
+    epi_rows<0, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<1, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<2, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<3, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<4, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<5, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<6, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<7, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
   }
-  constexpr int kStride = 260;  // floats per staged row (256 + 4 pad)
+  constexpr int kStride = W + 4;  // floats per staged row (+ 4 pad)
   float* stg = reinterpret_cast<float*>(smem);
   __syncthreads();  // every wave is done reading the operand buffers
 #pragma unroll
@@ -561,33 +610,42 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            stg[(16 * i + 4 * quad + r) * kStride + wn * 64 + 16 * j + col_in] = acc[i][j][r];
+            stg[(16 * i + 4 * quad + r) * kStride + wn * WN + 16 * j + col_in] = acc[i][j][r];
     }
     __syncthreads();
     const int rbase = m0 + pass * 128;
     if (EPI == kEpiStoreBf16) {
       bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+      constexpr int CPR = W / 8;  // 128 rows x W/8 chunks of 8 columns
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {  // 128 rows x 32 chunks of 8 columns
+      for (int u = 0; u < 128 * CPR / kThreads; ++u) {
         const int idx = tid + u * kThreads;
-        const int row = idx >> 5, c8 = idx & 31;
+        const int row = idx / CPR, c8 = idx % CPR;
         if (rbase + row >= g.M || n0 + 8 * c8 >= g.N) continue;
-        const float4 lo = *reinterpret_cast<const float4*>(stg + row * kStride + 8 * c8);
-        const float4 hi = *reinterpret_cast<const float4*>(stg + row * kStride + 8 * c8 + 4);
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8 + 4);
+        const int64_t at = (int64_t)(rbase + row) * g.ldc + n0 + 8 * c8;
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (g.res != nullptr) {
+          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(g.res) + at);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+        }
         bf16x8 o;
-        o[0] = (__bf16)lo.x; o[1] = (__bf16)lo.y; o[2] = (__bf16)lo.z; o[3] = (__bf16)lo.w;
-        o[4] = (__bf16)hi.x; o[5] = (__bf16)hi.y; o[6] = (__bf16)hi.z; o[7] = (__bf16)hi.w;
-        *reinterpret_cast<bf16x8*>(C + (int64_t)(rbase + row) * g.ldc + n0 + 8 * c8) = o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+        *reinterpret_cast<bf16x8*>(C + at) = o;
       }
     } else {
       float* C = reinterpret_cast<float*>(g.C);
+      constexpr int CPR = W / 4;  // 128 rows x W/4 chunks of 4 columns
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {  // 128 rows x 64 chunks of 4 columns
+      for (int u = 0; u < 128 * CPR / kThreads; ++u) {
         const int idx = tid + u * kThreads;
-        const int row = idx >> 6, c4 = idx & 63;
+        const int row = idx / CPR, c4 = idx % CPR;
         if (rbase + row >= g.M || n0 + 4 * c4 >= g.N) continue;
         const float4 v = *reinterpret_cast<const float4*>(stg + row * kStride + 4 * c4);
         float4* dst = reinterpret_cast<float4*>(C + (int64_t)(rbase + row) * g.ldc + n0 + 4 * c4);
@@ -605,34 +663,65 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 
 }  // namespace big
 
-int big_tiles(const GemmArgs& g) { return ((g.M + big::BM - 1) / big::BM) * ((g.N + big::BN - 1) / big::BN); }
+int big_tiles(const GemmArgs& g, int w) { return ((g.M + big::BM - 1) / big::BM) * ((g.N + w - 1) / w); }
 
-// The 256x256 kernel handles every shape (edge tiles masked); the 128x128 one
+// The 256-row kernel handles every shape (edge tiles masked); the 128x128 one
 // only exact multiples of 128, where it is kept for grids too small to fill
 // the 256 CUs with 256x256 tiles.
 bool use_big(const GemmArgs& g) {
-  return g.seg_k > 0 || g.M % BM != 0 || g.N % BN != 0 || big_tiles(g) >= 128;
+  return g.seg_k > 0 || g.M % BM != 0 || g.N % BN != 0 || big_tiles(g, 256) >= 128;
+}
+
+// Block width of the 256-row kernel: 256, or 128 when the grid of 256x256
+// tiles quantises badly onto the 256 CUs -- rounds of 256 tiles, a round of
+// 256x128 tiles costing ~0.73 of a 256x256 round (measured, 2048 x 12288 x
+// 4096).  E.g. T = 2048: 2048 x 4096 is 128 256x256 tiles, half the chip
+// idle, or 256 256x128 tiles (1.2x faster, profiles/gemm_vs_hipblaslt.txt).
+// gemm_set_width(128 / 256) or MIPIPE_GEMM_W forces one (A/B, tests).
+int g_gemm_width = -1;  // -1: not read from the environment yet, 0: auto
+
+int big_width(const GemmArgs& g) {
+  if (g_gemm_width < 0) {
+    const char* e = getenv("MIPIPE_GEMM_W");
+    g_gemm_width = e ? atoi(e) : 0;
+  }
+  if (g_gemm_width == 128 || g_gemm_width == 256) return g_gemm_width;
+  const int r256 = (big_tiles(g, 256) + 255) / 256, r128 = (big_tiles(g, 128) + 255) / 256;
+  return 0.75 * r128 < 1.0 * r256 ? 128 : 256;
+}
+
+template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP, int W, bool EXTRA>
+void launch_big(const GemmArgs& g, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA>), dim3(big_tiles(g, W)),
+                     dim3(big::kThreads), big::kSmemBytes, s, g);
+}
+
+template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
+void launch_big_w(const GemmArgs& g, hipStream_t s) {
+  const bool pp = big::g_gemm_sched == 1 || (big::g_gemm_sched == 2 && (A_KC || B_KC));
+  const bool narrow = big_width(g) == 128;
+  if (pp && narrow) launch_big<A_KC, B_KC, EPI, ACT, true, 128, EXTRA>(g, s);
+  else if (pp) launch_big<A_KC, B_KC, EPI, ACT, true, 256, EXTRA>(g, s);
+  else if (narrow) launch_big<A_KC, B_KC, EPI, ACT, false, 128, EXTRA>(g, s);
+  else launch_big<A_KC, B_KC, EPI, ACT, false, 256, EXTRA>(g, s);
 }
 
 template <bool A_KC, bool B_KC, int EPI, int ACT>
 void launch(const GemmArgs& g, hipStream_t s) {
   if (use_big(g)) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
-      attr_set = true;
+    if constexpr (EPI == kEpiStoreBf16) {
+      if (g.p > 0.f || g.aux != nullptr) {
+        launch_big_w<A_KC, B_KC, EPI, ACT, true>(g, s);
+        return;
+      }
     }
-    const int blocks = big_tiles(g);
-    const bool pp = big::g_gemm_sched == 1 || (big::g_gemm_sched == 2 && (A_KC || B_KC));
-    if (pp)
-      hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, true>), dim3(blocks), dim3(big::kThreads),
-                         big::kSmemBytes, s, g);
-    else
-      hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, false>), dim3(blocks), dim3(big::kThreads),
-                         big::kSmemBytes, s, g);
+    launch_big_w<A_KC, B_KC, EPI, ACT, false>(g, s);
     return;
   }
   const int blocks = (g.M / BM) * (g.N / BN);
@@ -651,6 +740,7 @@ void launch_act(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 void gemm_set_schedule(int mode) { big::g_gemm_sched = mode; }
+void gemm_set_width(int w) { g_gemm_width = w; }
 int gemm_get_schedule() { return big::g_gemm_sched; }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {

@@ -119,6 +119,7 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K);
 // Main-loop schedule of the 256x256 GEMM: 0 = one barrier per K-tile, 1 = ping-pong wave groups,
 // 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout (default).
 void gemm_set_schedule(int mode);
+void gemm_set_width(int w);  // 256-row GEMM block width: 0 auto, 128, 256
 int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
 // Same interface with fp32 operands (and fp32 bias / res / aux / C): v_mfma_f32_32x32x2_f32.

@@ -74,12 +74,19 @@ def _gemm_supported(k, dtype: torch.dtype, m: int, n: int, kk: int) -> bool:
     return False
 
 
+def _aligned(t: Tensor) -> bool:
+    """The GEMM moves operands, addends and outputs in 16-byte chunks."""
+    return t.data_ptr() % 16 == 0
+
+
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
     """All three GEMMs of the layer (fwd [T,N,K], dgrad [T,K,N], wgrad [N,K,T]) fit the tile kernel."""
     t, (n, kk) = x2.shape[0], weight.shape
     dt = x2.dtype
     return (
         weight.dtype == dt
+        and _aligned(x2)
+        and _aligned(weight)
         and _gemm_supported(k, dt, t, n, kk)
         and _gemm_supported(k, dt, t, kk, n)
         and _gemm_supported(k, dt, n, kk, t)
@@ -102,8 +109,10 @@ class _Linear(torch.autograd.Function):
             r2 = None
             if res is not None:
                 r2 = res.reshape(-1, w.shape[0])
-                if r2.dtype != x2.dtype or not r2.is_contiguous():
+                if r2.dtype != x2.dtype or not r2.is_contiguous() or not _aligned(r2):
                     r2 = r2.to(x2.dtype).contiguous()
+                    if not _aligned(r2):
+                        r2 = r2.clone()
             y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2, r2)
             res = None  # added in the epilogue
         else:
@@ -162,7 +171,7 @@ class _Linear(torch.autograd.Function):
             r2 = None
             if dres is not None:
                 r2 = dres.reshape(-1, dres.shape[-1])
-                if not (ctx.fused_tile and r2.dtype == dpre.dtype and r2.is_contiguous()):
+                if not (ctx.fused_tile and r2.dtype == dpre.dtype and r2.is_contiguous() and _aligned(r2)):
                     r2 = None
             if ctx.fused_tile:
                 dx = k.linear_dgrad(dpre, w, r2)

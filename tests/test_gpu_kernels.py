@@ -349,6 +349,48 @@ def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
     assert err < 1e-2 * math.sqrt(K / 64), err
 
 
+@pytest.mark.parametrize("width", [256, 128])
+@pytest.mark.parametrize("sched", [0, 1, 2])
+def test_gemm_main_loop_schedules(k, sched, width):
+    """Every 256x256 main loop (per-tile barrier, ping-pong, the default mix) on every
+    layout, for 1, 2, 3 and many K-tiles, edge tiles, K-segments and the bf16 epilogue."""
+    from mipipe.ops import linear
+
+    old = k.gemm_get_schedule()
+    k.gemm_set_schedule(sched)
+    k.gemm_set_width(width)
+    try:
+        torch.manual_seed(7)
+        for M, N, K in [(520, 264, 64), (1000, 1000, 128), (4096, 4800, 192), (2048, 4096, 1024), (256, 256, 320)]:
+            a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+            b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+            ref = a.float() @ b.float()
+            for a_kc, b_kc in [(True, True), (True, False), (False, False), (False, True)]:
+                c = k.gemm_f32(a if a_kc else a.t().contiguous(), b.t().contiguous() if b_kc else b, a_kc, b_kc)
+                err = (c - ref).abs().max().item()
+                assert err < 1e-2 * math.sqrt(K / 64), (M, N, K, a_kc, b_kc, err)
+        dys = [torch.randn(128, 264, device=DEV).to(torch.bfloat16) for _ in range(5)]
+        xs = [torch.randn(128, 136, device=DEV).to(torch.bfloat16) for _ in range(5)]
+        main = torch.zeros(264, 136, device=DEV)
+        k.linear_wgrad_segments(dys, xs, main)
+        expect = sum(d.float().t() @ x.float() for d, x in zip(dys, xs))
+        assert ((main - expect).abs().max() / expect.abs().max()).item() < 1e-3
+        x = torch.randn(1000, 512, device=DEV).to(torch.bfloat16)
+        w = (torch.randn(1000, 512, device=DEV) / math.sqrt(512)).to(torch.bfloat16)
+        bias = torch.randn(1000, device=DEV).to(torch.bfloat16)
+        y = linear(x, w, bias, "gelu", 0.0, True)
+        ref = F.gelu(x.float() @ w.float().t() + bias.float())
+        assert torch.allclose(y.float(), ref, atol=3e-2, rtol=3e-2)
+        # the residual addend (16-byte row chunks in the staged epilogue)
+        r = torch.randn(1000, 1000, device=DEV).to(torch.bfloat16)
+        y = k.linear_fwd(x, w, bias, 0, 0.0, False, r)[0]
+        ref = x.float() @ w.float().t() + bias.float() + r.float()
+        assert torch.allclose(y.float(), ref, atol=3e-2, rtol=3e-2)
+    finally:
+        k.gemm_set_schedule(old)
+        k.gemm_set_width(0)
+
+
 def test_linear_op_matches_reference(k):
     from mipipe.ops import linear
 
@@ -639,9 +681,12 @@ def test_transformer_layer_bf16_kernels_vs_torch(k):
 
     from mipipe.models import TransformerEncoderLayer
 
+    import copy
+
     torch.manual_seed(0)
     E, H, F_, B, S = 512, 4, 1024, 2, 128
     ref = nn.TransformerEncoderLayer(E, H, F_, dropout=0.0, batch_first=True).to(DEV)
+    ref_bf16 = copy.deepcopy(ref).to(torch.bfloat16)  # PyTorch's own bf16 error sets the gradient bar
     ours = TransformerEncoderLayer(E, H, F_, dropout=0.0, device=DEV).load_from_torch(ref).to(torch.bfloat16)
     x = torch.randn(B, S, E, device=DEV)
     xb = x.to(torch.bfloat16).requires_grad_()
@@ -654,26 +699,32 @@ def test_transformer_layer_bf16_kernels_vs_torch(k):
     g = torch.randn_like(yr)
     y.backward(g.to(torch.bfloat16))
     yr.backward(g)
+    ref_bf16(x.to(torch.bfloat16)).backward(g.to(torch.bfloat16))
 
     def rel(a, b):
         return (a.float() - b.float()).abs().max().item() / (b.float().abs().max().item() + 1e-6)
 
     assert rel(xb.grad, xr.grad) < 3e-2, rel(xb.grad, xr.grad)
     attn, ff = ours[0], ours[1]
-    pairs = [(attn.core.in_proj_weight, ref.self_attn.in_proj_weight), (attn.core.in_proj_bias, ref.self_attn.in_proj_bias),
-             (attn.out.out_proj_weight, ref.self_attn.out_proj.weight), (attn.out.out_proj_bias, ref.self_attn.out_proj.bias),
-             (attn.out.norm_weight, ref.norm1.weight), (attn.out.norm_bias, ref.norm1.bias),
-             (ff.fc_in.linear1_weight, ref.linear1.weight), (ff.fc_in.linear1_bias, ref.linear1.bias),
-             (ff.fc_out.linear2_weight, ref.linear2.weight), (ff.fc_out.linear2_bias, ref.linear2.bias),
-             (ff.fc_out.norm_weight, ref.norm2.weight), (ff.fc_out.norm_bias, ref.norm2.bias)]
+    names = [("self_attn.in_proj_weight", attn.core.in_proj_weight), ("self_attn.in_proj_bias", attn.core.in_proj_bias),
+             ("self_attn.out_proj.weight", attn.out.out_proj_weight), ("self_attn.out_proj.bias", attn.out.out_proj_bias),
+             ("norm1.weight", attn.out.norm_weight), ("norm1.bias", attn.out.norm_bias),
+             ("linear1.weight", ff.fc_in.linear1_weight), ("linear1.bias", ff.fc_in.linear1_bias),
+             ("linear2.weight", ff.fc_out.linear2_weight), ("linear2.bias", ff.fc_out.linear2_bias),
+             ("norm2.weight", ff.fc_out.norm_weight), ("norm2.bias", ff.fc_out.norm_bias)]
+    ref_p, bf_p = dict(ref.named_parameters()), dict(ref_bf16.named_parameters())
+
     def rel_fro(a, b):
         # norm-wise: a ReLU whose bf16 pre-activation lands on the other side of 0
         # moves single elements of the weight gradient by a whole token's share
         return (a.float() - b.float()).norm().item() / (b.float().norm().item() + 1e-6)
 
-    for ours_p, ref_p in pairs:
+    for name, ours_p in names:
         got = ours_p.main_grad if getattr(ours_p, "main_grad", None) is not None else ours_p.grad
-        assert got is not None and rel_fro(got, ref_p.grad) < 2e-2, (tuple(ref_p.shape), rel_fro(got, ref_p.grad))
+        assert got is not None
+        err, torch_err = rel_fro(got, ref_p[name].grad), rel_fro(bf_p[name].grad, ref_p[name].grad)
+        # within PyTorch's own bf16 error (linear1.weight: ~0.045 vs torch 0.050 -- ReLU flips)
+        assert err < max(1.25 * torch_err, 2e-2), (name, err, torch_err)
 
 
 def test_vocab_split_decoder_gpu(k):

@@ -1,6 +1,8 @@
 """A/B of the GEMM main-loop schedules at the enc12_d4096 training shapes
 (micro-batch T = 4096 tokens): forward (KC,KC + bias/ReLU), dgrad (KC,IC),
-deferred wgrad (IC,IC, K-segmented over 4 micro-batches, fp32 accumulate)."""
+deferred wgrad (IC,IC, K-segmented over 4 micro-batches, fp32 accumulate).
+
+    python tools/gemm_model_ab.py [SCHED ...]    (default: 0 1; see gemm_set_schedule)"""
 import statistics
 import sys
 
@@ -10,6 +12,7 @@ sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from mipipe._native_loader import kernels  # noqa: E402
 
 k = kernels()
+SCHEDS = [int(a) for a in sys.argv[1:]] or [0, 1]
 T, E, V = 4096, 4096, 28928
 
 
@@ -44,7 +47,7 @@ for N, K in ((3 * E, E), (E, E), (V, E)):
 
 for name, fl, fn in cases:
     res = []
-    for sc in (0, 1):
+    for sc in SCHEDS:
         k.gemm_set_schedule(sc)
         t = timeit(fn)
         res.append(f"sched={sc} {t:8.1f} us {fl / t / 1e6:6.0f} TF/s")
