@@ -133,7 +133,7 @@ __device__ __forceinline__ float erf_as(float x) {
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
 
 // Bijective XCD-aware remap + grouped (8 tile-rows) ordering.
-__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn, int G = 8) {
   const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
   int wg = bid;
@@ -142,7 +142,6 @@ __device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, i
     const int q = nwg >> 3, r = nwg & 7;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
   }
-  constexpr int G = 8;
   const int group = wg / (G * tiles_n);
   const int first_m = group * G;
   const int gsize = min(tiles_m - first_m, G);
@@ -460,7 +459,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
 
   int tm, tn;
-  tile_coords((g.M + BM - 1) / BM, (g.N + W - 1) / W, tm, tn);
+  tile_coords((g.M + BM - 1) / BM, (g.N + W - 1) / W, tm, tn, g.group_m);
   const int m0 = tm * BM, n0 = tn * W;
   f32x4 acc[8][NJ];
 #pragma unroll
@@ -712,8 +711,16 @@ void launch_big_w(const GemmArgs& g, hipStream_t s) {
   else launch_big<A_KC, B_KC, EPI, ACT, false, 256, EXTRA>(g, s);
 }
 
+int g_gemm_group = -1;  // MIPIPE_GEMM_G: tile-rows per ordering group (A/B); -1 unread, 0 default
+
 template <bool A_KC, bool B_KC, int EPI, int ACT>
-void launch(const GemmArgs& g, hipStream_t s) {
+void launch(const GemmArgs& gi, hipStream_t s) {
+  if (g_gemm_group < 0) {
+    const char* e = getenv("MIPIPE_GEMM_G");
+    g_gemm_group = e ? atoi(e) : 0;
+  }
+  GemmArgs g = gi;
+  if (g_gemm_group > 0) g.group_m = g_gemm_group;
   if (use_big(g)) {
     if constexpr (EPI == kEpiStoreBf16) {
       if (g.p > 0.f || g.aux != nullptr) {

@@ -106,6 +106,7 @@ struct GemmArgs {
   float p = 0.f;
   uint32_t threshold = 0;
   uint64_t seed = 0, offset = 0;
+  int group_m = 8;  // tile-rows per group of the block -> tile order (L2 reuse of B tiles)
   // K-segmented operands (deferred weight gradients: one GEMM over the
   // micro-batches of a step without concatenating them).  seg_k > 0: K-rows
   // [s*seg_k, (s+1)*seg_k) of A / B live at a_seg[s] / b_seg[s] (leading
