@@ -476,6 +476,15 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
   if (res) g.res = res->data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)M; g.N = (int)K; g.K = (int)N;
   g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreAct;
+  Tensor ws;  // split-K partials (stream-ordered caching allocator: freed after the kernels that use it)
+  if (dt == at::kBFloat16) {
+    const int splits = gemm_splitk_factor(g);
+    if (splits > 1) {
+      ws = at::empty({splits, M, K}, dy.options().dtype(at::kFloat));
+      g.k_splits = splits;
+      g.ws = ws.data_ptr<float>();
+    }
+  }
   gemm_run(dt, g, cur_stream(dy));
   return dx;
 }

@@ -32,6 +32,7 @@
 //                    autograd add kernel folded into the dgrad), bf16 store;
 //   kEpiAccumF32  -- C(fp32) += acc  (weight gradients straight into main_grad);
 //   kEpiStoreF32  -- fp32 store.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -467,15 +468,20 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = g.K / BK;
+  int kt0 = 0, nk = g.K / BK;
+  if (g.k_splits > 1) {  // this block's share of the K-tiles
+    const int total = nk;
+    kt0 = (int)blockIdx.y * total / g.k_splits;
+    nk = ((int)blockIdx.y + 1) * total / g.k_splits - kt0;
+  }
   uint32_t offA[4], offB[NJ];
   stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave, lane, offA);
   stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave, lane, offB);
   {
     int kl;
-    const bf16_t* A = seg_base(g, true, 0, kl);
+    const bf16_t* A = seg_base(g, true, kt0 * BK, kl);
     stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem, wave);
-    const bf16_t* B = seg_base(g, false, 0, kl);
+    const bf16_t* B = seg_base(g, false, kt0 * BK, kl);
     stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
   }
 
@@ -508,12 +514,12 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         }
         if (ph == 0 && more) {
           int kl;
-          const bf16_t* A = seg_base(g, true, (u + 1) * BK, kl);
+          const bf16_t* A = seg_base(g, true, (kt0 + u + 1) * BK, kl);
           stage_fast<A_KC, 256>(A, g.lda, kl, offA, nxt, wave);
         }
         if (ph == 1 && more) {
           int kl;
-          const bf16_t* B = seg_base(g, false, (u + 1) * BK, kl);
+          const bf16_t* B = seg_base(g, false, (kt0 + u + 1) * BK, kl);
           stage_fast<B_KC, W>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
         }
         if (ph == 3 && wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -548,9 +554,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * kBuf;
       int kl;
-      const bf16_t* A = seg_base(g, true, (kt + 1) * BK, kl);
+      const bf16_t* A = seg_base(g, true, (kt0 + kt + 1) * BK, kl);
       stage_fast<A_KC, 256>(A, g.lda, kl, offA, nxt, wave);
-      const bf16_t* B = seg_base(g, false, (kt + 1) * BK, kl);
+      const bf16_t* B = seg_base(g, false, (kt0 + kt + 1) * BK, kl);
       stage_fast<B_KC, W>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
     }
     const char* cur = smem + (kt & 1) * kBuf;
@@ -639,7 +645,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         *reinterpret_cast<bf16x8*>(C + at) = o;
       }
     } else {
-      float* C = reinterpret_cast<float*>(g.C);
+      float* C = reinterpret_cast<float*>(g.C) + (int64_t)blockIdx.y * g.M * g.ldc;  // split-K partial y
       constexpr int CPR = W / 4;  // 128 rows x W/4 chunks of 4 columns
 #pragma unroll
       for (int u = 0; u < 128 * CPR / kThreads; ++u) {
@@ -685,6 +691,7 @@ int big_width(const GemmArgs& g) {
     g_gemm_width = e ? atoi(e) : 0;
   }
   if (g_gemm_width == 128 || g_gemm_width == 256) return g_gemm_width;
+  if (g.k_splits > 1) return 256;
   const int r256 = (big_tiles(g, 256) + 255) / 256, r128 = (big_tiles(g, 128) + 255) / 256;
   return 0.75 * r128 < 1.0 * r256 ? 128 : 256;
 }
@@ -697,7 +704,7 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
     attr_set = true;
   }
-  hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA>), dim3(big_tiles(g, W)),
+  hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA>), dim3(big_tiles(g, W), g.k_splits),
                      dim3(big::kThreads), big::kSmemBytes, s, g);
 }
 
@@ -735,6 +742,37 @@ void launch(const GemmArgs& gi, hipStream_t s) {
   hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, ACT>), dim3(blocks), dim3(kThreads), kSmemBytes, s, g);
 }
 
+// C[M, N] (bf16, row stride ldc) = sum of the k_splits fp32 partials [s][M][N]
+// (+ res): 8 columns per thread, 16-byte loads and stores.
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                            int64_t ldc, const bf16_t* __restrict__ res,
+                                                            bf16_t* __restrict__ C) {
+  const int64_t chunks = (int64_t)M * (N / 8);
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= chunks) return;
+  const int row = (int)(c / (N / 8)), col = (int)(c % (N / 8)) * 8;
+  const int64_t at = (int64_t)row * N + col;
+  f32x4 lo = *reinterpret_cast<const f32x4*>(ws + at);
+  f32x4 hi = *reinterpret_cast<const f32x4*>(ws + at + 4);
+  for (int s = 1; s < splits; ++s) {
+    lo += *reinterpret_cast<const f32x4*>(ws + (int64_t)s * M * N + at);
+    hi += *reinterpret_cast<const f32x4*>(ws + (int64_t)s * M * N + at + 4);
+  }
+  float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  const int64_t out = (int64_t)row * ldc + col;
+  if (res != nullptr) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + out);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+  *reinterpret_cast<bf16x8*>(C + out) = o;
+}
+
+int g_gemm_splitk = -1;  // MIPIPE_GEMM_SPLITK=0 disables (A/B); -1 unread
+
 template <bool A_KC, bool B_KC, int EPI>
 void launch_act(const GemmArgs& g, hipStream_t s) {
   switch (g.act) {
@@ -757,9 +795,45 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K) {
          N < (1LL << 30) && M * K < (1LL << 31) && N * K < (1LL << 31);
 }
 
+// Split-K for a plain bf16 output whose 256x256 grid fills at most half the
+// 256 CUs while K is long (T = 2048 LM-head dgrad: 2048 x 4096 x 28928 is
+// 128 tiles): 2-4 blocks per tile, >= 32 K-tiles each.  The partials cost
+// 4 * splits * M * N bytes of writes + reads, worth it only for K >= 8192.
+int gemm_splitk_factor(const GemmArgs& g) {
+  if (g_gemm_splitk < 0) {
+    const char* e = getenv("MIPIPE_GEMM_SPLITK");
+    g_gemm_splitk = e ? atoi(e) : 1;
+  }
+  if (g_gemm_splitk == 0) return 1;
+  if (g.epi != kEpiStoreBf16 || g.act != kActNone || g.bias != nullptr || g.p > 0.f || g.aux != nullptr ||
+      g.seg_k > 0 || !use_big(g) || g.K < 8192)
+    return 1;
+  const int tiles = big_tiles(g, 256);
+  if (tiles > 128) return 1;
+  int splits = std::min(4, 256 / tiles);
+  while (splits > 1 && g.K / BK / splits < 32) --splits;
+  return splits;
+}
+
 void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
   GemmArgs g = gi;
   g.threshold = dropout_threshold(g.p);
+  if (g.k_splits > 1) {
+    // fp32 partials into the caller's workspace, then one reduction (+ res)
+    GemmArgs p = g;
+    p.epi = kEpiStoreF32;
+    p.C = g.ws;
+    p.ldc = g.N;
+    p.res = nullptr;
+    if (p.a_kc && p.b_kc) launch<true, true, kEpiStoreF32, kActNone>(p, s);
+    else if (p.a_kc && !p.b_kc) launch<true, false, kEpiStoreF32, kActNone>(p, s);
+    else if (!p.a_kc && !p.b_kc) launch<false, false, kEpiStoreF32, kActNone>(p, s);
+    else launch<false, true, kEpiStoreF32, kActNone>(p, s);
+    const int64_t chunks = (int64_t)g.M * (g.N / 8);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws, g.k_splits,
+                       g.M, g.N, g.ldc, reinterpret_cast<const bf16_t*>(g.res), reinterpret_cast<bf16_t*>(g.C));
+    return;
+  }
   if (g.epi == kEpiStoreBf16) {
     if (g.a_kc && g.b_kc) launch_act<true, true, kEpiStoreBf16>(g, s);
     else if (g.a_kc && !g.b_kc) launch_act<true, false, kEpiStoreBf16>(g, s);

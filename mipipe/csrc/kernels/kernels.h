@@ -107,6 +107,11 @@ struct GemmArgs {
   uint32_t threshold = 0;
   uint64_t seed = 0, offset = 0;
   int group_m = 8;  // tile-rows per group of the block -> tile order (L2 reuse of B tiles)
+  // Split-K (plain bf16 output of an under-filled grid with a long K): the
+  // K-tiles are divided among k_splits blocks per output tile, each writing
+  // an fp32 partial into ws [k_splits][M][N]; a reduction adds them (+ res).
+  int k_splits = 1;
+  float* ws = nullptr;
   // K-segmented operands (deferred weight gradients: one GEMM over the
   // micro-batches of a step without concatenating them).  seg_k > 0: K-rows
   // [s*seg_k, (s+1)*seg_k) of A / B live at a_seg[s] / b_seg[s] (leading
@@ -117,6 +122,9 @@ struct GemmArgs {
   const void* b_seg[kMaxSegs] = {};
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
+// Split-K factor gemm_bf16 would use for g (1 = none); the caller provides
+// g.ws with k_splits * M * N floats when it is > 1.
+int gemm_splitk_factor(const GemmArgs& g);
 // Main-loop schedule of the 256x256 GEMM: 0 = one barrier per K-tile, 1 = ping-pong wave groups,
 // 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout (default).
 void gemm_set_schedule(int mode);

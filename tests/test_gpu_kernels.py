@@ -391,6 +391,22 @@ def test_gemm_main_loop_schedules(k, sched, width):
         k.gemm_set_width(0)
 
 
+@pytest.mark.parametrize("M,K,N", [(2048, 4096, 9216), (1000, 4096, 8192), (2048, 1600, 28928), (776, 1024, 16384)])
+def test_linear_dgrad_split_k(k, M, K, N):
+    """Under-filled grid with a long K (the T=2048 LM-head dgrad): K split over 2-4 blocks per
+    tile, fp32 partials, one reduction (+ the fan-out residual) -- against fp32."""
+    torch.manual_seed(8)
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(N)).to(torch.bfloat16)
+    r = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = dy.float() @ w.float()
+    for res in (None, r):
+        dx = k.linear_dgrad(dy, w, res)
+        want = ref + (r.float() if res is not None else 0)
+        err = ((dx.float() - want).abs().max() / want.abs().max()).item()
+        assert err < 1e-2, (M, K, N, res is not None, err)
+
+
 def test_linear_op_matches_reference(k):
     from mipipe.ops import linear
 
