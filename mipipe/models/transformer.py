@@ -175,6 +175,39 @@ class SelfAttentionBlock(nn.Module):
         return self.core.flops_per_token(seq_len) + self.out.flops_per_token(seq_len)
 
 
+class _Unpack(torch.autograd.Function):
+    """A packed stage-boundary activation -> its parts, as contiguous views.
+
+    The packs are block-concatenated (part after part in memory, not
+    interleaved per row), so every part is a contiguous view -- the consumer
+    needs no ``.contiguous()`` copies -- and the backward writes the parts'
+    gradients into one packed gradient with a single concatenation (autograd's
+    own slice/select backward would zero-fill a packed-size tensor per part
+    and add them)."""
+
+    @staticmethod
+    def forward(ctx, packed: Tensor, lead, widths):  # type: ignore[override]
+        flat = packed.reshape(-1)
+        n = math.prod(lead)
+        outs, o = [], 0
+        for w in widths:
+            outs.append(flat[o:o + n * w].view(*lead, w))
+            o += n * w
+        ctx.packed_shape, ctx.lead, ctx.widths = packed.shape, lead, widths
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):  # type: ignore[override]
+        ref = next(g for g in grads if g is not None)
+        n = math.prod(ctx.lead)
+        parts = [g.reshape(-1) if g is not None else ref.new_zeros(n * w) for g, w in zip(grads, ctx.widths)]
+        return torch.cat(parts).view(ctx.packed_shape), None, None
+
+
+def unpack(packed: Tensor, lead, widths):
+    return _Unpack.apply(packed, tuple(lead), tuple(widths))
+
+
 class PackedAttentionCore(nn.Module):
     """Pipeline unit: ``x -> stack(x, core(x))`` so a stage boundary can fall
     between the attention core and its output projection."""
@@ -187,7 +220,9 @@ class PackedAttentionCore(nn.Module):
         self.core.reset_parameters()
 
     def forward(self, x: Tensor) -> Tensor:
-        return torch.stack((x, self.core(x)))
+        # x's residual-branch gradient comes back through the QKV dgrad epilogue (fan-out)
+        o, xr = self.core.forward_fanout(x, FANOUT)
+        return torch.stack((xr, o))
 
     def flops_per_token(self, seq_len: int) -> float:
         return self.core.flops_per_token(seq_len)
@@ -204,7 +239,9 @@ class PackedAttentionOutput(nn.Module):
         self.out.reset_parameters()
 
     def forward(self, packed: Tensor) -> Tensor:
-        return self.out(packed[0], packed[1])
+        e = packed.shape[-1]
+        x, o = unpack(packed, packed.shape[1:-1], (e, e))
+        return self.out(x, o)
 
     def flops_per_token(self, seq_len: int) -> float:
         return self.out.flops_per_token(seq_len)
@@ -328,7 +365,8 @@ class FeedForwardBlock(nn.Module):
 
 
 class PackedFeedForwardIn(nn.Module):
-    """Pipeline unit: ``x -> cat(x, h)`` on the feature dim (``[.., E + F]``)."""
+    """Pipeline unit: ``x -> [.., E + F]`` holding x and h block-concatenated
+    (all of x, then all of h: see :class:`_Unpack`)."""
 
     def __init__(self, fc_in: FeedForwardIn) -> None:
         super().__init__()
@@ -338,7 +376,8 @@ class PackedFeedForwardIn(nn.Module):
         self.fc_in.reset_parameters()
 
     def forward(self, x: Tensor) -> Tensor:
-        return torch.cat((x, self.fc_in(x)), dim=-1)
+        h, xr = self.fc_in.forward_fanout(x, FANOUT)
+        return torch.cat((xr.reshape(-1), h.reshape(-1))).view(*x.shape[:-1], x.shape[-1] + h.shape[-1])
 
     def flops_per_token(self, seq_len: int) -> float:
         return self.fc_in.flops_per_token(seq_len)
@@ -356,7 +395,8 @@ class PackedFeedForwardOut(nn.Module):
 
     def forward(self, packed: Tensor) -> Tensor:
         e = self.fc_out.d_model
-        return self.fc_out(packed[..., :e].contiguous(), packed[..., e:].contiguous())
+        x, h = unpack(packed, packed.shape[:-1], (e, packed.shape[-1] - e))
+        return self.fc_out(x, h)
 
     def flops_per_token(self, seq_len: int) -> float:
         return self.fc_out.flops_per_token(seq_len)

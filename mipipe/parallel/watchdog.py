@@ -61,6 +61,18 @@ class PendingWorks:
                 done = None
             if done is not True:
                 out.append(f"{label}{'' if done is False else ' (state unknown)'}")
+                continue
+            # completed -- but a transfer whose peer went away completes with an error
+            failed = False
+            try:
+                failed = not work.is_success()
+            except Exception:
+                try:
+                    failed = work.exception() is not None
+                except Exception:
+                    failed = False
+            if failed:
+                out.append(f"{label} (failed)")
         return out
 
     def __len__(self) -> int:
