@@ -360,25 +360,22 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane
   }
 }
 
-// Epilogue parameters as plain values: read from the kernel arguments once.
-// (Reached through a GemmArgs reference, every field was re-loaded -- an
-// s_load plus its wait -- after each 2-byte aux store, which may alias it.)
+// Epilogue parameters as plain values, read from the kernel arguments once
+// (through a GemmArgs reference the fields were re-loaded -- an s_load plus
+// its wait -- after every store that might alias them).
 struct EpiParams {
-  bf16_t* aux;
-  int64_t ldc;
   uint64_t seed, offset;
-  int M, N;
+  int N;
   float p, pscale;
   uint32_t threshold;
 };
 
 // Register-phase bf16 epilogue of accumulator row block i (16 rows x 16 NJ
-// cols of the wave's tile): bias, activation, dropout in place, aux (pre-activation)
-// stores.  One instantiation per i: as a loop, the Philox-heavy body is not
+// cols of the wave's tile): bias, activation, dropout, in place.  One instantiation per i: as a loop, the Philox-heavy body is not
 // unrolled and a runtime i demotes the whole accumulator array to scratch.
 // Predicated throughout (no continue/break, for the same reason).
-// EXTRA = false: bias + activation only (no dropout, no aux) -- straight-line
-// code; with the dropout / aux branches merely present, the compiler's
+// EXTRA = false: bias + activation only (no dropout) -- straight-line code;
+// with the dropout and aux-store branches merely present, the compiler's
 // per-element control flow cost ~5 us per 256x256 tile round (K = 64 sweep).
 template <int I, int ACT, int NJ, bool EXTRA>
 __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ], int nrow, int ncol,
@@ -397,7 +394,6 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = ncol + 16 * j;
-    const bool col_ok = col < ep.N;
     const float b = bias[j];
     uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     if (ep.p > 0.f) {
@@ -411,8 +407,78 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
       float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
       if (ep.p > 0.f) out = ws[r] >= ep.threshold ? out * ep.pscale : 0.f;
       acc[I][j][r] = out;
-      if (ep.aux != nullptr && col_ok && row0 + r < ep.M) ep.aux[(int64_t)(row0 + r) * ep.ldc + col] = f2bf(pre);
     }
+  }
+}
+
+// Writes the block's result through LDS (two halves: waves wm = 0, then 1):
+// each wave spills its 128 x W/4 accumulator tile into a [128][W+4] fp32
+// image (the 4-float row pad keeps the scattered 4-byte writes conflict-free),
+// then all 512 threads stream whole rows out with 16-byte accesses -- 8 bf16
+// per store (+ the bf16 addend `res`, read as 16-byte row chunks), fp32
+// read-modify-write (kEpiAccumF32) or fp32 stores.  Starts with the LDS free,
+// ends with a barrier (so it can run twice: aux, then the output).
+template <int EPI, int W>
+__device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W / 64], int wm, int wn, int lane,
+                                             int tid, int m0, int n0, int M, int N, int64_t ldc, void* out,
+                                             const bf16_t* res) {
+  constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512;
+  const int quad = lane >> 4, col_in = lane & 15;
+  float* stg = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(16 * i + 4 * quad + r) * kStride + wn * WN + 16 * j + col_in] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int rbase = m0 + pass * 128;
+    if (EPI == kEpiStoreBf16) {
+      bf16_t* C = reinterpret_cast<bf16_t*>(out);
+      constexpr int CPR = W / 8;  // 128 rows x W/8 chunks of 8 columns
+#pragma unroll
+      for (int u = 0; u < 128 * CPR / kT; ++u) {
+        const int idx = tid + u * kT;
+        const int row = idx / CPR, c8 = idx % CPR;
+        if (rbase + row >= M || n0 + 8 * c8 >= N) continue;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8 + 4);
+        const int64_t at = (int64_t)(rbase + row) * ldc + n0 + 8 * c8;
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (res != nullptr) {
+          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + at);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+        *reinterpret_cast<bf16x8*>(C + at) = o;
+      }
+    } else {
+      float* C = reinterpret_cast<float*>(out);
+      constexpr int CPR = W / 4;  // 128 rows x W/4 chunks of 4 columns
+#pragma unroll
+      for (int u = 0; u < 128 * CPR / kT; ++u) {
+        const int idx = tid + u * kT;
+        const int row = idx / CPR, c4 = idx % CPR;
+        if (rbase + row >= M || n0 + 4 * c4 >= N) continue;
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * kStride + 4 * c4);
+        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(rbase + row) * ldc + n0 + 4 * c4);
+        if (EPI == kEpiAccumF32) {
+          const float4 o = *dst;
+          *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        } else {
+          *dst = v;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -577,26 +643,33 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 
   // ---- epilogue ----
   // 1) element-wise epilogue in registers (accumulator layout): bias,
-  //    activation, dropout (the mask is tied to this layout), the optional
-  //    pre-activation aux output;
-  // 2) the block's 256 x 256 result is written out through LDS in two halves
-  //    (waves wm = 0, then wm = 1): each wave spills its 128 x 64 tile into a
-  //    [128][260] fp32 image (the 4-float row pad makes the scattered 4-byte
-  //    writes conflict-free), then all 512 threads stream whole rows back with
-  //    16-byte accesses -- 8 bf16 per store (+ the residual addend, read as
-  //    16-byte row chunks), fp32 read-modify-write for an accumulated weight
-  //    gradient, plain fp32 stores for the first write of a step.
+  //    activation, dropout (the mask is tied to this layout); with an aux
+  //    output, the pre-activation (acc + bias) is first written out through
+  //    the same staged path;
+  // 2) staged_store: LDS-staged 16-byte row stores (+ residual addend), fp32
+  //    read-modify-write for an accumulated weight gradient, fp32 stores for
+  //    the first write of a step or a split-K partial.
   //    (The earlier direct 2-byte bf16 stores cost ~5 us per 256x256 tile at
   //    K = 64 more than this path: tools/gemm_k_sweep.py.)
   const int quad = lane >> 4, col_in = lane & 15;
-  const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
+  __syncthreads();  // every wave is done reading the operand buffers
   if (EPI == kEpiStoreBf16 && (EXTRA || ACT != kActNone || g.bias != nullptr)) {
     const int ncol = n0 + wn * WN + col_in, nrow = m0 + wm * 128 + 4 * quad;
-    const EpiParams ep{reinterpret_cast<bf16_t*>(g.aux), g.ldc, g.seed, g.offset, g.M, g.N, g.p, pscale, g.threshold};
+    const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
+    const EpiParams ep{g.seed, g.offset, g.N, g.p, pscale, g.threshold};
     float bias[NJ];  // the lane's NJ columns: loaded once, all in flight together
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       bias[j] = (g.bias != nullptr && ncol + 16 * j < g.N) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[ncol + 16 * j]) : 0.f;
+    if (EXTRA && g.aux != nullptr) {  // pre-activation output
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] += bias[j];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bias[j] = 0.f;
+      staged_store<kEpiStoreBf16, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, g.aux, nullptr);
+    }
     epi_rows<0, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
     epi_rows<1, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
     epi_rows<2, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
@@ -606,64 +679,11 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     epi_rows<6, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
     epi_rows<7, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
   }
-  constexpr int kStride = W + 4;  // floats per staged row (+ 4 pad)
-  float* stg = reinterpret_cast<float*>(smem);
-  __syncthreads();  // every wave is done reading the operand buffers
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            stg[(16 * i + 4 * quad + r) * kStride + wn * WN + 16 * j + col_in] = acc[i][j][r];
-    }
-    __syncthreads();
-    const int rbase = m0 + pass * 128;
-    if (EPI == kEpiStoreBf16) {
-      bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
-      constexpr int CPR = W / 8;  // 128 rows x W/8 chunks of 8 columns
-#pragma unroll
-      for (int u = 0; u < 128 * CPR / kThreads; ++u) {
-        const int idx = tid + u * kThreads;
-        const int row = idx / CPR, c8 = idx % CPR;
-        if (rbase + row >= g.M || n0 + 8 * c8 >= g.N) continue;
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8 + 4);
-        const int64_t at = (int64_t)(rbase + row) * g.ldc + n0 + 8 * c8;
-        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (g.res != nullptr) {
-          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(g.res) + at);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
-        }
-        bf16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
-        *reinterpret_cast<bf16x8*>(C + at) = o;
-      }
-    } else {
-      float* C = reinterpret_cast<float*>(g.C) + (int64_t)blockIdx.y * g.M * g.ldc;  // split-K partial y
-      constexpr int CPR = W / 4;  // 128 rows x W/4 chunks of 4 columns
-#pragma unroll
-      for (int u = 0; u < 128 * CPR / kThreads; ++u) {
-        const int idx = tid + u * kThreads;
-        const int row = idx / CPR, c4 = idx % CPR;
-        if (rbase + row >= g.M || n0 + 4 * c4 >= g.N) continue;
-        const float4 v = *reinterpret_cast<const float4*>(stg + row * kStride + 4 * c4);
-        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(rbase + row) * g.ldc + n0 + 4 * c4);
-        if (EPI == kEpiAccumF32) {
-          const float4 o = *dst;
-          *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
-        } else {
-          *dst = v;
-        }
-      }
-    }
-    __syncthreads();
-  }
+  void* out = EPI == kEpiStoreBf16 ? g.C
+                                   : reinterpret_cast<void*>(reinterpret_cast<float*>(g.C) +
+                                                             (int64_t)blockIdx.y * g.M * g.ldc);  // split-K partial y
+  staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+                       EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr);
 }
 
 }  // namespace big
