@@ -453,6 +453,19 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   return {y, pre, (int64_t)seed, (int64_t)offset};
 }
 
+// Split-K (bf16 GEMMs on under-filled grids, gemm_splitk_factor): the fp32
+// partials' workspace, from the stream-ordered caching allocator (released
+// after the kernels queued on this stream that use it).  Empty when unsplit.
+Tensor split_k_workspace(GemmArgs& g, at::ScalarType dt, const Tensor& like) {
+  if (dt != at::kBFloat16) return Tensor();
+  const int splits = gemm_splitk_factor(g);
+  if (splits <= 1) return Tensor();
+  Tensor ws = at::empty({splits, (int64_t)g.M, (int64_t)g.N}, like.options().dtype(at::kFloat));
+  g.k_splits = splits;
+  g.ws = ws.data_ptr<float>();
+  return ws;
+}
+
 // dx[M,K] = dy[M,N] . w[N,K]
 // dx = dy . w (+ res): `res` is the gradient the input receives from its
 // other consumer (a residual branch), added in the epilogue.
@@ -476,15 +489,7 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
   if (res) g.res = res->data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)M; g.N = (int)K; g.K = (int)N;
   g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreAct;
-  Tensor ws;  // split-K partials (stream-ordered caching allocator: freed after the kernels that use it)
-  if (dt == at::kBFloat16) {
-    const int splits = gemm_splitk_factor(g);
-    if (splits > 1) {
-      ws = at::empty({splits, M, K}, dy.options().dtype(at::kFloat));
-      g.k_splits = splits;
-      g.ws = ws.data_ptr<float>();
-    }
-  }
+  Tensor ws = split_k_workspace(g, dt, dy);
   gemm_run(dt, g, cur_stream(dy));
   return dx;
 }
@@ -505,6 +510,7 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad, bool accumulate) {
   g.A = dy.data_ptr(); g.B = x.data_ptr(); g.C = main_grad.data_ptr();
   g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)T;
   g.a_kc = false; g.b_kc = false; g.epi = accumulate ? kEpiAccumF32 : kEpiStoreF32;
+  Tensor ws = split_k_workspace(g, dt, dy);
   gemm_run(dt, g, cur_stream(dy));
 }
 
@@ -597,6 +603,7 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
       g.b_seg[i] = xs[first + i].data_ptr();
     }
     g.A = g.a_seg[0]; g.B = g.b_seg[0];
+    Tensor ws = split_k_workspace(g, dt, main_grad);
     gemm_run(dt, g, cur_stream(main_grad));
   }
 }

@@ -791,6 +791,22 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<bf16x8*>(C + out) = o;
 }
 
+// C[M, N] (fp32, row stride ldc) (+)= sum of the k_splits fp32 partials: the
+// split-K reduction of a weight gradient (accumulate: into main_grad).
+__global__ void __launch_bounds__(256) splitk_reduce_f32_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                                int64_t ldc, bool accumulate, float* __restrict__ C) {
+  const int64_t chunks = (int64_t)M * (N / 4);
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= chunks) return;
+  const int row = (int)(c / (N / 4)), col = (int)(c % (N / 4)) * 4;
+  const int64_t at = (int64_t)row * N + col;
+  f32x4 v = *reinterpret_cast<const f32x4*>(ws + at);
+  for (int s = 1; s < splits; ++s) v += *reinterpret_cast<const f32x4*>(ws + (int64_t)s * M * N + at);
+  f32x4* dst = reinterpret_cast<f32x4*>(C + (int64_t)row * ldc + col);
+  if (accumulate) v += *dst;
+  *dst = v;
+}
+
 int g_gemm_splitk = -1;  // MIPIPE_GEMM_SPLITK=0 disables (A/B); -1 unread
 
 template <bool A_KC, bool B_KC, int EPI>
@@ -815,24 +831,40 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K) {
          N < (1LL << 30) && M * K < (1LL << 31) && N * K < (1LL << 31);
 }
 
-// Split-K for a plain bf16 output whose 256x256 grid fills at most half the
-// 256 CUs while K is long (T = 2048 LM-head dgrad: 2048 x 4096 x 28928 is
-// 128 tiles): 2-4 blocks per tile, >= 32 K-tiles each.  The partials cost
-// 4 * splits * M * N bytes of writes + reads, worth it only for K >= 8192.
+// Split-K for grids that leave CUs idle while K is long: the T = 2048 LM-head
+// dgrad (2048 x 4096 x 28928 = 128 256x256 tiles), GPT-2-XL's weight
+// gradients (1600 x 1600 = 49 tiles, 6400 x 1600 = 175, K = 4 x 8192).
+// s blocks per tile, each a contiguous share of the K-tiles, write fp32
+// partials; one reduction adds them (+ the residual / into main_grad).  s
+// minimises rounds(tiles * s) / s of the tile time (a round = 256 blocks, one
+// per CU; a 256x256 tile at ~4.5 TFLOP/s per CU) plus the partials' HBM
+// traffic, (2 s + 1) * 4 * M * N bytes at ~4 TB/s.  Plain bf16 output (no
+// bias / activation / dropout / aux: those stay in the GEMM epilogue) or an
+// fp32 weight gradient.
 int gemm_splitk_factor(const GemmArgs& g) {
   if (g_gemm_splitk < 0) {
     const char* e = getenv("MIPIPE_GEMM_SPLITK");
     g_gemm_splitk = e ? atoi(e) : 1;
   }
   if (g_gemm_splitk == 0) return 1;
-  if (g.epi != kEpiStoreBf16 || g.act != kActNone || g.bias != nullptr || g.p > 0.f || g.aux != nullptr ||
-      g.seg_k > 0 || !use_big(g) || g.K < 8192)
-    return 1;
+  const bool plain_bf16 = g.epi == kEpiStoreBf16 && g.act == kActNone && g.bias == nullptr && g.p <= 0.f &&
+                          g.aux == nullptr;
+  const bool f32_out = g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32;
+  if (!(plain_bf16 || f32_out) || !use_big(g) || g.K < 8192) return 1;
   const int tiles = big_tiles(g, 256);
-  if (tiles > 128) return 1;
-  int splits = std::min(4, 256 / tiles);
-  while (splits > 1 && g.K / BK / splits < 32) --splits;
-  return splits;
+  const int kt = g.K / BK;
+  const double t_tile = 2.0 * 256 * 256 * (double)g.K / 4.5e12;
+  const double mn = (double)g.M * g.N;
+  int best = 1;
+  double best_t = (double)((tiles + 255) / 256) * t_tile;
+  for (int sp = 2; sp <= 8 && kt / sp >= 16; ++sp) {
+    const double t = (double)((tiles * sp + 255) / 256) * t_tile / sp + (2.0 * sp + 1.0) * 4.0 * mn / 4.0e12;
+    if (t < 0.97 * best_t) {
+      best = sp;
+      best_t = t;
+    }
+  }
+  return best;
 }
 
 void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
@@ -849,9 +881,16 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
     else if (p.a_kc && !p.b_kc) launch<true, false, kEpiStoreF32, kActNone>(p, s);
     else if (!p.a_kc && !p.b_kc) launch<false, false, kEpiStoreF32, kActNone>(p, s);
     else launch<false, true, kEpiStoreF32, kActNone>(p, s);
-    const int64_t chunks = (int64_t)g.M * (g.N / 8);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws, g.k_splits,
-                       g.M, g.N, g.ldc, reinterpret_cast<const bf16_t*>(g.res), reinterpret_cast<bf16_t*>(g.C));
+    if (g.epi == kEpiStoreBf16) {
+      const int64_t chunks = (int64_t)g.M * (g.N / 8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws,
+                         g.k_splits, g.M, g.N, g.ldc, reinterpret_cast<const bf16_t*>(g.res),
+                         reinterpret_cast<bf16_t*>(g.C));
+    } else {
+      const int64_t chunks = (int64_t)g.M * (g.N / 4);
+      hipLaunchKernelGGL(splitk_reduce_f32_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws,
+                         g.k_splits, g.M, g.N, g.ldc, g.epi == kEpiAccumF32, reinterpret_cast<float*>(g.C));
+    }
     return;
   }
   if (g.epi == kEpiStoreBf16) {

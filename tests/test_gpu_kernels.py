@@ -407,6 +407,25 @@ def test_linear_dgrad_split_k(k, M, K, N):
         assert err < 1e-2, (M, K, N, res is not None, err)
 
 
+@pytest.mark.parametrize("N,K,T,nseg", [(1600, 1600, 4096, 4), (6400, 1600, 2048, 4), (520, 776, 8192, 1)])
+def test_wgrad_split_k(k, N, K, T, nseg):
+    """Weight gradients on under-filled grids (GPT-2-XL widths) split K over several blocks per
+    tile: fp32 partials reduced into main_grad -- store (first write) and accumulate."""
+    torch.manual_seed(9)
+    dys = [torch.randn(T, N, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    xs = [torch.randn(T, K, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    expect = sum(d.float().t() @ x.float() for d, x in zip(dys, xs))
+    for accumulate in (False, True):
+        main = torch.randn(N, K, device=DEV)
+        base = main.clone() if accumulate else torch.zeros_like(main)
+        if nseg == 1:
+            k.linear_wgrad(dys[0], xs[0], main, accumulate)
+        else:
+            k.linear_wgrad_segments(dys, xs, main, accumulate)
+        err = ((main - base - expect).abs().max() / expect.abs().max()).item()
+        assert err < 1e-3, (N, K, T, nseg, accumulate, err)
+
+
 def test_linear_op_matches_reference(k):
     from mipipe.ops import linear
 
