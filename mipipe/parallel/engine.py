@@ -41,6 +41,7 @@ compute.  Per-stage busy time is measured with HIP events (bubble %).
 """
 from __future__ import annotations
 
+import os
 import time
 from contextlib import contextmanager
 from dataclasses import dataclass, field
@@ -142,6 +143,9 @@ class PipelineEngine:
             marks every action, and registers every transfer, so a stalled
             step ends the process with a report naming the transfer that never
             completed.  Callers can arm it around their own waits too.
+        sync_debug: synchronise the device after every action (default: the
+            ``MIPIPE_SYNC_DEBUG=1`` environment switch) -- the serialised run
+            :func:`mipipe.debug.check_engine` compares a scheduled step with.
     """
 
     def __init__(
@@ -161,6 +165,7 @@ class PipelineEngine:
         skip_shapes: Optional[Dict[str, Tuple[Sequence[int], torch.dtype]]] = None,
         skip_routes: Optional[Dict[str, SkipRoute]] = None,
         watchdog: Union[None, float, Watchdog] = None,
+        sync_debug: Optional[bool] = None,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
             raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
@@ -188,6 +193,10 @@ class PipelineEngine:
         if isinstance(watchdog, (int, float)):
             watchdog = Watchdog(float(watchdog))
         self.watchdog: Optional[Watchdog] = watchdog
+        # serialised mode: the device is synchronised after every
+        # action, so nothing overlaps; mipipe.debug.check_engine compares a
+        # step run this way with a scheduled one
+        self.sync_debug = (os.environ.get("MIPIPE_SYNC_DEBUG") == "1") if sync_debug is None else bool(sync_debug)
         self._action = "construction"
         if isinstance(group, Channels):
             self.chan: Optional[Channels] = group
@@ -561,6 +570,8 @@ class PipelineEngine:
                             self._post_skip_recvs(sk_grad_rx, training, grad=True)
                     post_grad_recv(c, i)
                     backward(c, i)
+                if self.sync_debug and self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
             if defer is not None and started_backward:
                 self._mark("deferred weight gradients")
                 tm = self._timer()

@@ -190,6 +190,40 @@ def test_pipe_recompute_bit_identical_with_dropout():
             assert torch.equal(g[n], g0[n]), (mode, n, (g[n] - g0[n]).abs().max().item())
 
 
+# ------------------------------------------------------------------ stream-race checker
+def test_check_pipe_and_engine_on_gpu():
+    """mipipe.debug: the scheduled step (copy / compute streams overlapping) equals
+    the serialised one on our bf16 kernels with dropout 0.2 -- for the Pipe and
+    the engine."""
+    from mipipe.debug import check_engine, check_pipe
+
+    cfg = _cfg(dropout=0.2)
+    m, mb = 4, 2
+    inputs, targets = _data(cfg, m, mb)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Sequential(*build_lm_blocks(cfg, dtype=torch.bfloat16)).to(DEV)).train()
+    FlatAdam(model.parameters(), lr=1e-3)
+    pipe = Pipe(model, chunks=m, checkpoint="except_last")
+    t = torch.cat(targets).to(DEV)
+    try:
+        torch.manual_seed(3)
+        rep = check_pipe(pipe, torch.cat(inputs).to(DEV), loss_fn=lambda y: _loss_fn(cfg)(y, t))
+    finally:
+        pipe.close()
+    assert rep.ok, rep.worst()
+    assert len(rep.max_rel) > 10
+
+    torch.manual_seed(0)
+    full = torch.nn.Sequential(*build_lm_blocks(cfg)).train().to(DEV, torch.bfloat16)
+    FlatAdam(full.parameters(), lr=1e-3)
+    eng = PipelineEngine(full, chunks=m, checkpoint="always", act_shape=(mb, cfg.seq_len), act_dtype=torch.bfloat16,
+                         loss_fn=_loss_fn(cfg), device=DEV)
+    torch.manual_seed(4)
+    rep = check_engine(eng, [x.to(DEV) for x in inputs], [y.to(DEV) for y in targets])
+    assert rep.ok, rep.worst()
+    assert "loss" in rep.max_rel and not eng.sync_debug
+
+
 # ------------------------------------------------------------------ engine over RCCL
 @pytest.mark.multigpu
 @pytest.mark.parametrize("world", [2, 4])
