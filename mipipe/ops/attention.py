@@ -14,7 +14,11 @@ regenerated from Philox (seed, offset) in backward, so checkpoint recompute
 replays it exactly.  Supported on the GPU path: bf16 with ``S % 64 == 0`` and
 ``D in {64, 128, 256}`` (attention.hip), fp32 with ``S % 32 == 0`` and
 ``D == 64`` (attention_f32.hip, the reference's own precision); the
-CPU path is eager math.
+CPU path is eager math.  A CAUSAL sequence of any other length (the
+reference's ``get_batch`` tail window, /root/reference/main.py:108-113) is
+zero-padded at the end to the next supported length: under the causal mask
+no real query sees a padded key, so the real rows are exact; the padded rows
+are sliced off (and get no gradient).
 """
 from __future__ import annotations
 
@@ -116,6 +120,15 @@ def _gpu_ok(t: Tensor, S: int, D: int) -> bool:
     return False
 
 
+def _causal_pad(t: Tensor, S: int, D: int) -> Optional[int]:
+    """The padded length a causal sequence of S runs at on the kernels (None: none fits)."""
+    step = 64 if t.dtype == torch.bfloat16 else 32
+    for sp in (-(-S // step) * step, max(128, -(-S // step) * step)):
+        if sp != S and _gpu_ok(t, sp, D):
+            return sp
+    return None
+
+
 def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, training: bool = True,
                      scale: Optional[float] = None) -> Tensor:
     """``qkv [B, S, 3, H, D]`` -> ``o [B, S, H, D]``."""
@@ -125,6 +138,10 @@ def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, 
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(D)
     if qkv.is_cuda and _gpu_ok(qkv, S, D):
         return _AttentionPacked.apply(qkv.contiguous(), bool(causal), p, scale)
+    sp = _causal_pad(qkv, S, D) if (qkv.is_cuda and causal) else None
+    if sp is not None:
+        padded = torch.cat((qkv, qkv.new_zeros(B, sp - S, 3, H, D)), dim=1)
+        return _AttentionPacked.apply(padded, True, p, scale)[:, :S]
     q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
     if qkv.is_cuda:
         _note_math_path(S, D, qkv.dtype)
@@ -143,8 +160,12 @@ def attention(
         return attention_reference(q, k, v, causal, p, scale)
     S, D = q.shape[2], q.shape[3]
     if not _gpu_ok(q, S, D):
-        _note_math_path(S, D, q.dtype)
-        return attention_reference(q, k, v, causal, p, scale)
+        sp = _causal_pad(q, S, D) if causal else None
+        if sp is None:
+            _note_math_path(S, D, q.dtype)
+            return attention_reference(q, k, v, causal, p, scale)
+        pad = lambda t: torch.cat((t, t.new_zeros(t.shape[0], t.shape[1], sp - S, D)), dim=2)  # noqa: E731
+        return attention(pad(q), pad(k), pad(v), True, dropout_p, training, scale)[:, :, :S]
     qs, ks, vs = (t.transpose(1, 2) for t in (q, k, v))
     if not (qs.stride() == ks.stride() == vs.stride()) or qs.stride(3) != 1:
         qs, ks, vs = (t.contiguous() for t in (qs, ks, vs))
