@@ -22,16 +22,18 @@
 // (M, N any multiple of 8) are clamped on load and masked on store; K may be
 // split into segments living in different buffers (deferred weight gradients).
 // Block ids are remapped so consecutive tiles of an 8-row group share an XCD's
-// L2 (T1, bijective form).  A 128x128 register-staged kernel serves grids too
-// small for 256x256 tiles.
-// Epilogues:
+// L2 (T1, bijective form).  Grids that would leave CUs idle get a 256x128 block
+// (big_width) or, with a long K, split-K: 2-8 blocks per tile writing fp32
+// partials that one reduction adds (gemm_splitk_factor).  A 128x128
+// register-staged kernel serves small exact-multiple grids.
+// Epilogues (all results leave through LDS as 16-byte row stores, staged_store):
 //   kEpiStoreBf16 -- + bias, activation (ReLU/GELU), dropout (Philox mask in
 //                    the "column-quad" layout shared with the elementwise
 //                    backward), optional pre-activation aux output, optional
 //                    bf16 addend `res` (a fan-out's other gradient: the
 //                    autograd add kernel folded into the dgrad), bf16 store;
 //   kEpiAccumF32  -- C(fp32) += acc  (weight gradients straight into main_grad);
-//   kEpiStoreF32  -- fp32 store.
+//   kEpiStoreF32  -- fp32 store (first write of a step, split-K partials).
 #include <algorithm>
 #include <cstdlib>
 
