@@ -830,6 +830,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);
   m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 ping-pong except wgrad (default)");
   m.def("gemm_get_schedule", &gemm_get_schedule);
+  m.def("gemm_set_rounds", &gemm_set_rounds, "1: launch multi-round GEMM grids one round of tiles at a time (default)");
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none());

@@ -370,6 +370,7 @@ struct EpiParams {
   int N;
   float p, pscale;
   uint32_t threshold;
+  int mask_row0, mask_col0, mask_ld;  // launch chunk -> full-matrix mask coordinates
 };
 
 // Register-phase bf16 epilogue of accumulator row block i (16 rows x 16 NJ
@@ -399,7 +400,7 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
     const float b = bias[j];
     uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     if (ep.p > 0.f) {
-      const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)ep.N + (uint64_t)col;
+      const uint64_t sub = (uint64_t)((row0 + ep.mask_row0) >> 2) * (uint64_t)ep.mask_ld + (uint64_t)(col + ep.mask_col0);
       const uint4 w = Philox(ep.seed, sub, ep.offset).next4();
       ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
     }
@@ -658,7 +659,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   if (EPI == kEpiStoreBf16 && (EXTRA || ACT != kActNone || g.bias != nullptr)) {
     const int ncol = n0 + wn * WN + col_in, nrow = m0 + wm * 128 + 4 * quad;
     const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
-    const EpiParams ep{g.seed, g.offset, g.N, g.p, pscale, g.threshold};
+    const EpiParams ep{g.seed, g.offset, g.N, g.p, pscale, g.threshold, g.mask_row0, g.mask_col0,
+                       g.mask_ld > 0 ? g.mask_ld : g.N};
     float bias[NJ];  // the lane's NJ columns: loaded once, all in flight together
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -706,6 +708,7 @@ bool use_big(const GemmArgs& g) {
 // idle, or 256 256x128 tiles (1.2x faster, profiles/gemm_vs_hipblaslt.txt).
 // gemm_set_width(128 / 256) or MIPIPE_GEMM_W forces one (A/B, tests).
 int g_gemm_width = -1;  // -1: not read from the environment yet, 0: auto
+int g_gemm_rounds = -1;  // MIPIPE_GEMM_ROUNDS=0: multi-round grids in one launch (A/B); -1 unread
 
 int big_width(const GemmArgs& g) {
   if (g_gemm_width < 0) {
@@ -824,6 +827,7 @@ void launch_act(const GemmArgs& g, hipStream_t s) {
 
 void gemm_set_schedule(int mode) { big::g_gemm_sched = mode; }
 void gemm_set_width(int w) { g_gemm_width = w; }
+void gemm_set_rounds(int on) { g_gemm_rounds = on; }
 int gemm_get_schedule() { return big::g_gemm_sched; }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
@@ -869,6 +873,59 @@ int gemm_splitk_factor(const GemmArgs& g) {
   return best;
 }
 
+// Multi-round grids are launched one round at a time: a 4096 x 12288 x 4096
+// GEMM (768 256x256 tiles, 3 rounds of the 256 CUs) ran 345 us as one launch
+// and 322 us as three launches of 4096 columns, hipBLASLt's time; the LM head
+// (113 column tiles) 837 -> 778 us (tools/gemm_rounds_probe.py).  The grid is
+// cut along its longer tile dimension into chunks of floor(256 / other) tiles.
+
+static const char* byte_off(const void* p, int64_t bytes) {
+  return p == nullptr ? nullptr : reinterpret_cast<const char*>(p) + bytes;
+}
+
+template <typename F>
+bool launch_by_rounds(const GemmArgs& g, F&& run) {
+  if (g_gemm_rounds < 0) {
+    const char* e = getenv("MIPIPE_GEMM_ROUNDS");
+    g_gemm_rounds = e ? atoi(e) : 1;
+  }
+  if (g_gemm_rounds == 0 || g.k_splits > 1 || !use_big(g) || big_width(g) != 256) return false;
+  const int tm = (g.M + 255) / 256, tn = (g.N + 255) / 256;
+  if (tm * tn <= 256) return false;
+  const bool along_n = tn >= tm;
+  const int other = along_n ? tm : tn, along = along_n ? tn : tm;
+  const int per = 256 / other;  // tiles of the split dimension per launch
+  if (per < 1 || (along + per - 1) / per > 16) return false;
+  const int cbytes = g.epi == kEpiStoreBf16 ? 2 : 4;
+  for (int t0 = 0; t0 < along; t0 += per) {
+    GemmArgs c = g;
+    const int lo = t0 * 256, hi = std::min((t0 + per) * 256, along_n ? g.N : g.M);
+    c.mask_ld = g.mask_ld > 0 ? g.mask_ld : g.N;
+    if (along_n) {
+      c.N = hi - lo;
+      c.mask_col0 = g.mask_col0 + lo;
+      const int64_t boff = (g.b_kc ? (int64_t)lo * g.ldb : (int64_t)lo) * 2;
+      c.B = byte_off(g.B, boff);
+      for (int i = 0; i < GemmArgs::kMaxSegs; ++i) c.b_seg[i] = byte_off(g.b_seg[i], boff);
+      c.C = const_cast<char*>(byte_off(g.C, (int64_t)lo * cbytes));
+      c.bias = byte_off(g.bias, (int64_t)lo * 2);
+      c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * 2));
+      c.res = byte_off(g.res, (int64_t)lo * 2);
+    } else {
+      c.M = hi - lo;
+      c.mask_row0 = g.mask_row0 + lo;
+      const int64_t aoff = (g.a_kc ? (int64_t)lo * g.lda : (int64_t)lo) * 2;
+      c.A = byte_off(g.A, aoff);
+      for (int i = 0; i < GemmArgs::kMaxSegs; ++i) c.a_seg[i] = byte_off(g.a_seg[i], aoff);
+      c.C = const_cast<char*>(byte_off(g.C, (int64_t)lo * g.ldc * cbytes));
+      c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * g.ldc * 2));
+      c.res = byte_off(g.res, (int64_t)lo * g.ldc * 2);
+    }
+    run(c);
+  }
+  return true;
+}
+
 void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
   GemmArgs g = gi;
   g.threshold = dropout_threshold(g.p);
@@ -895,22 +952,25 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
     }
     return;
   }
-  if (g.epi == kEpiStoreBf16) {
-    if (g.a_kc && g.b_kc) launch_act<true, true, kEpiStoreBf16>(g, s);
-    else if (g.a_kc && !g.b_kc) launch_act<true, false, kEpiStoreBf16>(g, s);
-    else if (!g.a_kc && !g.b_kc) launch_act<false, false, kEpiStoreBf16>(g, s);
-    else launch_act<false, true, kEpiStoreBf16>(g, s);
-  } else if (g.epi == kEpiAccumF32) {
-    if (g.a_kc && g.b_kc) launch<true, true, kEpiAccumF32, kActNone>(g, s);
-    else if (g.a_kc && !g.b_kc) launch<true, false, kEpiAccumF32, kActNone>(g, s);
-    else if (!g.a_kc && !g.b_kc) launch<false, false, kEpiAccumF32, kActNone>(g, s);
-    else launch<false, true, kEpiAccumF32, kActNone>(g, s);
-  } else {
-    if (g.a_kc && g.b_kc) launch<true, true, kEpiStoreF32, kActNone>(g, s);
-    else if (g.a_kc && !g.b_kc) launch<true, false, kEpiStoreF32, kActNone>(g, s);
-    else if (!g.a_kc && !g.b_kc) launch<false, false, kEpiStoreF32, kActNone>(g, s);
-    else launch<false, true, kEpiStoreF32, kActNone>(g, s);
-  }
+  auto dispatch = [s](const GemmArgs& g) {
+    if (g.epi == kEpiStoreBf16) {
+      if (g.a_kc && g.b_kc) launch_act<true, true, kEpiStoreBf16>(g, s);
+      else if (g.a_kc && !g.b_kc) launch_act<true, false, kEpiStoreBf16>(g, s);
+      else if (!g.a_kc && !g.b_kc) launch_act<false, false, kEpiStoreBf16>(g, s);
+      else launch_act<false, true, kEpiStoreBf16>(g, s);
+    } else if (g.epi == kEpiAccumF32) {
+      if (g.a_kc && g.b_kc) launch<true, true, kEpiAccumF32, kActNone>(g, s);
+      else if (g.a_kc && !g.b_kc) launch<true, false, kEpiAccumF32, kActNone>(g, s);
+      else if (!g.a_kc && !g.b_kc) launch<false, false, kEpiAccumF32, kActNone>(g, s);
+      else launch<false, true, kEpiAccumF32, kActNone>(g, s);
+    } else {
+      if (g.a_kc && g.b_kc) launch<true, true, kEpiStoreF32, kActNone>(g, s);
+      else if (g.a_kc && !g.b_kc) launch<true, false, kEpiStoreF32, kActNone>(g, s);
+      else if (!g.a_kc && !g.b_kc) launch<false, false, kEpiStoreF32, kActNone>(g, s);
+      else launch<false, true, kEpiStoreF32, kActNone>(g, s);
+    }
+  };
+  if (!launch_by_rounds(g, dispatch)) dispatch(g);
 }
 
 }  // namespace mipipe

@@ -112,6 +112,10 @@ struct GemmArgs {
   // an fp32 partial into ws [k_splits][M][N]; a reduction adds them (+ res).
   int k_splits = 1;
   float* ws = nullptr;
+  // Launch chunks of a larger GEMM (one round of tiles each): the chunk's
+  // position in the full output, so the dropout mask (Philox counter
+  // (row >> 2) * mask_ld + col) is the full matrix's.  mask_ld = 0: N.
+  int mask_row0 = 0, mask_col0 = 0, mask_ld = 0;
   // K-segmented operands (deferred weight gradients: one GEMM over the
   // micro-batches of a step without concatenating them).  seg_k > 0: K-rows
   // [s*seg_k, (s+1)*seg_k) of A / B live at a_seg[s] / b_seg[s] (leading
@@ -128,7 +132,8 @@ int gemm_splitk_factor(const GemmArgs& g);
 // Main-loop schedule of the 256x256 GEMM: 0 = one barrier per K-tile, 1 = ping-pong wave groups,
 // 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout (default).
 void gemm_set_schedule(int mode);
-void gemm_set_width(int w);  // 256-row GEMM block width: 0 auto, 128, 256
+void gemm_set_width(int w);
+void gemm_set_rounds(int on);  // 1: multi-round grids launched one round at a time (default), 0: one launch  // 256-row GEMM block width: 0 auto, 128, 256
 int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
 // Same interface with fp32 operands (and fp32 bias / res / aux / C): v_mfma_f32_32x32x2_f32.

@@ -426,6 +426,49 @@ def test_wgrad_split_k(k, N, K, T, nseg):
         assert err < 1e-3, (N, K, T, nseg, accumulate, err)
 
 
+def test_gemm_round_launches_identical(k):
+    """Multi-round grids launched one round of tiles at a time give the same bits as one
+    launch -- forward with bias / ReLU / dropout (the mask keeps full-matrix coordinates),
+    GELU with the pre-activation output, dgrad with the residual addend, segmented wgrad
+    (split along M) -- and the unchunked result is right."""
+    torch.manual_seed(12)
+    T, K, N = 2048, 512, 9000  # 8 x 36 tiles: 2 launches along N, the second an edge chunk
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(4096, 1024, device=DEV).to(torch.bfloat16)  # dgrad 4096 x 4608: 16 x 18 tiles
+    w2 = (torch.randn(1024, 4608, device=DEV) / 32).to(torch.bfloat16)
+    r = torch.randn(4096, 4608, device=DEV).to(torch.bfloat16)
+    dys = [torch.randn(256, 8200, device=DEV).to(torch.bfloat16) for _ in range(2)]  # wgrad 8200 x 2048: 33 x 8
+    xs = [torch.randn(256, 2048, device=DEV).to(torch.bfloat16) for _ in range(2)]
+
+    def run():
+        torch.manual_seed(77)
+        y1 = k.linear_fwd(x, w, b, 1, 0.3, False)[0]
+        torch.manual_seed(78)
+        y2, pre, _, _ = k.linear_fwd(x, w, b, 2, 0.0, True)
+        dx = k.linear_dgrad(dy, w2, r)
+        mg = torch.zeros(8200, 2048, device=DEV)
+        k.linear_wgrad_segments(dys, xs, mg, False)
+        return [y1, y2, pre, dx, mg]
+
+    try:
+        k.gemm_set_rounds(0)
+        ref = run()
+        k.gemm_set_rounds(1)
+        got = run()
+    finally:
+        k.gemm_set_rounds(1)
+    for a, bb in zip(got, ref):
+        assert torch.equal(a, bb)
+    want = torch.relu(x.float() @ w.float().t() + b.float())
+    pos = want > 0.05  # clearly positive under bf16 rounding: zero only where dropped
+    kept = (ref[0] != 0) & pos
+    assert abs(kept.float().sum().item() / pos.float().sum().item() - 0.7) < 0.02
+    assert torch.allclose(ref[0].float()[kept], (want / 0.7)[kept], atol=5e-2, rtol=3e-2)
+    assert torch.allclose(ref[3].float(), dy.float() @ w2.float() + r.float(), atol=0.5, rtol=3e-2)
+
+
 def test_linear_op_matches_reference(k):
     from mipipe.ops import linear
 
