@@ -873,11 +873,14 @@ int gemm_splitk_factor(const GemmArgs& g) {
   return best;
 }
 
-// Multi-round grids are launched one round at a time: a 4096 x 12288 x 4096
-// GEMM (768 256x256 tiles, 3 rounds of the 256 CUs) ran 345 us as one launch
-// and 322 us as three launches of 4096 columns, hipBLASLt's time; the LM head
-// (113 column tiles) 837 -> 778 us (tools/gemm_rounds_probe.py).  The grid is
-// cut along its longer tile dimension into chunks of floor(256 / other) tiles.
+// Grids of several rounds whose last round is at most half full are launched
+// one round of tiles at a time: the LM head (4096 x 28928 x 4096, 1808 tiles =
+// 7 rounds + 16 tiles) 812 -> 786 us, 2048 x 12288 x 4096 (384 tiles) 176 ->
+// 167 us (hipBLASLt's time).  Whole rounds (4096 x 12288: 768 tiles, 292 vs
+// 296 us) and a last round over half full (2048 x 28928: 904 tiles, 407 vs
+// 415 us) stay one launch (tools/gemm_rounds_probe.py, warm clocks, arms
+// alternated).  The grid is cut along its longer tile dimension into chunks of
+// floor(256 / other) tiles.
 
 static const char* byte_off(const void* p, int64_t bytes) {
   return p == nullptr ? nullptr : reinterpret_cast<const char*>(p) + bytes;
@@ -891,7 +894,8 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
   }
   if (g_gemm_rounds == 0 || g.k_splits > 1 || !use_big(g) || big_width(g) != 256) return false;
   const int tm = (g.M + 255) / 256, tn = (g.N + 255) / 256;
-  if (tm * tn <= 256) return false;
+  // only when the last round is at most half full (see above)
+  if (tm * tn <= 256 || (tm * tn) % 256 == 0 || (tm * tn) % 256 > 128) return false;
   const bool along_n = tn >= tm;
   const int other = along_n ? tm : tn, along = along_n ? tn : tm;
   const int per = 256 / other;  // tiles of the split dimension per launch
