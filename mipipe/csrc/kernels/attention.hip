@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_fwd_kernel(At
     for (int r = 0; r < 4; ++r) {
       const float mx = row_reduce_max16(tmax[r]);
       const float mn = fmaxf(m[r], mx);
-      alpha[r] = m[r] == -INFINITY ? 0.f : exp2f(m[r] - mn);
+      alpha[r] = m[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[r] - mn);
       m[r] = mn;
     }
     float psum[4] = {0.f, 0.f, 0.f, 0.f};
@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_fwd_kernel(At
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pr = m[r] == -INFINITY ? 0.f : exp2f(sv[j][r] - m[r]);
+        const float pr = m[r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sv[j][r] - m[r]);
         psum[r] += pr;
         sv[j][r] = (a.p > 0.f) ? (w[r] >= a.threshold ? pr * pscale : 0.f) : pr;
       }
@@ -617,7 +617,7 @@ __global__ void __launch_bounds__(kThreads, D == 256 ? 1 : 2) attn_dq_kernel(Att
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pr = exp2f(sacc[j][r] * sl2 - lse2[r]);
+        float pr = __builtin_amdgcn_exp2f(sacc[j][r] * sl2 - lse2[r]);
         if (CAUSAL && key > qrow0 + r) pr = 0.f;
         float dp = pacc[j][r];
         if (a.p > 0.f) dp = w[r] >= a.threshold ? dp * pscale : 0.f;
@@ -879,7 +879,7 @@ __global__ void __launch_bounds__(kThreads, D >= 128 ? 1 : 2) attn_dkdv_kernel(A
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = key0 + r;
-        float pr = exp2f(sacc[j][r] * sl2 - l2);
+        float pr = __builtin_amdgcn_exp2f(sacc[j][r] * sl2 - l2);
         if (CAUSAL && key > q) pr = 0.f;
         float dp = pacc[j][r];
         float pdrop = pr;
@@ -1078,7 +1078,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_bwd_s128_kernel(AttnArgs a) 
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float pr = exp2f(sacc[j][r] * sl2 - lse2[r]);
+      float pr = __builtin_amdgcn_exp2f(sacc[j][r] * sl2 - lse2[r]);
       if (CAUSAL && key > qrow0 + r) pr = 0.f;
       float dp = pacc[j][r];
       float pd = pr;
@@ -1221,7 +1221,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_s128_kernel(AttnArgs a) 
   for (int j = 0; j < 8; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float e = exp2f(sacc[j][r] - mx[r]);
+      const float e = __builtin_amdgcn_exp2f(sacc[j][r] - mx[r]);
       sacc[j][r] = e;
       sum[r] += e;
     }

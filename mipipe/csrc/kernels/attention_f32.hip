@@ -194,11 +194,11 @@ __global__ void __launch_bounds__(kThreads, D <= 64 ? 2 : 1) attn_f32_fwd_kernel
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);  // finite: key 32 kb <= every query of this wave
-      const float alpha = exp2f(m - mnew);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float psum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s[r] = exp2f(s[r] - mnew);
+        s[r] = __builtin_amdgcn_exp2f(s[r] - mnew);
         psum += s[r];
       }
       psum += __shfl_xor(psum, 32, 64);
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dq_kernel(AttnArgs a) {
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pr = exp2f(s[r] - lse2);
+        float pr = __builtin_amdgcn_exp2f(s[r] - lse2);
         if (CAUSAL && 32 * kb + arow(r, h) > q0 + li) pr = 0.f;
         float d = dp[r];
         if (a.p > 0.f) d = ws[r] >= a.threshold ? d * pscale : 0.f;
@@ -391,7 +391,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) 
       for (int r = 0; r < 16; ++r) {
         const int qr = arow(r, h);
         const int qg = 32 * qb + qr;
-        float pr = exp2f(s[r] - ldsL[qr]);
+        float pr = __builtin_amdgcn_exp2f(s[r] - ldsL[qr]);
         if (CAUSAL && k0 + li > qg) pr = 0.f;
         float keep = 1.f;
         if (a.p > 0.f) {

@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
         if (__ballot(mx > m[qb] + kRescale)) {
           // raise the running max; rescale O (queries in registers there) and l
           const float mn = fmaxf(m[qb], mx);
-          const float alpha = m[qb] == -INFINITY ? 0.f : exp2f(m[qb] - mn);
+          const float alpha = m[qb] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[qb] - mn);
           m[qb] = mn;
           l[qb] *= alpha;
 #pragma unroll
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
         float ps = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(fmaf(st[qb][r], sl2, -mq));
+          float p = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -mq));
           ps += p;
           if (drop) p = ((wds[r] >> li) & 1u) ? p * pscale : 0.f;
           st[qb][r] = p;
@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int qr = arow(r, h);
-            float p = exp2f(fmaf(sacc[kb][r], sl2, -lr[r]));
+            float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -lr[r]));
             if (diag && key > qrow + qr) p = 0.f;
             const float keep = drop ? (((word >> qr) & 1u) ? pscale : 0.f) : 1.f;
             const float pd = p * keep;
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
         const bool diag = CAUSAL && kk0 + 31 > qrow;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(fmaf(st[qb][r], sl2, -lse2[qb]));
+          float p = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -lse2[qb]));
           if (diag && kk0 + arow(r, h) > q) p = 0.f;
           float d = dpt[qb][r];
           if (drop) d = ((wds[r] >> li) & 1u) ? d * pscale : 0.f;
