@@ -237,13 +237,14 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
         }
         uint32_t wds[16] = {};
         if (drop) load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
-        const bool diag = CAUSAL && kk0 + 31 > qrow;
+        if (CAUSAL && kk0 + 31 > qrow) {  // diagonal sub-tile (wave-uniform branch): mask keys > query
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kk0 + arow(r, h) > q) st[qb][r] = -INFINITY;
+        }
         float mx = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if (diag && kk0 + arow(r, h) > q) st[qb][r] = -INFINITY;
-          mx = fmaxf(mx, st[qb][r]);
-        }
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[qb][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
         if (__ballot(mx > m[qb] + kRescale)) {
           // raise the running max; rescale O (queries in registers there) and l
@@ -264,7 +265,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
         for (int r = 0; r < 16; ++r) {
           float p = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -mq));
           ps += p;
-          if (drop) p = ((wds[r] >> li) & 1u) ? p * pscale : 0.f;
+          // dropped -> 0; the 1/(1-p) scale is applied once to O at the end
+          if (drop) p = __builtin_amdgcn_ubfe(wds[r], li, 1) ? p : 0.f;
           st[qb][r] = p;
         }
         l[qb] += ps;
@@ -291,7 +293,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const float lt = l[qb] + __shfl_xor(l[qb], 32, 64);
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    const float inv = lt > 0.f ? pscale / lt : 0.f;  // dropout scale folded into the normalisation
     const int qrow = q0w + 32 * qb;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
