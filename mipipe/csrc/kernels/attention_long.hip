@@ -429,7 +429,6 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
           const int key = k0w + 32 * kb + li;
           uint32_t word = 0xFFFFFFFFu;
           if (drop) word = a.dmask[((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + key];
-          const bool diag = CAUSAL && k0w + 32 * kb + 31 > qrow;
           // row constants (lse, delta) of the 16 query rows this lane holds: LDS broadcasts
           float lr[16], dr[16];
 #pragma unroll
@@ -442,15 +441,22 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
               dr[4 * g + j] = dv4[j];
             }
           }
+          float pr[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pr[r] = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -lr[r]));
+          if (CAUSAL && k0w + 32 * kb + 31 > qrow) {  // diagonal sub-tile (wave-uniform branch)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (key > qrow + arow(r, h)) pr[r] = 0.f;
+          }
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int qr = arow(r, h);
-            float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -lr[r]));
-            if (diag && key > qrow + qr) p = 0.f;
-            const float keep = drop ? (((word >> qr) & 1u) ? pscale : 0.f) : 1.f;
-            const float pd = p * keep;
-            sacc[kb][r] = pd;                              // P with dropout (for dV)
-            dpacc[kb][r] = p * (dpacc[kb][r] * keep - dr[r]);  // dS
+            // kept: P (for dV; the 1/(1-p) is applied to dV once at the end) and
+            // dS = P (dP / (1-p) - delta); dropped: P -> 0, dS = -P delta
+            const bool kept = !drop || __builtin_amdgcn_ubfe(word, arow(r, h), 1);
+            const float dsel = kept ? dpacc[kb][r] : 0.f;
+            sacc[kb][r] = kept ? pr[r] : 0.f;
+            dpacc[kb][r] = pr[r] * fmaf(dsel, pscale, -dr[r]);
           }
           pb[kb][0] = pack8(sacc[kb], 0);
           pb[kb][1] = pack8(sacc[kb], 1);
@@ -491,7 +497,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           kv[j] = (__bf16)(dk[kb][dt][4 * g + j] * a.scale);
-          vv[j] = (__bf16)dv[kb][dt][4 * g + j];
+          vv[j] = (__bf16)(dv[kb][dt][4 * g + j] * pscale);  // dropout scale of P, folded here
         }
         *reinterpret_cast<bf16x4*>(dK + d0) = kv;
         *reinterpret_cast<bf16x4*>(dV + d0) = vv;
@@ -586,14 +592,18 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
         }
         uint32_t wds[16] = {};
         if (drop) load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
-        const bool diag = CAUSAL && kk0 + 31 > qrow;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[qb][r] = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -lse2[qb]));
+        if (CAUSAL && kk0 + 31 > qrow) {  // diagonal sub-tile (wave-uniform branch)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kk0 + arow(r, h) > q) st[qb][r] = 0.f;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -lse2[qb]));
-          if (diag && kk0 + arow(r, h) > q) p = 0.f;
-          float d = dpt[qb][r];
-          if (drop) d = ((wds[r] >> li) & 1u) ? d * pscale : 0.f;
-          st[qb][r] = p * (d - dlt[qb]);
+          const bool kept = !drop || __builtin_amdgcn_ubfe(wds[r], li, 1);
+          const float d = kept ? dpt[qb][r] : 0.f;
+          st[qb][r] *= fmaf(d, pscale, -dlt[qb]);  // dS = P (dP / (1-p) - delta), dropped: -P delta
         }
         sb[qb][0] = pack8(st[qb], 0);
         sb[qb][1] = pack8(st[qb], 1);
