@@ -334,7 +334,8 @@ __global__ void __launch_bounds__(256) attn_long_delta_kernel(AttnArgs a) {
 // ------------------------------------------------------------------ dK, dV
 template <bool CAUSAL>
 __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 2 * 2 * kTile * 4];  // Q, dO (x2) + lse2, delta (x2)
+  // Q, dO (x2) + lse2, delta (x2) + this workgroup's K and V (one [64][64] image per wave each)
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 2 * 2 * kTile * 4 + 2 * 4 * kImg];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nkt = (a.S + kBlockRows - 1) / kBlockRows;
@@ -353,17 +354,20 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
   const float sl2 = a.scale * kLog2e;
   (void)nkt;
 
-  // K^T and V^T fragments (B operands of S = Q K^T and dP = dO V^T): key k0w + 32 kb + li
-  bf16x8 kf[2][4], vf[2][4];
+  // This wave's 64 keys of K and V as LDS images (row = key): the B operands of
+  // S = Q K^T and dP = dO V^T are read from there per use rather than held in 64
+  // registers for the whole kernel -- the register file then holds dK/dV in the
+  // accumulator registers without copies between the two register files.
+  char* kimg_w = lds + 4 * kImg + 4 * kTile * 4 + wave * 2 * kImg;
+  char* vimg_w = kimg_w + kImg;
+  {
+    const int key = min(k0w + lane, a.S - 1);
+    const bf16_t* kr = reinterpret_cast<const bf16_t*>(a.k) + hoff + (int64_t)key * a.ld_qkv;
+    const bf16_t* vr = reinterpret_cast<const bf16_t*>(a.v) + hoff + (int64_t)key * a.ld_qkv;
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int key = min(k0w + 32 * kb + li, a.S - 1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[kb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.k) + hoff +
-                                                   (int64_t)key * a.ld_qkv + 16 * s + 8 * h);
-      vf[kb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.v) + hoff +
-                                                   (int64_t)key * a.ld_qkv + 16 * s + 8 * h);
+    for (int c = 0; c < 8; ++c) {
+      *reinterpret_cast<u32x4*>(kimg_w + ioff(lane, c)) = *reinterpret_cast<const u32x4*>(kr + 8 * c);
+      *reinterpret_cast<u32x4*>(vimg_w + ioff(lane, c)) = *reinterpret_cast<const u32x4*>(vr + 8 * c);
     }
   }
   f32x16 dk[2][2], dv[2][2];  // [kb][dt]: rows d, columns keys
@@ -398,7 +402,17 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
     lstore(0);
   }
   __syncthreads();
-  for (int t = qstart; t < ntiles; ++t) {
+  // Tiles wholly before this wave's keys (causal; all of them for an inactive
+  // wave) are only staged for the others.  Splitting them into their own loop
+  // leaves the compute loop without a branch around the dK/dV accumulation, so
+  // those accumulators stay in the accumulator registers across iterations.
+  const int tw = !active ? ntiles : (CAUSAL ? max(qstart, k0w / kTile) : qstart);
+  for (int t = qstart; t < tw; ++t) {
+    gload(min(t + 1, ntiles - 1));
+    lstore(((t - qstart) & 1) ^ 1);
+    __syncthreads();
+  }
+  for (int t = tw; t < ntiles; ++t) {
     const int buf = (t - qstart) & 1;
     const char* qimg = lds + buf * 2 * kImg;
     const char* oimg = qimg + kImg;
@@ -406,11 +420,11 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
     const float* dlt = lse2 + kTile;
     const int q0 = t * kTile;
     gload(min(t + 1, ntiles - 1));
-    if (active && !(CAUSAL && q0 + kTile - 1 < k0w)) {
+    {
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
+        // q0 >= k0w here (both multiples of 64): no query block of the tile lies wholly before the keys
         const int qrow = q0 + 32 * qb;
-        if (CAUSAL && qrow + 31 < k0w) continue;  // every query of the block precedes every key
         f32x16 sacc[2], dpacc[2];
         sacc[0] = sacc[1] = dpacc[0] = dpacc[1] = zero16();
 #pragma unroll
@@ -419,8 +433,8 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
           const bf16x8 oa = row_frag(oimg, 32 * qb + li, s, h);
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
-            sacc[kb] = mfma(qa, kf[kb][s], sacc[kb]);
-            dpacc[kb] = mfma(oa, vf[kb][s], dpacc[kb]);
+            sacc[kb] = mfma(qa, row_frag(kimg_w, 32 * kb + li, s, h), sacc[kb]);
+            dpacc[kb] = mfma(oa, row_frag(vimg_w, 32 * kb + li, s, h), dpacc[kb]);
           }
         }
         bf16x8 pb[2][2], sb[2][2];  // [kb][step]
@@ -453,7 +467,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
           for (int r = 0; r < 16; ++r) {
             // kept: P (for dV; the 1/(1-p) is applied to dV once at the end) and
             // dS = P (dP / (1-p) - delta); dropped: P -> 0, dS = -P delta
-            const bool kept = !drop || __builtin_amdgcn_ubfe(word, arow(r, h), 1);
+            const bool kept = __builtin_amdgcn_ubfe(word, arow(r, h), 1);  // all ones without dropout
             const float dsel = kept ? dpacc[kb][r] : 0.f;
             sacc[kb][r] = kept ? pr[r] : 0.f;
             dpacc[kb][r] = pr[r] * fmaf(dsel, pscale, -dr[r]);
