@@ -32,8 +32,8 @@
 // occupancy: the RNG no longer competes with the softmax for issue slots in
 // the MFMA kernels) and stored as one 32-bit word per (head, 32-query block,
 // key), bit = query % 32.  Philox4x32-10 with 16-bit uniforms: the uniform of
-// (q, key) of head bh is 16-bit half (q & 1) of word (q >> 1) & 3 of the block
-// for counter (((bh * S/32 + q/32) * S + key) * 4 + (q >> 3) & 3).  Forward,
+// (q, key) of head bh is the signed 16-bit half (q % 32) / 16 of word q % 4 of
+// the block for counter ((bh * S/32 + q/32) * S + key) * 4 + (q % 16) / 4.  Forward,
 // dQ and dK/dV read the bits; checkpoint recompute regenerates them.
 #include "common.h"
 #include "kernels.h"
@@ -132,6 +132,15 @@ __device__ __forceinline__ float bperm(float v, int src_lane) {
 // One thread per (head, 32-query block, key) word; causal: only words with a
 // query >= the key somewhere in the block.  Grid (S / 256, S / 32, B * H): no
 // 64-bit division in the index math.
+//
+// The 32 uniforms of a word are the 16-bit halves of the 16 words r_j of four
+// Philox blocks (counter 4 idx + j/4, word j%4), read as SIGNED 16-bit s: query
+// bit q takes half q/16 of r_{q%16} and is dropped iff s < t - 2^15 (the same
+// probability t / 2^16 as unsigned u < t).  One saturating v_pk_sub_i16 per r_j
+// puts both drop flags in its sign bits 15 and 31, a rotate by 15 - j moves them
+// to bits j and 16 + j, and one v_bitop3 merges them: 3 instructions per 2 bits.
+typedef __attribute__((ext_vector_type(2))) short s16x2;
+
 template <bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
   const int key = blockIdx.x * 256 + threadIdx.x;
@@ -139,19 +148,22 @@ __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
   if (CAUSAL && (int)blockIdx.x * 256 > 32 * qblk + 31) return;  // whole block above the diagonal
   if (key >= a.S || (CAUSAL && key > 32 * qblk + 31)) return;
   const int64_t idx = ((int64_t)blockIdx.z * gridDim.y + qblk) * a.S + key;
-  const uint32_t t16 = a.threshold >> 16;
-  uint32_t word = 0;
+  const short ts = (short)((int)(a.threshold >> 16) - 32768);
+  const s16x2 t2 = {ts, ts};
+  uint32_t dropped = 0;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const uint4 w = Philox(a.seed, (uint64_t)idx * 4 + (uint64_t)c, a.offset).next4();
     const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      word |= (uint32_t)((ws[i] & 0xFFFFu) >= t16) << (8 * c + 2 * i);
-      word |= (uint32_t)((ws[i] >> 16) >= t16) << (8 * c + 2 * i + 1);
+      const int j = 4 * c + i;
+      const uint32_t d = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, ws[i]), t2));
+      const uint32_t rot = __builtin_amdgcn_alignbit(d, d, 15 - j);  // rotate right: bit 15 -> j, bit 31 -> 16 + j
+      dropped |= rot & ((1u << j) | (1u << (16 + j)));
     }
   }
-  a.dmask[idx] = word;
+  a.dmask[idx] = ~dropped;
 }
 
 // ------------------------------------------------------------------ forward

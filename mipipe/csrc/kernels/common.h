@@ -128,9 +128,9 @@ struct Philox {
       const uint64_t p1 = (uint64_t)0xCD9E8D57u * x2;
       const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
       const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-      x0 = hi1 ^ x1 ^ a;
+      x0 = __builtin_amdgcn_bitop3_b32(hi1, x1, a, 0x96);  // hi1 ^ x1 ^ a in one v_bitop3_b32 (0x96 = xor3)
       x1 = lo1;
-      x2 = hi0 ^ x3 ^ b;
+      x2 = __builtin_amdgcn_bitop3_b32(hi0, x3, b, 0x96);
       x3 = lo0;
       a += 0x9E3779B9u;
       b += 0xBB67AE85u;

@@ -646,23 +646,25 @@ def _attn_keep_mask(B, H, S, p, seed, offset):
 
 def _long_keep_mask(B, H, S, p, seed, offset):
     """Dropout mask of the long-sequence kernels (attention_long.hip): the uniform of
-    (q, key) of head bh is 16-bit half (q & 1) of word (q >> 1) & 3 of Philox counter
-    ((bh * S/32 + q/32) * S + key) * 4 + (q >> 3) & 3."""
+    (q, key) of head bh is the SIGNED 16-bit half (q % 32) // 16 of word q % 4 of
+    Philox counter ((bh * S/32 + q/32) * S + key) * 4 + (q % 16) // 4, kept iff it is
+    >= (p * 2^32 >> 16) - 2^15."""
     import numpy as np
 
     bh, q, key = np.meshgrid(np.arange(B * H), np.arange(S), np.arange(S), indexing="ij")
     qq = q % 32
     sub = ((bh.astype(np.uint64) * np.uint64(S // 32) + (q // 32).astype(np.uint64)) * np.uint64(S)
-           + key.astype(np.uint64)) * np.uint64(4) + (qq >> 3).astype(np.uint64)
+           + key.astype(np.uint64)) * np.uint64(4) + ((qq % 16) // 4).astype(np.uint64)
     seed &= 0xFFFFFFFFFFFFFFFF
     offset &= 0xFFFFFFFFFFFFFFFF
     m32 = np.uint64(0xFFFFFFFF)
     words = _philox4x32_10(sub & m32, sub >> np.uint64(32), np.uint64(offset) & m32, np.uint64(offset) >> np.uint64(32),
                            seed & 0xFFFFFFFF, seed >> 32)
-    w = np.choose((qq >> 1) & 3, words)
-    u16 = (w >> (np.uint64(16) * (qq & 1).astype(np.uint64))) & np.uint64(0xFFFF)
-    thr = min(int(p * 4294967296.0), 0xFFFFFFFF) >> 16
-    return torch.from_numpy((u16 >= thr).reshape(B, H, S, S))
+    w = np.choose(qq % 4, words)
+    u16 = (w >> (np.uint64(16) * (qq // 16).astype(np.uint64))) & np.uint64(0xFFFF)
+    s16 = u16.astype(np.int64) - (u16 >= np.uint64(0x8000)).astype(np.int64) * 65536
+    thr = (min(int(p * 4294967296.0), 0xFFFFFFFF) >> 16) - 32768
+    return torch.from_numpy((s16 >= thr).reshape(B, H, S, S))
 
 
 def _bits_to_mask(bits, B, H, S):
