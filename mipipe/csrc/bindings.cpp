@@ -825,6 +825,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lse"), py::arg("causal"), py::arg("p"), py::arg("scale"), py::arg("seed"), py::arg("offset"),
         py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none());
   m.def("attention_long_supported", [](int64_t S, int64_t D) { return attention_long_supported((int)S, (int)D); });
+  m.def("attention_long_set_fused_rng", &attention_long_set_fused_rng,
+        "long-sequence attention: make the dropout keep words inside the forward kernel (true, default) or in a "
+        "kernel of their own before it (false)");
   m.def("gemm_supported", &py_gemm_supported);
   m.def("gemm_f32_supported", &py_gemm_f32_supported);
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);

@@ -141,13 +141,8 @@ __device__ __forceinline__ float bperm(float v, int src_lane) {
 // to bits j and 16 + j, and one v_bitop3 merges them: 3 instructions per 2 bits.
 typedef __attribute__((ext_vector_type(2))) short s16x2;
 
-template <bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
-  const int key = blockIdx.x * 256 + threadIdx.x;
-  const int qblk = blockIdx.y;
-  if (CAUSAL && (int)blockIdx.x * 256 > 32 * qblk + 31) return;  // whole block above the diagonal
-  if (key >= a.S || (CAUSAL && key > 32 * qblk + 31)) return;
-  const int64_t idx = ((int64_t)blockIdx.z * gridDim.y + qblk) * a.S + key;
+// Keep word `idx` = (bh * S/32 + query block) * S + key.
+__device__ __forceinline__ uint32_t keep_word(const AttnArgs& a, int64_t idx) {
   const short ts = (short)((int)(a.threshold >> 16) - 32768);
   const s16x2 t2 = {ts, ts};
   uint32_t dropped = 0;
@@ -163,7 +158,18 @@ __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
       dropped |= rot & ((1u << j) | (1u << (16 + j)));
     }
   }
-  a.dmask[idx] = ~dropped;
+  return ~dropped;
+}
+
+// Stand-alone form (attention_long_set_fused_rng(false)): the forward then reads the words.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
+  const int key = blockIdx.x * 256 + threadIdx.x;
+  const int qblk = blockIdx.y;
+  if (CAUSAL && (int)blockIdx.x * 256 > 32 * qblk + 31) return;  // whole block above the diagonal
+  if (key >= a.S || (CAUSAL && key > 32 * qblk + 31)) return;
+  const int64_t idx = ((int64_t)blockIdx.z * gridDim.y + qblk) * a.S + key;
+  a.dmask[idx] = keep_word(a, idx);
 }
 
 // ------------------------------------------------------------------ forward
@@ -171,9 +177,10 @@ __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
 // K fragments), softmax, P V (both share the V fragments).  K/V tiles are
 // double-buffered in LDS and staged through registers one tile ahead: one
 // barrier per tile.
-template <bool CAUSAL>
+template <bool CAUSAL, bool RNG>
 __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg];  // K, V double-buffered
+  // K, V double-buffered + (RNG) one 64-word keep-word exchange slot per wave
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + (RNG ? 4 * 64 * 4 : 0)];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // grid (B*H, query tiles): the query tile is the SLOW grid dimension, so under
@@ -237,6 +244,19 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) st[qb] = mfma(kf, qf[qb][s], st[qb]);
       }
+      uint32_t* wx = reinterpret_cast<uint32_t*>(lds + 4 * kImg) + wave * 64;
+      if (RNG && drop) {
+        // Keep words made here, beside the S MFMAs (pure VALU): lane (h, li) makes
+        // the word of query block q0w/32 + h and key kk0 + li, stores it for the
+        // backward pass and passes it through LDS to the lanes that apply it.
+        const int64_t idx = ((int64_t)bh * (a.S >> 5) + (q0w >> 5) + h) * a.S + kk0 + li;
+        uint32_t w = 0xFFFFFFFFu;
+        if (!(CAUSAL && kk0 > q0w + 32 * h + 31)) {  // words above the diagonal are never read
+          w = keep_word(a, idx);
+          a.dmask[idx] = w;
+        }
+        wx[lane] = w;
+      }
       bf16x8 pf[2][2];  // [qb][k-step]
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
@@ -248,7 +268,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
           continue;
         }
         uint32_t wds[16] = {};
-        if (drop) load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
+        if (drop) {
+          if (RNG) load_keep_words(wx + 32 * qb + 4 * h, wds);
+          else load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
+        }
         if (CAUSAL && kk0 + 31 > qrow) {  // diagonal sub-tile (wave-uniform branch): mask keys > query
 #pragma unroll
           for (int r = 0; r < 16; ++r)
@@ -660,12 +683,18 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
     }
 }
 
+bool g_fused_rng = true;
+
 template <bool CAUSAL>
 void run_fwd(const AttnArgs& a, hipStream_t s) {
+  const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
+  if (a.p > 0.f && g_fused_rng) {
+    hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
+    return;
+  }
   if (a.p > 0.f)
     hipLaunchKernelGGL((attn_long_mask_kernel<CAUSAL>), dim3((a.S + 255) / 256, a.S / 32, a.B * a.H), dim3(256), 0, s, a);
-  const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
-  hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, false>), grid, dim3(kThreads), 0, s, a);
 }
 
 template <bool CAUSAL>
@@ -678,6 +707,8 @@ void run_bwd(const AttnArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+void attention_long_set_fused_rng(bool on) { g_fused_rng = on; }
 
 bool attention_long_supported(int S, int Dh) { return Dh == D && S >= kBlockRows && S % kTile == 0; }
 

@@ -173,6 +173,8 @@ void attention_bwd(const AttnArgs& a, hipStream_t s);
 bool attention_f32_supported(int S, int D);
 // bf16, D == 64, S >= 256, S % 64 == 0 (attention_long.hip): 32x32x16 MFMA, stored dropout bits.
 bool attention_long_supported(int S, int D);
+// Keep words made inside the forward kernel (default) or by their own kernel first.
+void attention_long_set_fused_rng(bool on);
 void attention_long_fwd(const AttnArgs& a, hipStream_t s);
 void attention_long_bwd(const AttnArgs& a, hipStream_t s);
 void attention_f32_fwd(const AttnArgs& a, hipStream_t s);

@@ -745,6 +745,33 @@ def _check_attention_packed(k, D, causal, p, S):
     assert gerr < 3e-2 * max(1.0, gscale), (gerr, gscale)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_long_fused_rng_identical(k, causal):
+    """Keep words made inside the long-sequence forward kernel (default) and by the
+    stand-alone keep-bit kernel are the same words: output, LSE and stored bits match
+    bitwise."""
+    torch.manual_seed(2)
+    B, H, S, D, p = 2, 3, 512, 64, 0.2
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16)
+    q, kk, v = (qkv.select(2, i) for i in range(3))
+    outs = []
+    for fused in (True, False):
+        k.attention_long_set_fused_rng(fused)
+        try:
+            torch.manual_seed(9)
+            outs.append(k.attention_fwd(q, kk, v, causal, p, D ** -0.5))
+        finally:
+            k.attention_long_set_fused_rng(True)
+    (o1, l1, s1, f1, b1), (o2, l2, s2, f2, b2) = outs
+    assert (s1, f1) == (s2, f2)
+    assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    m1, m2 = _bits_to_mask(b1, B, H, S), _bits_to_mask(b2, B, H, S)
+    if causal:
+        tri = torch.ones(S, S, dtype=torch.bool).tril()
+        m1, m2 = m1 & tri, m2 & tri
+    assert torch.equal(m1, m2)
+
+
 @pytest.mark.parametrize("dtype,D", [(torch.bfloat16, 64), (torch.bfloat16, 128), (torch.float32, 64)])
 @pytest.mark.parametrize("S", [37, 100, 200])
 def test_attention_causal_any_length(k, dtype, D, S):
