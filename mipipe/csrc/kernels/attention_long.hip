@@ -124,6 +124,12 @@ __device__ __forceinline__ void load_keep_words(const uint32_t* mw, uint32_t (&w
   }
 }
 
+// x if bit `bit` of `word` is set, else +0: a sign-extended one-bit field is an
+// all-ones / all-zeros mask (v_bfe_i32 + v_and_b32 -- no compare, no select).
+__device__ __forceinline__ float keep_or_zero(float x, uint32_t word, int bit) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(int, x) & __builtin_amdgcn_sbfe((int)word, bit, 1));
+}
+
 __device__ __forceinline__ float bperm(float v, int src_lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, v)));
 }
@@ -177,8 +183,10 @@ __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
 // K fragments), softmax, P V (both share the V fragments).  K/V tiles are
 // double-buffered in LDS and staged through registers one tile ahead: one
 // barrier per tile.
-template <bool CAUSAL, bool RNG>
+// DM: 0 no dropout, 1 keep words read (made by attn_long_mask_kernel), 2 made here.
+template <bool CAUSAL, int DM>
 __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) {
+  constexpr bool RNG = DM == 2;
   // K, V double-buffered + (RNG) one 64-word keep-word exchange slot per wave
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + (RNG ? 4 * 64 * 4 : 0)];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
@@ -194,7 +202,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
   const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + hoff;
   const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + hoff;
   const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + hoff;
-  const bool drop = a.p > 0.f;
+  constexpr bool drop = DM != 0;
   const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
   const float sl2 = a.scale * kLog2e;
 
@@ -301,7 +309,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
           float p = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -mq));
           ps += p;
           // dropped -> 0; the 1/(1-p) scale is applied once to O at the end
-          if (drop) p = __builtin_amdgcn_ubfe(wds[r], li, 1) ? p : 0.f;
+          if (drop) p = keep_or_zero(p, wds[r], li);
           st[qb][r] = p;
         }
         l[qb] += ps;
@@ -367,7 +375,7 @@ __global__ void __launch_bounds__(256) attn_long_delta_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------ dK, dV
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a) {
   // Q, dO (x2) + lse2, delta (x2) + this workgroup's K and V (one [64][64] image per wave each)
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 2 * 2 * kTile * 4 + 2 * 4 * kImg];
@@ -384,7 +392,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
   const int64_t ooff = (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o;
   const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + hoff;
   const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + ooff;
-  const bool drop = a.p > 0.f;
+  constexpr bool drop = DROP;
   const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
   const float sl2 = a.scale * kLog2e;
   (void)nkt;
@@ -502,10 +510,9 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
           for (int r = 0; r < 16; ++r) {
             // kept: P (for dV; the 1/(1-p) is applied to dV once at the end) and
             // dS = P (dP / (1-p) - delta); dropped: P -> 0, dS = -P delta
-            const bool kept = __builtin_amdgcn_ubfe(word, arow(r, h), 1);  // all ones without dropout
-            const float dsel = kept ? dpacc[kb][r] : 0.f;
-            sacc[kb][r] = kept ? pr[r] : 0.f;
-            dpacc[kb][r] = pr[r] * fmaf(dsel, pscale, -dr[r]);
+            const float dsel = drop ? keep_or_zero(dpacc[kb][r], word, arow(r, h)) : dpacc[kb][r];
+            sacc[kb][r] = drop ? keep_or_zero(pr[r], word, arow(r, h)) : pr[r];
+            dpacc[kb][r] = pr[r] * (drop ? fmaf(dsel, pscale, -dr[r]) : dsel - dr[r]);
           }
           pb[kb][0] = pack8(sacc[kb], 0);
           pb[kb][1] = pack8(sacc[kb], 1);
@@ -555,7 +562,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
 }
 
 // ------------------------------------------------------------------ dQ
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg];  // K, V double-buffered
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
@@ -571,7 +578,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
   const int64_t ooff = (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o;
   const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + hoff;
   const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + hoff;
-  const bool drop = a.p > 0.f;
+  constexpr bool drop = DROP;
   const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
   const float sl2 = a.scale * kLog2e;
 
@@ -650,9 +657,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const bool kept = !drop || __builtin_amdgcn_ubfe(wds[r], li, 1);
-          const float d = kept ? dpt[qb][r] : 0.f;
-          st[qb][r] *= fmaf(d, pscale, -dlt[qb]);  // dS = P (dP / (1-p) - delta), dropped: -P delta
+          const float d = drop ? keep_or_zero(dpt[qb][r], wds[r], li) : dpt[qb][r];
+          st[qb][r] *= drop ? fmaf(d, pscale, -dlt[qb]) : d - dlt[qb];  // dS = P (dP / (1-p) - delta), dropped: -P delta
         }
         sb[qb][0] = pack8(st[qb], 0);
         sb[qb][1] = pack8(st[qb], 1);
@@ -688,13 +694,14 @@ bool g_fused_rng = true;
 template <bool CAUSAL>
 void run_fwd(const AttnArgs& a, hipStream_t s) {
   const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
-  if (a.p > 0.f && g_fused_rng) {
-    hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
-    return;
-  }
-  if (a.p > 0.f)
+  if (!(a.p > 0.f)) {
+    hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, 0>), grid, dim3(kThreads), 0, s, a);
+  } else if (g_fused_rng) {
+    hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, 2>), grid, dim3(kThreads), 0, s, a);
+  } else {
     hipLaunchKernelGGL((attn_long_mask_kernel<CAUSAL>), dim3((a.S + 255) / 256, a.S / 32, a.B * a.H), dim3(256), 0, s, a);
-  hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, false>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((attn_long_fwd_kernel<CAUSAL, 1>), grid, dim3(kThreads), 0, s, a);
+  }
 }
 
 template <bool CAUSAL>
@@ -702,8 +709,13 @@ void run_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.S * a.H;
   hipLaunchKernelGGL(attn_long_delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, a);
   const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
-  hipLaunchKernelGGL((attn_long_dkdv_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL>), grid, dim3(kThreads), 0, s, a);
+  if (a.p > 0.f) {
+    hipLaunchKernelGGL((attn_long_dkdv_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((attn_long_dkdv_kernel<CAUSAL, false>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL, false>), grid, dim3(kThreads), 0, s, a);
+  }
 }
 
 }  // namespace
