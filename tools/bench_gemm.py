@@ -1,7 +1,7 @@
 """Interleaved GEMM timing: mipipe MFMA kernel vs hipBLASLt (torch.matmul), one process, warm clocks,
 each arm timed twice in the order ours, hipBLASLt, hipBLASLt, ours (the better of each).
 
-    python tools/bench_gemm.py > profiles/gemm_bench.txt
+    python tools/bench_gemm.py [T] [enc12|gpt2xl] > profiles/gemm_bench.txt
 """
 import statistics
 import sys
@@ -37,7 +37,15 @@ def ab(fm, fh):
     return min(m1, m2), min(h1, h2)
 
 
-def main(T=int(sys.argv[1]) if len(sys.argv) > 1 else 4096):
+SHAPES = {
+    "enc12": lambda T: [("qkv fwd", T, 12288, 4096), ("out fwd", T, 4096, 4096), ("ffn fwd", T, 4096, 4096),
+                        ("dec fwd", T, 28928, 4096)],
+    "gpt2xl": lambda T: [("qkv fwd", T, 4800, 1600), ("out fwd", T, 1600, 1600), ("fc1 fwd", T, 6400, 1600),
+                         ("fc2 fwd", T, 1600, 6400)],
+}
+
+
+def main(T=int(sys.argv[1]) if len(sys.argv) > 1 else 4096, model=sys.argv[2] if len(sys.argv) > 2 else "enc12"):
     # clocks up before anything is timed: the first timings of a process read slow
     # (4096 x 12288 x 4096: ~357 us cold vs ~289 us warm)
     xw = torch.randn(4096, 4096, device=dev).to(torch.bfloat16)
@@ -45,8 +53,7 @@ def main(T=int(sys.argv[1]) if len(sys.argv) > 1 else 4096):
         k.linear_fwd(xw, xw, None, 0, 0.0, False)
     torch.cuda.synchronize()
 
-    shapes = [("qkv fwd", T, 12288, 4096), ("out fwd", T, 4096, 4096), ("ffn fwd", T, 4096, 4096),
-              ("dec fwd", T, 28928, 4096)]
+    shapes = SHAPES[model](T)
     print(f"{'case':12s} {'M':>6s} {'N':>6s} {'K':>6s} | {'mipipe ms':>9s} {'TF/s':>7s} | {'hipBLASLt ms':>12s} {'TF/s':>7s}")
     for name, M, N, K in shapes:
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
