@@ -257,12 +257,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
         // Keep words made here, beside the S MFMAs (pure VALU): lane (h, li) makes
         // the word of query block q0w/32 + h and key kk0 + li, stores it for the
         // backward pass and passes it through LDS to the lanes that apply it.
+        // made unconditionally (no branch between them and the MFMAs); words above
+        // the diagonal are neither stored nor read
         const int64_t idx = ((int64_t)bh * (a.S >> 5) + (q0w >> 5) + h) * a.S + kk0 + li;
-        uint32_t w = 0xFFFFFFFFu;
-        if (!(CAUSAL && kk0 > q0w + 32 * h + 31)) {  // words above the diagonal are never read
-          w = keep_word(a, idx);
-          a.dmask[idx] = w;
-        }
+        const uint32_t w = keep_word(a, idx);
+        if (!(CAUSAL && kk0 > q0w + 32 * h + 31)) a.dmask[idx] = w;
         wx[lane] = w;
       }
       bf16x8 pf[2][2];  // [qb][k-step]
