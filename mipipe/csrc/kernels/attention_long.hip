@@ -187,8 +187,8 @@ __global__ void __launch_bounds__(256) attn_long_mask_kernel(AttnArgs a) {
 template <bool CAUSAL, int DM>
 __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) {
   constexpr bool RNG = DM == 2;
-  // K, V double-buffered + (RNG) one 64-word keep-word exchange slot per wave
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + (RNG ? 4 * 64 * 4 : 0)];
+  // K, V double-buffered + each wave's Q image + (RNG) one 128-word keep-word exchange slot per wave
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 4 * kImg + (RNG ? 4 * 128 * 4 : 0)];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // grid (B*H, query tiles): the query tile is the SLOW grid dimension, so under
@@ -207,12 +207,14 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
   const float sl2 = a.scale * kLog2e;
 
   // Q^T fragments (B operand of S^T = K Q^T): query q0w + 32 qb + li, d = 16 s + 8 h + j
-  bf16x8 qf[2][4];
+  // as an LDS image of the wave's 64 queries (row = 32 qb + li), read per use: the
+  // 32 registers the fragments would hold for the whole kernel go to the S tiles of
+  // both key sub-tiles instead
+  char* qimg_w = lds + 4 * kImg + wave * kImg;
+  {
+    const bf16_t* qr = Q + (int64_t)min(q0w + lane, a.S - 1) * a.ld_qkv;
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = min(q0w + 32 * qb + li, a.S - 1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[qb][s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)q * a.ld_qkv + 16 * s + 8 * h);
+    for (int c = 0; c < 8; ++c) *reinterpret_cast<u32x4*>(qimg_w + ioff(lane, c)) = *reinterpret_cast<const u32x4*>(qr + 8 * c);
   }
   f32x16 o[2][2];
   float m[2], l[2];
@@ -241,89 +243,100 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_fwd_kernel(AttnArgs a) 
       sk.load(K, a.ld_qkv, tn, tid);
       sv.load(V, a.ld_qkv, tn, tid);
     }
+    if (active && !(CAUSAL && k0 > q0w)) {  // wave-uniform: the tile meets this wave's queries
+      const bool diag = CAUSAL && k0 == q0w;  // this wave's diagonal tile (k0, q0w multiples of 64)
+      // S^T of both 32-key sub-tiles first: the second one's MFMAs run under the first
+      // one's softmax, the first one's P V MFMAs under the second one's softmax
+      f32x16 st[2][2];  // [kb][qb]: rows keys, columns queries
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int kk0 = k0 + 32 * kb;
-      if (!active || (CAUSAL && kk0 > q0w + kWaveRows - 1)) continue;  // wave-uniform
-      f32x16 st[2] = {zero16(), zero16()};  // [qb]: rows keys, columns queries
+      for (int kb = 0; kb < 2; ++kb) {
+        st[kb][0] = st[kb][1] = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = row_frag(kimg, 32 * kb + li, s, h);
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = row_frag(kimg, 32 * kb + li, s, h);
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) st[qb] = mfma(kf, qf[qb][s], st[qb]);
+          for (int qb = 0; qb < 2; ++qb) st[kb][qb] = mfma(kf, row_frag(qimg_w, 32 * qb + li, s, h), st[kb][qb]);
+        }
       }
-      uint32_t* wx = reinterpret_cast<uint32_t*>(lds + 4 * kImg) + wave * 64;
-      if (RNG && drop) {
-        // Keep words made here, beside the S MFMAs (pure VALU): lane (h, li) makes
-        // the word of query block q0w/32 + h and key kk0 + li, stores it for the
-        // backward pass and passes it through LDS to the lanes that apply it.
-        // made unconditionally (no branch between them and the MFMAs); words above
-        // the diagonal are neither stored nor read
-        const int64_t idx = ((int64_t)bh * (a.S >> 5) + (q0w >> 5) + h) * a.S + kk0 + li;
-        const uint32_t w = keep_word(a, idx);
-        if (!(CAUSAL && kk0 > q0w + 32 * h + 31)) a.dmask[idx] = w;
-        wx[lane] = w;
+      uint32_t* wx = reinterpret_cast<uint32_t*>(lds + 8 * kImg) + wave * 128;
+      if (RNG) {
+        // Keep words made here, beside the S MFMAs (pure VALU, no branch between them):
+        // lane (h, li) makes the word of query block q0w/32 + h and key kk0 + li, stores
+        // it for the backward pass and passes it through LDS to the lanes that apply it.
+        // Words above the diagonal are made but neither stored nor read.
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int kk0 = k0 + 32 * kb;
+          const int64_t idx = ((int64_t)bh * (a.S >> 5) + (q0w >> 5) + h) * a.S + kk0 + li;
+          const uint32_t w = keep_word(a, idx);
+          if (!(CAUSAL && kk0 > q0w + 32 * h + 31)) a.dmask[idx] = w;
+          wx[64 * kb + lane] = w;
+        }
       }
-      bf16x8 pf[2][2];  // [qb][k-step]
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        const int qrow = q0w + 32 * qb;  // block's first query
-        const int q = qrow + li;
-        if (CAUSAL && kk0 > qrow + 31) {  // wholly above this block's diagonal: P = 0
-          pf[qb][0] = bf16x8{};
-          pf[qb][1] = bf16x8{};
-          continue;
-        }
-        uint32_t wds[16] = {};
-        if (drop) {
-          if (RNG) load_keep_words(wx + 32 * qb + 4 * h, wds);
-          else load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
-        }
-        if (CAUSAL && kk0 + 31 > qrow) {  // diagonal sub-tile (wave-uniform branch): mask keys > query
+      for (int kb = 0; kb < 2; ++kb) {
+        const int kk0 = k0 + 32 * kb;
+        bf16x8 pf[2][2];  // [qb][k-step]
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kk0 + arow(r, h) > q) st[qb][r] = -INFINITY;
-        }
-        float mx = -INFINITY;
+        for (int qb = 0; qb < 2; ++qb) {
+          const int qrow = q0w + 32 * qb;  // block's first query
+          const int q = qrow + li;
+          if (diag && kb > qb) {  // wholly above this block's diagonal: P = 0
+            pf[qb][0] = bf16x8{};
+            pf[qb][1] = bf16x8{};
+            continue;
+          }
+          uint32_t wds[16] = {};
+          if (drop) {
+            if (RNG) load_keep_words(wx + 64 * kb + 32 * qb + 4 * h, wds);
+            else load_keep_words(a.dmask + ((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + kk0 + 4 * h, wds);
+          }
+          if (diag && kb == qb) {  // diagonal sub-tile (wave-uniform branch): mask keys > query
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[qb][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-        if (__ballot(mx > m[qb] + kRescale)) {
-          // raise the running max; rescale O (queries in registers there) and l
-          const float mn = fmaxf(m[qb], mx);
-          const float alpha = m[qb] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[qb] - mn);
-          m[qb] = mn;
-          l[qb] *= alpha;
+            for (int r = 0; r < 16; ++r)
+              if (kk0 + arow(r, h) > q) st[kb][qb][r] = -INFINITY;
+          }
+          float mx = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb][qb][r]);
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+          if (__ballot(mx > m[qb] + kRescale)) {
+            // raise the running max; rescale O (queries in registers there) and l
+            const float mn = fmaxf(m[qb], mx);
+            const float alpha = m[qb] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[qb] - mn);
+            m[qb] = mn;
+            l[qb] *= alpha;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float ar = bperm(alpha, arow(r, h));
+              o[qb][0][r] *= ar;
+              o[qb][1][r] *= ar;
+            }
+          }
+          const float mq = m[qb];
+          float ps = 0.f;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float ar = bperm(alpha, arow(r, h));
-            o[qb][0][r] *= ar;
-            o[qb][1][r] *= ar;
+            float p = __builtin_amdgcn_exp2f(fmaf(st[kb][qb][r], sl2, -mq));
+            ps += p;
+            // dropped -> 0; the 1/(1-p) scale is applied once to O at the end
+            if (drop) p = keep_or_zero(p, wds[r], li);
+            st[kb][qb][r] = p;
           }
+          l[qb] += ps;
+          pf[qb][0] = pack8(st[kb][qb], 0);
+          pf[qb][1] = pack8(st[kb][qb], 1);
         }
-        const float mq = m[qb];
-        float ps = 0.f;
+        // ---- O += P V for this 32-key sub-tile
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = __builtin_amdgcn_exp2f(fmaf(st[qb][r], sl2, -mq));
-          ps += p;
-          // dropped -> 0; the 1/(1-p) scale is applied once to O at the end
-          if (drop) p = keep_or_zero(p, wds[r], li);
-          st[qb][r] = p;
-        }
-        l[qb] += ps;
-        pf[qb][0] = pack8(st[qb], 0);
-        pf[qb][1] = pack8(st[qb], 1);
+        for (int st_ = 0; st_ < 2; ++st_)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const bf16x8 vf = col_frag(vimg, 32 * kb + 16 * st_ + 4 * h, 32 * dt + 16 * ((lane >> 4) & 1), lane);
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) o[qb][dt] = mfma(pf[qb][st_], vf, o[qb][dt]);
+          }
       }
-      // ---- O += P V for this 32-key sub-tile
-#pragma unroll
-      for (int st_ = 0; st_ < 2; ++st_)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16x8 vf = col_frag(vimg, 32 * kb + 16 * st_ + 4 * h, 32 * dt + 16 * ((lane >> 4) & 1), lane);
-#pragma unroll
-          for (int qb = 0; qb < 2; ++qb) o[qb][dt] = mfma(pf[qb][st_], vf, o[qb][dt]);
-        }
     }
     char* nxt = lds + ((t + 1) & 1) * 2 * kImg;
     sk.store(nxt, tid);
