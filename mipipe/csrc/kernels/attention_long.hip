@@ -576,7 +576,8 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
 // ------------------------------------------------------------------ dQ
 template <bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg];  // K, V double-buffered
+  // K, V double-buffered + each wave's dO image
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 4 * kImg];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // grid (B*H, query tiles): the query tile is the SLOW grid dimension, so under
@@ -594,7 +595,16 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
   const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
   const float sl2 = a.scale * kLog2e;
 
-  bf16x8 qf[2][4], of[2][4];
+  // dO of the wave's 64 queries as an LDS image (row = 32 qb + li), read per use
+  // (32 registers fewer than holding the fragments: no scratch)
+  char* oimg_w = lds + 4 * kImg + wave * kImg;
+  {
+    const bf16_t* orow = reinterpret_cast<const bf16_t*>(a.dout) + ooff + (int64_t)min(q0w + lane, a.S - 1) * a.ld_o;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      *reinterpret_cast<u32x4*>(oimg_w + ioff(lane, c)) = *reinterpret_cast<const u32x4*>(orow + 8 * c);
+  }
+  bf16x8 qf[2][4];
   float lse2[2], dlt[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -603,8 +613,6 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
     for (int s = 0; s < 4; ++s) {
       qf[qb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.q) + hoff +
                                                    (int64_t)q * a.ld_qkv + 16 * s + 8 * h);
-      of[qb][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.dout) + ooff +
-                                                   (int64_t)q * a.ld_o + 16 * s + 8 * h);
     }
     lse2[qb] = a.lse[(int64_t)bh * a.S + q] * kLog2e;
     dlt[qb] = a.delta[(int64_t)bh * a.S + q];
@@ -645,7 +653,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
           st[qb] = mfma(kf, qf[qb][s], st[qb]);
-          dpt[qb] = mfma(vfr, of[qb][s], dpt[qb]);
+          dpt[qb] = mfma(vfr, row_frag(oimg_w, 32 * qb + li, s, h), dpt[qb]);
         }
       }
       bf16x8 sb[2][2];  // [qb][k-step]: dS^T as the A operand of dQ += dS K
