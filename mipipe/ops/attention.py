@@ -14,7 +14,9 @@ regenerated from Philox (seed, offset) in backward, so checkpoint recompute
 replays it exactly.  Supported on the GPU path: bf16 with ``S % 64 == 0`` and
 ``D in {64, 128, 256}`` (attention.hip), fp32 with ``S % 32 == 0`` and
 ``D == 64`` (attention_f32.hip, the reference's own precision); the
-CPU path is eager math.  A CAUSAL sequence of any other length (the
+CPU path is eager math.  Any smaller head dim (e.g. 32, 80, 96, 160) runs on
+the kernels zero-padded to the next supported one (the scale stays that of the
+real head dim; the padded columns are sliced off).  A CAUSAL sequence of any other length (the
 reference's ``get_batch`` tail window, /root/reference/main.py:108-113) is
 zero-padded at the end to the next supported length: under the causal mask
 no real query sees a padded key, so the real rows are exact; the padded rows
@@ -23,7 +25,7 @@ are sliced off (and get no gradient).
 from __future__ import annotations
 
 import math
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -129,6 +131,23 @@ def _causal_pad(t: Tensor, S: int, D: int) -> Optional[int]:
     return None
 
 
+def _run_shape(t: Tensor, S: int, D: int, causal: bool) -> Optional[Tuple[int, int]]:
+    """(sequence length, head dim) the kernels run a (S, D) attention at, or None (eager path).
+
+    A head dim the kernels do not tile is zero-padded to the next one they do: the
+    padded features add 0 to every score (the softmax scale stays 1/sqrt(D) of the
+    real head dim) and give output / gradient columns that are sliced off.  A causal
+    sequence of an unsupported length is zero-padded at the end (see the module doc)."""
+    dims = [D] + [d for d in ((64, 128, 256) if t.dtype == torch.bfloat16 else (64,)) if d > D]
+    for dp in dims:
+        if _gpu_ok(t, S, dp):
+            return S, dp
+        sp = _causal_pad(t, S, dp) if causal else None
+        if sp is not None:
+            return sp, dp
+    return None
+
+
 def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, training: bool = True,
                      scale: Optional[float] = None) -> Tensor:
     """``qkv [B, S, 3, H, D]`` -> ``o [B, S, H, D]``."""
@@ -138,10 +157,11 @@ def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, 
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(D)
     if qkv.is_cuda and _gpu_ok(qkv, S, D):
         return _AttentionPacked.apply(qkv.contiguous(), bool(causal), p, scale)
-    sp = _causal_pad(qkv, S, D) if (qkv.is_cuda and causal) else None
-    if sp is not None:
-        padded = torch.cat((qkv, qkv.new_zeros(B, sp - S, 3, H, D)), dim=1)
-        return _AttentionPacked.apply(padded, True, p, scale)[:, :S]
+    run = _run_shape(qkv, S, D, bool(causal)) if qkv.is_cuda else None
+    if run is not None:
+        sp, dp = run
+        padded = F.pad(qkv, (0, dp - D, 0, 0, 0, 0, 0, sp - S))
+        return _AttentionPacked.apply(padded, bool(causal), p, scale)[:, :S, :, :D]
     q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
     if qkv.is_cuda:
         _note_math_path(S, D, qkv.dtype)
@@ -160,12 +180,13 @@ def attention(
         return attention_reference(q, k, v, causal, p, scale)
     S, D = q.shape[2], q.shape[3]
     if not _gpu_ok(q, S, D):
-        sp = _causal_pad(q, S, D) if causal else None
-        if sp is None:
+        run = _run_shape(q, S, D, bool(causal))
+        if run is None:
             _note_math_path(S, D, q.dtype)
             return attention_reference(q, k, v, causal, p, scale)
-        pad = lambda t: torch.cat((t, t.new_zeros(t.shape[0], t.shape[1], sp - S, D)), dim=2)  # noqa: E731
-        return attention(pad(q), pad(k), pad(v), True, dropout_p, training, scale)[:, :, :S]
+        sp, dp = run
+        pad = lambda t: F.pad(t, (0, dp - D, 0, sp - S))  # noqa: E731
+        return attention(pad(q), pad(k), pad(v), causal, dropout_p, training, scale)[:, :, :S, :D]
     qs, ks, vs = (t.transpose(1, 2) for t in (q, k, v))
     if not (qs.stride() == ks.stride() == vs.stride()) or qs.stride(3) != 1:
         qs, ks, vs = (t.contiguous() for t in (qs, ks, vs))

@@ -798,6 +798,35 @@ def test_attention_causal_any_length(k, dtype, D, S):
     assert ((qkv.grad.float() - qf.grad).abs().max() / qf.grad.abs().max()).item() < 5 * tol
 
 
+@pytest.mark.parametrize("dtype,D,S,causal", [(torch.bfloat16, 32, 128, False), (torch.bfloat16, 80, 256, True),
+                                               (torch.bfloat16, 96, 128, False), (torch.bfloat16, 160, 100, True),
+                                               (torch.float32, 32, 128, True), (torch.float32, 48, 64, False)])
+def test_attention_any_head_dim(k, dtype, D, S, causal):
+    """Head dims the kernels do not tile run on them zero-padded to the next tiled one
+    (scale of the real head dim, padded columns sliced off) -- no eager path."""
+    import warnings
+
+    from mipipe.ops import attention, attention_packed, attention_reference
+
+    torch.manual_seed(6)
+    B, H = 2, 3
+    qkv = (torch.randn(B, S, 3, H, D, device=DEV) * 0.5).to(dtype).requires_grad_()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # the eager fallback warns
+        o = attention_packed(qkv, causal=causal, dropout_p=0.0)
+        o2 = attention(*(qkv.detach().select(2, i).transpose(1, 2) for i in range(3)), causal=causal)
+    assert o.shape == (B, S, H, D) and o2.shape == (B, H, S, D)
+    qf = qkv.detach().float().requires_grad_()
+    ref = attention_reference(*(qf.select(2, i).transpose(1, 2) for i in range(3)), causal, 0.0).transpose(1, 2)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert ((o.float() - ref).abs().max() / ref.abs().max()).item() < tol
+    assert ((o2.transpose(1, 2).float() - ref).abs().max() / ref.abs().max()).item() < tol
+    g = torch.randn_like(ref)
+    o.backward(g.to(dtype))
+    ref.backward(g)
+    assert ((qkv.grad.float() - qf.grad).abs().max() / qf.grad.abs().max()).item() < 5 * tol
+
+
 def test_attention_bhsd_api(k):
     from mipipe.ops import attention, attention_reference
 
