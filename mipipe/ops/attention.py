@@ -16,7 +16,9 @@ replays it exactly.  Supported on the GPU path: bf16 with ``S % 64 == 0`` and
 ``D == 64`` (attention_f32.hip, the reference's own precision); the
 CPU path is eager math.  Any smaller head dim (e.g. 32, 80, 96, 160) runs on
 the kernels zero-padded to the next supported one (the scale stays that of the
-real head dim; the padded columns are sliced off).  A CAUSAL sequence of any other length (the
+real head dim; the padded columns are sliced off), and a non-causal sequence of
+an unsupported length runs padded too when its head dim leaves a spare padded
+feature to mask the padded keys with (``_run_shape``).  A CAUSAL sequence of any other length (the
 reference's ``get_batch`` tail window, /root/reference/main.py:108-113) is
 zero-padded at the end to the next supported length: under the causal mask
 no real query sees a padded key, so the real rows are exact; the padded rows
@@ -131,18 +133,26 @@ def _causal_pad(t: Tensor, S: int, D: int) -> Optional[int]:
     return None
 
 
+_KEY_MASK = -32768.0  # exact in bf16; times the query's 1 and any scale >= 2^-4: exp underflows to 0
+
+
 def _run_shape(t: Tensor, S: int, D: int, causal: bool) -> Optional[Tuple[int, int]]:
     """(sequence length, head dim) the kernels run a (S, D) attention at, or None (eager path).
 
-    A head dim the kernels do not tile is zero-padded to the next one they do: the
-    padded features add 0 to every score (the softmax scale stays 1/sqrt(D) of the
-    real head dim) and give output / gradient columns that are sliced off.  A causal
-    sequence of an unsupported length is zero-padded at the end (see the module doc)."""
+    * A head dim the kernels do not tile is zero-padded to the next one they do: the
+      padded features add 0 to every score (the softmax scale stays 1/sqrt(D) of the
+      real head dim) and give output / gradient columns that are sliced off.
+    * A causal sequence of an unsupported length is zero-padded at the end (see the
+      module doc).
+    * A non-causal one too, when a padded feature is free to mask the padded keys:
+      feature D is 1 in every query, 0 in every real key and -32768 in every padded
+      key, so a padded key scores -32768 * scale below any real one and gets weight 0
+      (its V rows are 0 as well)."""
     dims = [D] + [d for d in ((64, 128, 256) if t.dtype == torch.bfloat16 else (64,)) if d > D]
     for dp in dims:
         if _gpu_ok(t, S, dp):
             return S, dp
-        sp = _causal_pad(t, S, dp) if causal else None
+        sp = _causal_pad(t, S, dp) if (causal or dp > D) else None
         if sp is not None:
             return sp, dp
     return None
@@ -161,6 +171,12 @@ def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, 
     if run is not None:
         sp, dp = run
         padded = F.pad(qkv, (0, dp - D, 0, 0, 0, 0, 0, sp - S))
+        if sp != S and not causal:  # mask the padded keys through the spare feature D
+            # [B, S, 3, H, D]: index (b, s, which, h, d) -> q = which 0, k = which 1, sequence dim 1
+            c = torch.zeros_like(padded)
+            c[:, :, 0, :, D] = 1.0
+            c[:, S:, 1, :, D] = _KEY_MASK
+            padded = padded + c
         return _AttentionPacked.apply(padded, bool(causal), p, scale)[:, :S, :, :D]
     q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
     if qkv.is_cuda:
@@ -186,7 +202,13 @@ def attention(
             return attention_reference(q, k, v, causal, p, scale)
         sp, dp = run
         pad = lambda t: F.pad(t, (0, dp - D, 0, sp - S))  # noqa: E731
-        return attention(pad(q), pad(k), pad(v), causal, dropout_p, training, scale)[:, :, :S, :D]
+        qp, kp = pad(q), pad(k)
+        if sp != S and not causal:  # mask the padded keys through the spare feature D ([B, H, S, D])
+            cq, ck = torch.zeros_like(qp), torch.zeros_like(kp)
+            cq[..., D] = 1.0
+            ck[:, :, S:, D] = _KEY_MASK
+            qp, kp = qp + cq, kp + ck
+        return attention(qp, kp, pad(v), causal, dropout_p, training, scale)[:, :, :S, :D]
     qs, ks, vs = (t.transpose(1, 2) for t in (q, k, v))
     if not (qs.stride() == ks.stride() == vs.stride()) or qs.stride(3) != 1:
         qs, ks, vs = (t.contiguous() for t in (qs, ks, vs))

@@ -800,10 +800,14 @@ def test_attention_causal_any_length(k, dtype, D, S):
 
 @pytest.mark.parametrize("dtype,D,S,causal", [(torch.bfloat16, 32, 128, False), (torch.bfloat16, 80, 256, True),
                                                (torch.bfloat16, 96, 128, False), (torch.bfloat16, 160, 100, True),
-                                               (torch.float32, 32, 128, True), (torch.float32, 48, 64, False)])
+                                               (torch.float32, 32, 128, True), (torch.float32, 48, 64, False),
+                                               (torch.bfloat16, 64, 100, False), (torch.bfloat16, 128, 200, False),
+                                               (torch.bfloat16, 80, 37, False), (torch.float32, 32, 50, False)])
 def test_attention_any_head_dim(k, dtype, D, S, causal):
     """Head dims the kernels do not tile run on them zero-padded to the next tiled one
-    (scale of the real head dim, padded columns sliced off) -- no eager path."""
+    (scale of the real head dim, padded columns sliced off); non-causal sequences of
+    other lengths run padded with the padded keys masked through a spare feature --
+    no eager path."""
     import warnings
 
     from mipipe.ops import attention, attention_packed, attention_reference
