@@ -26,6 +26,14 @@ import os
 import sys
 import time
 
+# Before HIP initialises: enough hardware queues that the compute stream and
+# every RCCL communicator stream get one each.  At HIP's default of 4, streams
+# share in-order queues, and a pre-posted RCCL receive (a spinning kernel)
+# holds back the compute kernels queued behind it -- serialising the pipeline,
+# or deadlocking a looping one (profiles/hw_queue_sharing.txt).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import torch
 import torch.distributed as dist
 

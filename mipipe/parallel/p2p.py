@@ -14,13 +14,45 @@ device tensor.  That path is for testing the engine, not for speed.
 """
 from __future__ import annotations
 
+import os
+import warnings
 from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 from torch import Tensor
 
-__all__ = ["P2P", "Channels", "DirectLinks", "exchange_shape"]
+__all__ = ["P2P", "Channels", "DirectLinks", "exchange_shape", "MIN_HW_QUEUES", "check_hw_queues"]
+
+# Hardware queues a pipeline rank wants: the compute stream plus one per RCCL
+# communicator stream (4 channel directions, the grad-norm all-reduce, skip
+# links), each on a queue of its own.
+MIN_HW_QUEUES = 16
+
+
+def check_hw_queues() -> bool:
+    """Warns when HIP will put RCCL streams on shared hardware queues.
+
+    HIP maps streams onto ``GPU_MAX_HW_QUEUES`` in-order hardware queues
+    (default 4).  Two streams on one queue run their kernels in submission
+    order, so a pre-posted receive -- a kernel that spins until the peer's data
+    arrives -- holds back every kernel queued behind it: the pipeline loses its
+    overlap, and a looping pipeline (rank 0 receiving from rank n-1) can
+    deadlock.  ``tools/micro/queue_share*.py`` measure this on the box
+    (``profiles/hw_queue_sharing.txt``).  The variable is read when HIP
+    initialises: set it before the process touches the GPU, as ``bench.py``
+    does."""
+    try:
+        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    except ValueError:
+        q = 4
+    if q < MIN_HW_QUEUES:
+        warnings.warn(f"mipipe: GPU_MAX_HW_QUEUES={q}: RCCL communicator streams may share in-order hardware "
+                      f"queues with the compute stream, and a pre-posted receive then blocks compute (lost overlap "
+                      f"or deadlock); export GPU_MAX_HW_QUEUES={MIN_HW_QUEUES} before the process initialises HIP",
+                      RuntimeWarning, stacklevel=3)
+        return False
+    return True
 
 
 class _HostStagedWork:
@@ -109,6 +141,8 @@ class Channels:
         self.rank = self.ranks.index(me) if me in self.ranks else -1
         self.world = n
         self.host_staged = dist.get_backend() == "gloo"
+        if not self.host_staged and n > 1:
+            check_hw_queues()
         fwd, bwd = {}, {}
         links = range(n) if wrap and n > 1 else range(n - 1)
         for r in links:

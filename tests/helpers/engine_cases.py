@@ -16,6 +16,7 @@ from mipipe.models.long_skip import insert_long_skips
 from mipipe.models.transformer import merge_units
 from mipipe.optim import FlatAdam
 from mipipe.parallel import PipelineEngine, plan_stages
+from mipipe.parallel.p2p import MIN_HW_QUEUES
 from mipipe.parallel.stage import stage_input_shape
 
 # (checkpoint, virtual chunks per rank, vocabulary-split head, cross-stage skips)
@@ -162,6 +163,10 @@ def run_engine_case(mode, world, checkpoint, virtual, split, skips):
     """Spawns ``world`` ranks and checks loss, every gradient and the global
     gradient norm against the single-rank engine."""
     ref_loss, ref, ref_sq = single_rank_reference(mode, checkpoint, split, skips)
+    if mode == "nccl":
+        # the ranks initialise HIP after spawn: give every RCCL stream its own
+        # hardware queue (mipipe.parallel.p2p.check_hw_queues)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()

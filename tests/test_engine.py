@@ -351,3 +351,25 @@ def test_engine_cases_gloo_emulation(world, checkpoint, virtual, split, skips):
     """The cases tests/test_gpu_pipeline.py runs over RCCL on 2 / 4 GPUs, here
     rank-for-rank over gloo on CPU (fp32, exact comparison)."""
     run_engine_case("cpu", world, checkpoint, virtual, split, skips)
+
+
+def test_check_hw_queues_warns_below_minimum(monkeypatch):
+    """RCCL ranks want a hardware queue per stream (profiles/hw_queue_sharing.txt):
+    below MIN_HW_QUEUES the engine's transport warns; bench.py raises the value
+    before HIP initialises."""
+    import warnings
+
+    from mipipe.parallel.p2p import MIN_HW_QUEUES, check_hw_queues
+
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    with pytest.warns(RuntimeWarning, match="GPU_MAX_HW_QUEUES=4"):
+        assert not check_hw_queues()
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    with pytest.warns(RuntimeWarning):
+        assert not check_hw_queues()  # HIP's default is 4
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", str(MIN_HW_QUEUES))
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert check_hw_queues()
+    src = open(os.path.join(os.path.dirname(__file__), "..", "bench.py")).read()
+    assert src.index("GPU_MAX_HW_QUEUES") < src.index("import torch")
