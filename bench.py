@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--watchdog", type=float, default=300.0,
                     help="seconds without pipeline progress before a rank reports its pending transfers and "
                          "exits (0 = off)")
+    ap.add_argument("--dp", type=int, default=1,
+                    help="data-parallel replicas of the pipeline (world = PP x DP; gradients averaged by bucketed "
+                         "RCCL all-reduces overlapped with the deferred weight gradients). Default 1: PP = world")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -121,7 +124,13 @@ def main() -> int:
 
     cfg = _config(args)
     S, E, V = cfg.seq_len, cfg.d_model, cfg.vocab
-    pp = world
+    dp = args.dp
+    if dp < 1 or world % dp:
+        raise SystemExit(f"--dp {dp} does not divide the world size {world}")
+    if dp > 1 and args.skips != "none":
+        raise SystemExit("--skips with --dp > 1 is not supported")
+    pp = world // dp
+    replica, prank = divmod(rank, pp)  # stage prank of pipeline replica `replica`
     if cfg.name == "gpt2_xl":
         # BASELINE config #4: GPT-2-XL PP=8 chunks=8, checkpoint='always'
         m = args.chunks or (8 if pp == 8 else 4 * pp)
@@ -144,19 +153,25 @@ def main() -> int:
     else:
         virtual = int(args.virtual)
         plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1, bwd_ratio=bwd_ratio)
-    torch.manual_seed(1234 + rank)
+    torch.manual_seed(1234 + prank)  # same initial weights in every data-parallel replica
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     from mipipe.models.long_skip import unet_pairs
 
     skip_pairs = unet_pairs(cfg.num_layers) if args.skips == "unet" else []
     stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype, skips=skip_pairs).train()
-              for vs in plan.vstages(rank)]
+              for vs in plan.vstages(prank)]
     params = [p for st_ in stages for p in st_.parameters()]
     n_params_local = sum(p.numel() for p in params)
 
     opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip)
 
-    is_last = rank == world - 1
+    is_last = prank == pp - 1
+    groups = dpg = None
+    if dp > 1:
+        from mipipe.parallel.data_parallel import DataParallelGrads, make_pp_dp_groups
+
+        groups = make_pp_dp_groups(pp, dp, wrap=virtual > 1)
+        dpg = DataParallelGrads(opt, groups.dp_group)
 
     def loss_fn(y, t):
         return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
@@ -165,18 +180,20 @@ def main() -> int:
 
     wd = Watchdog(args.watchdog) if args.watchdog > 0 else None
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
-                            act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)],
+                            act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(prank)],
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device,
-                            skip_shapes={"skip": ((mb, S, E), dtype)}, watchdog=wd)
+                            skip_shapes={"skip": ((mb, S, E), dtype)}, watchdog=wd,
+                            group=groups.channels if groups is not None else None,
+                            grad_divisor=dp)
     # explicit recompute (issued before each gradient wait, as the engine does)
     from mipipe.pipeline import checkpoint_stop_for
     sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
                                     pp, virtual, m, 2.0, deferred_w=0.5,
                                     checkpoint_stop=checkpoint_stop_for(args.checkpoint, m))
 
-    g = torch.Generator(device="cpu").manual_seed(0)
+    g = torch.Generator(device="cpu").manual_seed(replica)  # each data-parallel replica its own shard
     tokens = torch.randint(0, V, (m, mb, S + 1), generator=g)
-    inputs = [tokens[i, :, :S].to(device) for i in range(m)] if rank == 0 else None
+    inputs = [tokens[i, :, :S].to(device) for i in range(m)] if prank == 0 else None
     # every rank gets the targets: the vocabulary-split decoder's head stage needs them too
     targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(m)]
 
@@ -186,11 +203,16 @@ def main() -> int:
 
     def train_step():
         opt.zero_grad()
+        if dpg is not None:
+            dpg.begin()
         st = engine.step(inputs, targets)
+        if dpg is not None:
+            mark("data-parallel gradient all-reduce")
+            dpg.finish()
         mark("grad-norm all-reduce")
         sq = opt.grad_sumsq()
-        if world > 1:
-            dist.all_reduce(sq)
+        if pp > 1:
+            dist.all_reduce(sq, group=groups.pipeline_group if groups is not None else None)
         opt.step(sq)
         return st
 
@@ -256,9 +278,9 @@ def main() -> int:
     armed.__exit__(None, None, None)
     if wd is not None:
         wd.close()
-    tokens_per_step = m * mb * S
+    tokens_per_step = m * mb * S * dp
     value = tokens_per_step / (ms / 1e3)
-    total_params = sum(int(x) for x in _allsum([n_params_local], device, world))
+    total_params = sum(int(x) for x in _allsum([n_params_local], device, world)) // dp  # one replica
     ref_match = matches_reference(cfg, args, m, mb)
     if rank == 0:
         out = {
@@ -280,7 +302,7 @@ def main() -> int:
                          f"dim_feedforward={cfg.dim_feedforward}, dropout={cfg.dropout}, {cfg.activation}, "
                          f"{'pre' if cfg.norm_first else 'post'}-norm) + embedding/decoder V={V}",
                 "params": total_params,
-                "global_batch": m * mb,
+                "global_batch": m * mb * dp,
                 "seq_len": S,
                 "micro_batch": mb,
                 "chunks": m,
@@ -290,7 +312,7 @@ def main() -> int:
                 "vocab_split_decoder": plan.split_decoder,
                 "skips": args.skips if not skip_pairs else f"{args.skips}: {len(skip_pairs)} long residuals, "
                                                            f"{len(engine.skip_routes)} cross-stage",
-                "parallelism": f"pp{world}",
+                "parallelism": f"pp{pp}" + (f"dp{dp}" if dp > 1 else ""),
                 "impl": "engine (one process per GPU, RCCL send/recv)",
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),

@@ -240,24 +240,45 @@ def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
     return g.to(w.dtype)
 
 
+# Objects told when weight gradients become final during a flush (data-parallel
+# gradient buckets start their all-reduce then, overlapping the remaining
+# weight-gradient GEMMs): ``flush_begin(pending)`` with the parameters whose
+# GEMMs are about to be queued, then ``wgrad_done(param)`` after each one.
+_WGRAD_LISTENERS: list = []
+
+
+def add_wgrad_listener(listener) -> None:
+    _WGRAD_LISTENERS.append(listener)
+
+
+def remove_wgrad_listener(listener) -> None:
+    if listener in _WGRAD_LISTENERS:
+        _WGRAD_LISTENERS.remove(listener)
+
+
 def flush_wgrad() -> None:
     """Runs every queued weight-gradient GEMM (accumulating into main_grad)."""
     global _DEFERRED
     if not _DEFERRED:
         return
     queue, _DEFERRED = _DEFERRED, {}
+    listeners = list(_WGRAD_LISTENERS)
+    for li in listeners:
+        li.flush_begin([w for w, _, _ in queue.values()])
     for w, dys, xs in queue.values():
         k = kernels_for(dys[0])
         if xs is None:  # a bias
             k.column_sum_segments(dys, w.main_grad, True)
-            continue
-        T = dys[0].shape[0]
-        uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
-        if uniform and T % 64 == 0:
-            k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
         else:
-            for d, x in zip(dys, xs):
-                k.linear_wgrad(d, x, w.main_grad, _claim(w))
+            T = dys[0].shape[0]
+            uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
+            if uniform and T % 64 == 0:
+                k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
+            else:
+                for d, x in zip(dys, xs):
+                    k.linear_wgrad(d, x, w.main_grad, _claim(w))
+        for li in listeners:
+            li.wgrad_done(w)
 
 
 class deferred_wgrad:

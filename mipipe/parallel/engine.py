@@ -146,6 +146,9 @@ class PipelineEngine:
         sync_debug: synchronise the device after every action (default: the
             ``MIPIPE_SYNC_DEBUG=1`` environment switch) -- the serialised run
             :func:`mipipe.debug.check_engine` compares a scheduled step with.
+        grad_divisor: the backward is seeded with ``loss / (chunks * grad_divisor)``;
+            data-parallel replicas pass their count, so the gradient all-reduce
+            SUM is the mean (:mod:`mipipe.parallel.data_parallel`).
     """
 
     def __init__(
@@ -166,6 +169,7 @@ class PipelineEngine:
         skip_routes: Optional[Dict[str, SkipRoute]] = None,
         watchdog: Union[None, float, Watchdog] = None,
         sync_debug: Optional[bool] = None,
+        grad_divisor: float = 1.0,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
             raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
@@ -188,6 +192,7 @@ class PipelineEngine:
         self.schedule = schedule
         self.measure = measure
         self.defer_wgrad = defer_wgrad
+        self.grad_divisor = float(grad_divisor)
         if schedule == "1f1b" and self.virtual > 1:
             raise ValueError("1f1b supports one chunk per rank")
         if isinstance(watchdog, (int, float)):
@@ -200,6 +205,9 @@ class PipelineEngine:
         self._action = "construction"
         if isinstance(group, Channels):
             self.chan: Optional[Channels] = group
+            if group.world > 1:
+                with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
+                    group.warmup(device or next(mods[0].parameters()).device)
         elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
             self.chan = Channels(ranks, wrap=self.virtual > 1)
@@ -443,7 +451,7 @@ class PipelineEngine:
             if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
                 loss = self._loss(mod, y, targets, i)
                 losses.append(loss.detach())
-                y = loss / m  # backward seeds from the scaled loss
+                y = loss / (m * self.grad_divisor)  # backward seeds from the scaled loss
             if tm:
                 tm[1].record()
                 events.append(("F", tm))
@@ -487,7 +495,7 @@ class PipelineEngine:
                     with torch.enable_grad(), enable_recomputing():
                         y = self._run(mod, x, targets, i, tracker)
                         if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
-                            y = self._loss(mod, y, targets, i) / m
+                            y = self._loss(mod, y, targets, i) / (m * self.grad_divisor)
                 if tracker is not None:
                     skip_out[c][i] = tracker.outgoing
                 if tr:

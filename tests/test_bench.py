@@ -118,3 +118,22 @@ def test_vs_baseline_only_on_reference_config():
     assert not bench.matches_reference(CONFIGS["ref_main"], argparse.Namespace(dtype="bf16", checkpoint="never"), 4, 8)
     assert not bench.matches_reference(CONFIGS["enc12_d4096"], ns, 4, 8)
     assert not bench.matches_reference(CONFIGS["ref_main"], ns, 8, 4)
+
+
+def test_bench_data_parallel_contract():
+    """--dp 2 on 4 ranks: two 2-stage pipeline replicas; the JSON counts both
+    replicas' tokens and names the layout."""
+    args = ["--gpus", "4", "--dp", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--config", "tiny",
+            "--micro-batch", "2"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py")] + args
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp",
+                         env={**os.environ, "CUDA_VISIBLE_DEVICES": ""})
+    assert out.returncode == 0, out.stderr[-3000:]
+    (rec,) = _json_lines(out.stdout)
+    cfg = rec["config"]
+    assert rec["n_gpus"] == 4 and cfg["parallelism"] == "pp2dp2"
+    assert cfg["global_batch"] == 2 * cfg["chunks"] * cfg["micro_batch"] and cfg["chunks"] == 8
+    tokens = cfg["global_batch"] * cfg["seq_len"]
+    assert abs(rec["value"] - tokens / (rec["ms_per_step"] / 1e3)) / rec["value"] < 0.01
+    assert rec["loss"] is not None and rec["loss"] > 0

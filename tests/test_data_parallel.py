@@ -1,0 +1,167 @@
+"""Data parallelism: pipeline replicas with bucketed gradient
+all-reduce (mipipe.parallel.data_parallel), and the reference's documented
+interop -- ``Pipe`` wrapped in DDP with ``checkpoint='never'``
+(/root/reference/pipe.py:290-293).  CPU, gloo, spawned ranks."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers.engine_cases import _data, _grads, _loss_fn, _port, case_cfg
+
+
+def _build(cfg, pp, stage):
+    from mipipe.models import TargetSequential, build_lm_blocks, lm_pipeline_units
+    from mipipe.models.transformer import merge_units
+    from mipipe.parallel import plan_stages
+
+    torch.manual_seed(0)
+    full = torch.nn.Sequential(*build_lm_blocks(cfg))
+    names = {id(p): n for n, p in full.named_parameters()}
+    units = lm_pipeline_units(list(full.children()))
+    plan = plan_stages(cfg, pp, 1, split_decoder=False)
+    chunk = TargetSequential(*merge_units([units[i] for i in plan.slice(stage)])).train()
+    return chunk, names, plan
+
+
+def _reference(m_total, mb):
+    """Single-rank engine over ALL replicas' micro-batches."""
+    from mipipe.optim import FlatAdam
+    from mipipe.parallel import PipelineEngine
+
+    cfg = case_cfg("gloo")
+    model, names, _ = _build(cfg, 1, 0)
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    eng = PipelineEngine(model, chunks=m_total, act_shape=(mb, cfg.seq_len), act_dtype=torch.float32,
+                         loss_fn=_loss_fn(cfg), device=torch.device("cpu"))
+    inputs, targets = _data(cfg, m_total, mb)
+    opt.zero_grad()
+    loss = float(eng.step(inputs, targets).loss)
+    opt.fold_grads()
+    return loss, _grads(model.parameters(), names), float(opt.grad_sumsq())
+
+
+def _dp_worker(rank, world, port, pp, dp, m, mb, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mipipe.optim import FlatAdam
+        from mipipe.parallel import PipelineEngine
+        from mipipe.parallel.data_parallel import DataParallelGrads, make_pp_dp_groups
+        from mipipe.parallel.stage import stage_input_shape
+
+        cfg = case_cfg("gloo")
+        groups = make_pp_dp_groups(pp, dp)
+        chunk, names, plan = _build(cfg, pp, groups.stage)
+        opt = FlatAdam(chunk.parameters(), lr=1e-3)
+        dpg = DataParallelGrads(opt, groups.dp_group, bucket_mb=0.05)  # several buckets
+        eng = PipelineEngine(chunk, chunks=m, act_shape=stage_input_shape(cfg, plan, groups.stage, mb),
+                             act_dtype=torch.float32, loss_fn=_loss_fn(cfg) if groups.stage == pp - 1 else None,
+                             device=torch.device("cpu"), group=groups.channels, grad_divisor=dp)
+        inputs, targets = _data(cfg, m * dp, mb)
+        d = groups.replica
+        mine_in, mine_t = inputs[d * m:(d + 1) * m], targets[d * m:(d + 1) * m]
+        opt.zero_grad()
+        dpg.begin()
+        st = eng.step(mine_in if groups.stage == 0 else None, mine_t)
+        dpg.finish()
+        sq = opt.grad_sumsq()
+        dist.all_reduce(sq, group=groups.pipeline_group)
+        loss = None if st.loss is None else float(st.loss)
+        q.put((rank, groups.replica, loss, _grads(chunk.parameters(), names), float(sq), len(dpg.buckets)))
+        # early issue: buckets whose parameters are all final go out at flush_begin,
+        # the rest when their last weight gradient is done -- same sums either way
+        params = list(chunk.parameters())
+        w = params[-1]
+        before = [b.clone() for b in dpg.buckets]
+        dpg.begin()
+        dpg.flush_begin([w])
+        pending = [not x for x in dpg._issued]
+        assert sum(pending) == 1 and pending[dpg._bucket_of[id(w)]]
+        dpg.wgrad_done(w)
+        assert all(dpg._issued)
+        dpg.finish()
+        for b0, b1 in zip(before, dpg.buckets):
+            torch.testing.assert_close(b1, b0 * dp)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pp,dp", [(2, 2), (1, 2)])
+def test_engine_data_parallel_matches_single_rank(pp, dp):
+    """pp x dp ranks (gloo): every gradient, the loss and the global gradient
+    norm equal the single-rank engine on the union of the replicas' batches."""
+    m, mb = 4, 2
+    ref_loss, ref, ref_sq = _reference(m * dp, mb)
+    world = pp * dp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, pp, dp, m, mb, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    losses = {}
+    seen = set()
+    for rank, replica, loss, grads, sq, nb in results:
+        assert nb >= 2
+        if loss is not None:
+            losses[replica] = loss
+        for name, g in grads.items():
+            r = torch.from_numpy(ref[name])
+            g = torch.from_numpy(g)
+            assert (g - r).abs().max().item() <= 1e-4 * (r.abs().max().item() + 1e-6), name
+            seen.add(name)
+        assert abs(sq - ref_sq) / ref_sq < 1e-4
+    assert seen == set(ref)
+    assert len(losses) == dp
+    assert abs(sum(losses.values()) / dp - ref_loss) < 1e-5 * abs(ref_loss)
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import mipipe
+
+        torch.manual_seed(0)
+        seq = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+        pipe = mipipe.Pipe(seq, chunks=2, checkpoint="never", return_rref=False)
+        ddp = torch.nn.parallel.DistributedDataParallel(pipe)
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(8, 8, generator=g)
+        mine = x[rank * 4:(rank + 1) * 4]
+        ddp(mine).pow(2).mean().backward()
+        q.put((rank, [p.grad.numpy().copy() for p in seq.parameters()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipe_wrapped_in_ddp_checkpoint_never():
+    """The reference's DDP interop: DDP(Pipe(..., checkpoint='never')) averages
+    the replicas' gradients -- equal to one process on the whole batch."""
+    torch.manual_seed(0)
+    seq = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(8, 8, generator=g)
+    seq(x[:4]).pow(2).mean().backward()
+    seq(x[4:]).pow(2).mean().backward()
+    ref = [p.grad / 2 for p in seq.parameters()]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, grads in results:
+        for a, b in zip(grads, ref):
+            torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-5, atol=1e-6)
