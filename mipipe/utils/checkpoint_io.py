@@ -1,0 +1,173 @@
+"""Training-state save / resume.
+
+The reference has no model or optimizer checkpointing ("checkpoint" there
+always means activation checkpointing); a production pipeline needs it.  One
+file per pipeline rank (each rank owns only its stages' parameters -- nothing
+is gathered), in safetensors, whose loader executes nothing from the file:
+
+* ``param.<name>``                    -- the model weights in their dtype (a plain
+  inference checkpoint: :func:`load_weights` needs nothing else);
+* ``flat.<g>.{master,exp_avg,exp_avg_sq}`` -- :class:`mipipe.optim.FlatAdam`'s
+  fp32 flat buffers, saved as the contiguous device buffers they are (one
+  tensor each, no per-parameter split), with the parameter layout in the
+  metadata so a resume into a different partition fails loudly instead of
+  scrambling moments;
+* ``adam.<name>.{exp_avg,exp_avg_sq,step}`` -- ``torch.optim.Adam`` state;
+* ``rng.cpu`` / ``rng.cuda.<i>`` -- generator states, so dropout masks after a
+  resume are the ones the uninterrupted run would have drawn (the HIP dropout
+  kernels take their Philox seed/offset from the torch generator).
+
+A resumed run is bit-identical to the uninterrupted one
+(``tests/test_checkpoint_io.py``).  Data-parallel replicas hold identical
+state: save from replica 0 only and load the same file everywhere.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Iterable, Optional, Tuple
+
+import torch
+from torch import Tensor, nn
+
+__all__ = ["save_training_state", "load_training_state", "load_weights", "rank_path"]
+
+FORMAT = "mipipe-train-state/1"
+
+
+def rank_path(directory: str, rank: int) -> str:
+    """``<directory>/rank00003.safetensors``: one file per pipeline rank."""
+    return os.path.join(directory, f"rank{rank:05d}.safetensors")
+
+
+def _host(t: Tensor) -> Tensor:
+    t = t.detach()
+    return t.to("cpu") if t.device.type != "cpu" else t.clone()
+
+
+def _named(params: Iterable[Tuple[str, nn.Parameter]]) -> Dict[str, nn.Parameter]:
+    out: Dict[str, nn.Parameter] = {}
+    for name, p in params:
+        if name in out:
+            raise ValueError(f"duplicate parameter name {name!r}")
+        out[name] = p
+    return out
+
+
+def save_training_state(path: str, named_params: Iterable[Tuple[str, nn.Parameter]], optimizer=None, *,
+                        step: int = 0, extra: Optional[dict] = None, rng: bool = True) -> None:
+    """Writes this rank's weights, optimizer state and RNG state to ``path``.
+
+    ``named_params``: e.g. ``stage.named_parameters()``; ``optimizer``: a
+    :class:`~mipipe.optim.FlatAdam`, a ``torch.optim.Adam``/``AdamW`` or None."""
+    from safetensors.torch import save_file
+
+    from ..optim import FlatAdam
+
+    params = _named(named_params)
+    by_id = {id(p): n for n, p in params.items()}
+    tensors: Dict[str, Tensor] = {f"param.{n}": _host(p) for n, p in params.items()}
+    meta = {"format": FORMAT, "step": int(step), "extra": extra or {}}
+    if isinstance(optimizer, FlatAdam):
+        layout = []
+        for gi, g in enumerate(optimizer.groups):
+            layout.append([[by_id.get(id(p), "?"), list(p.shape)] for p in g.params])
+            tensors[f"flat.{gi}.master"] = _host(g.master)
+            tensors[f"flat.{gi}.exp_avg"] = _host(g.exp_avg)
+            tensors[f"flat.{gi}.exp_avg_sq"] = _host(g.exp_avg_sq)
+        meta["optimizer"] = {"kind": "FlatAdam", "step": optimizer.step_count, "lr": optimizer.lr,
+                             "layout": layout}
+    elif isinstance(optimizer, torch.optim.Optimizer):
+        kinds = {}
+        for p, st in optimizer.state.items():
+            n = by_id.get(id(p))
+            if n is None:
+                raise ValueError("optimizer holds a parameter missing from named_params")
+            for k, v in st.items():
+                if torch.is_tensor(v):
+                    tensors[f"adam.{n}.{k}"] = _host(v).reshape(v.shape)
+                    kinds[k] = True
+        meta["optimizer"] = {"kind": type(optimizer).__name__,
+                             "lr": [g["lr"] for g in optimizer.param_groups]}
+    elif optimizer is not None:
+        raise TypeError(f"unsupported optimizer {type(optimizer).__name__}")
+    if rng:
+        tensors["rng.cpu"] = torch.get_rng_state()
+        if torch.cuda.is_available():
+            devs = sorted({p.device.index for p in params.values() if p.device.type == "cuda"})
+            for d in devs:
+                tensors[f"rng.cuda.{d}"] = torch.cuda.get_rng_state(d)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = path + ".tmp"
+    save_file({k: v.contiguous() for k, v in tensors.items()}, tmp, metadata={"mipipe": json.dumps(meta)})
+    os.replace(tmp, path)  # a crash mid-save never leaves a torn checkpoint behind
+
+
+def _read(path: str):
+    from safetensors import safe_open
+    from safetensors.torch import load_file
+
+    with safe_open(path, framework="pt") as f:
+        meta = json.loads((f.metadata() or {}).get("mipipe", "{}"))
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"{path}: not a {FORMAT} file")
+    return load_file(path), meta
+
+
+@torch.no_grad()
+def load_weights(path: str, named_params: Iterable[Tuple[str, nn.Parameter]]) -> None:
+    """Copies the saved weights into ``named_params`` (every name must be present)."""
+    tensors, _ = _read(path)
+    for n, p in _named(named_params).items():
+        key = f"param.{n}"
+        if key not in tensors:
+            raise KeyError(f"{path}: no weights for {n!r}")
+        if tuple(tensors[key].shape) != tuple(p.shape):
+            raise ValueError(f"{path}: {n!r} is {tuple(tensors[key].shape)}, the model has {tuple(p.shape)}")
+        p.copy_(tensors[key])
+
+
+@torch.no_grad()
+def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Parameter]], optimizer=None, *,
+                        rng: bool = True) -> dict:
+    """Restores what :func:`save_training_state` wrote; returns its metadata
+    (``step``, ``extra``).  The optimizer must be built over the same
+    parameters in the same order (FlatAdam layouts are checked)."""
+    from ..optim import FlatAdam
+
+    params = _named(named_params)
+    tensors, meta = _read(path)
+    load_weights(path, params.items())
+    opt_meta = meta.get("optimizer")
+    if isinstance(optimizer, FlatAdam):
+        if not opt_meta or opt_meta.get("kind") != "FlatAdam":
+            raise ValueError(f"{path}: no FlatAdam state")
+        by_id = {id(p): n for n, p in params.items()}
+        layout = [[[by_id.get(id(p), "?"), list(p.shape)] for p in g.params] for g in optimizer.groups]
+        if layout != opt_meta["layout"]:
+            raise ValueError(f"{path}: the optimizer's parameter layout differs from the saved one "
+                             f"(a different partition or model)")
+        for gi, g in enumerate(optimizer.groups):
+            g.master.copy_(tensors[f"flat.{gi}.master"])
+            g.exp_avg.copy_(tensors[f"flat.{gi}.exp_avg"])
+            g.exp_avg_sq.copy_(tensors[f"flat.{gi}.exp_avg_sq"])
+            if g.master is not g.model:
+                g.model.copy_(g.master)
+        optimizer.step_count = int(opt_meta["step"])
+        optimizer.lr = float(opt_meta["lr"])
+    elif isinstance(optimizer, torch.optim.Optimizer):
+        for p in (q for grp in optimizer.param_groups for q in grp["params"]):
+            n = next(k for k, v in params.items() if v is p)
+            st = {}
+            for key in [k for k in tensors if k.startswith(f"adam.{n}.")]:
+                st[key[len(f"adam.{n}."):]] = tensors[key].to(p.device if key.split(".")[-1] != "step" else "cpu")
+            if st:
+                optimizer.state[p] = st
+        for grp, lr in zip(optimizer.param_groups, (opt_meta or {}).get("lr", [])):
+            grp["lr"] = lr
+    if rng and "rng.cpu" in tensors:
+        torch.set_rng_state(tensors["rng.cpu"])
+        for key, st in tensors.items():
+            if key.startswith("rng.cuda.") and torch.cuda.is_available():
+                torch.cuda.set_rng_state(st, int(key.rsplit(".", 1)[1]))
+    return {"step": meta.get("step", 0), "extra": meta.get("extra", {})}

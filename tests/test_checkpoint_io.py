@@ -1,0 +1,102 @@
+"""Training-state save / resume (mipipe.utils.checkpoint_io): a run resumed from
+a checkpoint is bit-identical to the uninterrupted run -- weights, Adam
+moments, step count and the dropout RNG -- through the Pipe."""
+import dataclasses
+
+import pytest
+import torch
+
+import mipipe
+from mipipe.models import CONFIGS, build_lm_blocks
+from mipipe.ops import cross_entropy
+from mipipe.optim import FlatAdam
+from mipipe.utils.checkpoint_io import load_training_state, load_weights, rank_path, save_training_state
+
+
+def _cfg():
+    return dataclasses.replace(CONFIGS["tiny"], num_layers=2, d_model=32, nhead=4, dim_feedforward=64, vocab=100,
+                               seq_len=8, dropout=0.2)
+
+
+def _pipe(seed, device="cpu", dtype=torch.float32):
+    torch.manual_seed(seed)
+    blocks = build_lm_blocks(_cfg())
+    seq = torch.nn.Sequential(torch.nn.Sequential(*blocks[:3]).to(device, dtype),
+                              torch.nn.Sequential(*blocks[3:]).to(device, dtype))
+    return mipipe.Pipe(seq, chunks=2, checkpoint="except_last", return_rref=False)
+
+
+def _batches(n):
+    g = torch.Generator().manual_seed(5)
+    tok = torch.randint(0, 100, (n, 4, 9), generator=g)
+    return [(tok[i, :, :8], tok[i, :, 1:]) for i in range(n)]
+
+
+def _step(pipe, opt, x, t, flat):
+    opt.zero_grad()
+    dev = next(pipe.parameters()).device
+    loss = cross_entropy(pipe(x.to(dev)).reshape(-1, 100), t.to(dev).reshape(-1))
+    loss.backward()
+    if not flat:
+        torch.nn.utils.clip_grad_norm_(pipe.parameters(), 0.5)
+    opt.step()
+    return float(loss.detach())
+
+
+def _resume_case(tmp_path, flat, device="cpu", dtype=torch.float32):
+    data = _batches(4)
+
+    def make(seed):
+        pipe = _pipe(seed, device, dtype)
+        opt = (FlatAdam(pipe.parameters(), lr=1e-2, max_grad_norm=0.5) if flat
+               else torch.optim.Adam(pipe.parameters(), lr=1e-2))
+        return pipe, opt
+
+    pipe, opt = make(0)
+    for x, t in data[:2]:
+        _step(pipe, opt, x, t, flat)
+    path = rank_path(str(tmp_path), 0)
+    save_training_state(path, pipe.named_parameters(), opt, step=2, extra={"note": "after 2"})
+    tail = [_step(pipe, opt, x, t, flat) for x, t in data[2:]]
+    final = {n: p.detach().clone() for n, p in pipe.named_parameters()}
+
+    pipe2, opt2 = make(1)  # different initial weights: everything must come from the file
+    meta = load_training_state(path, pipe2.named_parameters(), opt2)
+    assert meta["step"] == 2 and meta["extra"] == {"note": "after 2"}
+    tail2 = [_step(pipe2, opt2, x, t, flat) for x, t in data[2:]]
+    assert tail == tail2
+    for n, p in pipe2.named_parameters():
+        assert torch.equal(p, final[n]), n
+
+
+@pytest.mark.parametrize("flat", [True, False])
+def test_resume_is_bit_identical(tmp_path, flat):
+    _resume_case(tmp_path, flat)
+
+
+@pytest.mark.gpu
+def test_resume_is_bit_identical_gpu(tmp_path):
+    """On the MI355X: bf16 HIP kernels, dropout masks from the restored HIP
+    generator (Philox seed/offset), FlatAdam's fused kernel."""
+    _resume_case(tmp_path, True, "cuda:0", torch.bfloat16)
+
+
+def test_load_weights_and_layout_check(tmp_path):
+    pipe = _pipe(0)
+    opt = FlatAdam(pipe.parameters(), lr=1e-2)
+    path = str(tmp_path / "ck.safetensors")
+    save_training_state(path, pipe.named_parameters(), opt)
+    other = _pipe(1)
+    load_weights(path, other.named_parameters())
+    for (n, a), (_, b) in zip(pipe.named_parameters(), other.named_parameters()):
+        assert torch.equal(a, b), n
+    # an optimizer over a different parameter order is refused, not silently scrambled
+    params = list(other.parameters())
+    bad = FlatAdam(params[::-1], lr=1e-2)
+    with pytest.raises(ValueError, match="layout"):
+        load_training_state(path, other.named_parameters(), bad)
+    with pytest.raises(ValueError, match="not a"):
+        from safetensors.torch import save_file
+
+        save_file({"x": torch.zeros(1)}, str(tmp_path / "foreign.safetensors"))
+        load_weights(str(tmp_path / "foreign.safetensors"), other.named_parameters())
