@@ -58,6 +58,8 @@ def parse(argv=None):
     ap.add_argument("--profile-dir", default=None)
     ap.add_argument("--memory-snapshot", default=None)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--save", default=None, help="write the training state (weights, optimizer, RNG) here at the end")
+    ap.add_argument("--resume", default=None, help="continue from a --save file (same model and partition)")
     return ap.parse_args(argv)
 
 
@@ -115,6 +117,14 @@ def main(argv=None) -> int:
         opt = None
     lr = args.lr
     out_dev = devices[-1]
+    start = 0
+    if args.resume:
+        from mipipe.utils.checkpoint_io import load_training_state
+
+        meta = load_training_state(args.resume, model.named_parameters(), flat if flat is not None else opt)
+        start = int(meta["step"])
+        lr = flat.lr if flat is not None else opt.param_groups[0]["lr"]
+        print(f"resumed from {args.resume} at batch {start}")
 
     def step(data, targets):
         nonlocal lr
@@ -140,15 +150,18 @@ def main(argv=None) -> int:
         prof.__enter__()
     model.train()
     t0 = time.time()
-    total_loss, ntok = 0.0, 0
+    total_loss, ntok, nbatches = 0.0, 0, 0
     try:
         for batch, (data, targets) in enumerate(D.iter_batches(train_data, bptt, args.batches)):
+            if batch < start:
+                continue
             if prof is not None:
                 prof.step()
             data = data.to(devices[0])
             loss = step(data, targets)
             lv = loss.item()
             total_loss += lv
+            nbatches += 1
             ntok += data.numel()
             print(f"| batch {batch:3d} | lr {lr:.3g} | loss {lv:6.3f} | ppl {math.exp(min(lv, 20)):9.2f}")
     finally:
@@ -164,12 +177,18 @@ def main(argv=None) -> int:
     else:
         for g in opt.param_groups:
             g["lr"] = lr
-    print(f"tokens/s {ntok / elapsed:.1f} over {elapsed:.2f}s; mean loss {total_loss / max(1, batch + 1):.3f}")
+    print(f"tokens/s {ntok / elapsed:.1f} over {elapsed:.2f}s; mean loss {total_loss / max(1, nbatches):.3f}")
     for d, r in P.memory_report(set(devices)).items():
         print(f"{d}: peak allocated {r['peak_allocated_mb']:.0f} MB, peak reserved {r['peak_reserved_mb']:.0f} MB")
     if args.memory_snapshot and on_gpu:
         P.dump_memory_snapshot(args.memory_snapshot)
         P.record_memory_history(False)
+    if args.save:
+        from mipipe.utils.checkpoint_io import save_training_state
+
+        save_training_state(args.save, model.named_parameters(), flat if flat is not None else opt,
+                            step=batch + 1, extra={"config": args.config, "checkpoint": args.checkpoint})
+        print(f"saved the training state to {args.save}")
     model.close()
     return 0
 
