@@ -365,7 +365,8 @@ def run_pipe(args) -> int:
     plan = plan_stages(cfg, n, 1, m, split_decoder=False)
     stages = [build_stage(cfg, plan, s, device=devices[s], dtype=dtype).train() for s in range(n)]
     params = [p for st_ in stages for p in st_.parameters()]
-    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip)
+    # weight gradients deferred to one K-segmented GEMM per weight after the backward, as the engine does
+    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
     pipe = mipipe.Pipe(torch.nn.Sequential(*stages), chunks=m, checkpoint=args.checkpoint)
 
     g = torch.Generator(device="cpu").manual_seed(0)

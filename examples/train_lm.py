@@ -113,7 +113,7 @@ def main(argv=None) -> int:
         opt = torch.optim.Adam(model.parameters(), lr=args.lr)
         flat = None
     else:
-        flat = FlatAdam(model.parameters(), lr=args.lr, max_grad_norm=args.clip)
+        flat = FlatAdam(model.parameters(), lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
         opt = None
     lr = args.lr
     out_dev = devices[-1]

@@ -267,18 +267,41 @@ def flush_wgrad() -> None:
         li.flush_begin([w for w, _, _ in queue.values()])
     for w, dys, xs in queue.values():
         k = kernels_for(dys[0])
-        if xs is None:  # a bias
-            k.column_sum_segments(dys, w.main_grad, True)
-        else:
-            T = dys[0].shape[0]
-            uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
-            if uniform and T % 64 == 0:
-                k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
+        # a single-process Pipe queues weights of several devices: launch each on its own
+        with torch.cuda.device(dys[0].device):
+            if xs is None:  # a bias
+                k.column_sum_segments(dys, w.main_grad, True)
             else:
-                for d, x in zip(dys, xs):
-                    k.linear_wgrad(d, x, w.main_grad, _claim(w))
+                T = dys[0].shape[0]
+                uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
+                if uniform and T % 64 == 0:
+                    k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
+                else:
+                    for d, x in zip(dys, xs):
+                        k.linear_wgrad(d, x, w.main_grad, _claim(w))
         for li in listeners:
             li.wgrad_done(w)
+
+
+def begin_deferred_wgrad() -> bool:
+    """Starts queueing weight gradients (as :class:`deferred_wgrad` does) until
+    :func:`end_deferred_wgrad`; for callers whose backward is the user's own
+    ``loss.backward()`` (``FlatAdam(defer_wgrad=True)`` around a ``Pipe``).
+    Returns False (and does nothing) when a deferral is already active."""
+    global _DEFERRED
+    if _DEFERRED is not None:
+        return False
+    _DEFERRED = {}
+    return True
+
+
+def end_deferred_wgrad() -> None:
+    """Runs the queued weight-gradient GEMMs and stops queueing."""
+    global _DEFERRED
+    try:
+        flush_wgrad()
+    finally:
+        _DEFERRED = None
 
 
 class deferred_wgrad:

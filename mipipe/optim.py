@@ -75,6 +75,7 @@ class FlatAdam:
         *,
         adamw: bool = False,
         max_grad_norm: Optional[float] = None,
+        defer_wgrad: bool = False,
     ) -> None:
         self.lr = lr
         self.betas = betas
@@ -82,6 +83,16 @@ class FlatAdam:
         self.weight_decay = weight_decay
         self.adamw = adamw
         self.max_grad_norm = max_grad_norm
+        # defer_wgrad: zero_grad() starts queueing the weight-gradient GEMMs of
+        # the coming backward (mipipe.ops.linear deferral) and fold_grads() --
+        # called by grad_sumsq() and step() -- runs them as ONE K-segmented GEMM
+        # per weight over all micro-batches: main_grad is written once per step
+        # instead of read-modified-written per micro-batch, and a multi-GPU Pipe
+        # sends its input gradients upstream without waiting for weight
+        # gradients.  Read main_grad only after fold_grads().  Not for use
+        # inside the multi-process engine, which defers on its own.
+        self.defer_wgrad = defer_wgrad
+        self._deferring = False
         self.step_count = 0
         buckets: Dict[Tuple[torch.device, torch.dtype], List[nn.Parameter]] = {}
         seen = set()
@@ -103,6 +114,8 @@ class FlatAdam:
         MIPIPE_LAZY_ZERO=0."""
         if lazy is None:
             lazy = os.environ.get("MIPIPE_LAZY_ZERO", "1") != "0"
+        if self._deferring:  # a backward whose gradients were never read: drop its queue
+            self.fold_grads()
         for g in self.groups:
             if lazy and g.n_lazy:
                 g.main_grad[g.n_lazy:].zero_()
@@ -114,10 +127,20 @@ class FlatAdam:
                     p._mg_fresh = False  # type: ignore[attr-defined]
             for p in g.params:
                 p.grad = None
+        if self.defer_wgrad:
+            from .ops.linear import begin_deferred_wgrad
+
+            self._deferring = begin_deferred_wgrad()
 
     def fold_grads(self) -> None:
         """Adds any autograd ``.grad`` (ops without main_grad support) into
-        main_grad and zeroes lazily-zeroed gradients nothing wrote this step."""
+        main_grad and zeroes lazily-zeroed gradients nothing wrote this step
+        (after running deferred weight-gradient GEMMs, with ``defer_wgrad``)."""
+        if self._deferring:
+            from .ops.linear import end_deferred_wgrad
+
+            self._deferring = False
+            end_deferred_wgrad()
         with torch.no_grad():
             for g in self.groups:
                 for p in g.params:

@@ -51,7 +51,7 @@ def _ngpu():
 
 
 # ------------------------------------------------------------------ Pipe on our kernels
-def _pipe_vs_sequential(devices, checkpoint, copy_streams=None, dropout=0.0):
+def _pipe_vs_sequential(devices, checkpoint, copy_streams=None, dropout=0.0, defer_wgrad=False):
     cfg = _cfg(dropout=dropout)
     m, mb = 4, 2
     torch.manual_seed(0)
@@ -74,14 +74,23 @@ def _pipe_vs_sequential(devices, checkpoint, copy_streams=None, dropout=0.0):
     parts = [torch.nn.Sequential(*blocks[i * per:(i + 1) * per]).to(devices[i]) for i in range(n)
              if blocks[i * per:(i + 1) * per]]
     model = torch.nn.Sequential(*parts).train()
-    opt = FlatAdam(model.parameters(), lr=1e-3)
+    opt = FlatAdam(model.parameters(), lr=1e-3, defer_wgrad=defer_wgrad)
     pipe = Pipe(model, chunks=m, checkpoint=checkpoint, copy_streams=copy_streams)
     try:
         opt.zero_grad()
         out = pipe(x).local_value()
         loss = _loss_fn(cfg)(out, t.to(out.device))
         loss.backward()
+        if defer_wgrad:
+            import importlib
+
+            _lin = importlib.import_module("mipipe.ops.linear")  # the module, not ops.linear()
+
+            queued = len(_lin._DEFERRED or {})
+            assert queued > 0, "no weight gradient was deferred"
         opt.fold_grads()
+        if defer_wgrad:
+            assert _lin._DEFERRED is None
     finally:
         pipe.close()
     assert abs(float(loss) - float(loss_ref)) < 2e-3 * abs(float(loss_ref))
@@ -92,11 +101,29 @@ def _pipe_vs_sequential(devices, checkpoint, copy_streams=None, dropout=0.0):
     return pipe
 
 
+@pytest.mark.parametrize("checkpoint", ["never", "except_last"])
+def test_pipe_deferred_wgrad_one_gpu(checkpoint):
+    """FlatAdam(defer_wgrad=True) around a Pipe: the backward queues the weight
+    gradients of every micro-batch and fold_grads runs one K-segmented GEMM per
+    weight -- same gradients as the unsplit model."""
+    _pipe_vs_sequential([DEV], checkpoint, defer_wgrad=True)
+
+
 @pytest.mark.parametrize("checkpoint", ["never", "except_last", "always"])
 def test_pipe_lm_bf16_one_gpu(checkpoint):
     """Pipe on one MI355X (one partition: scatter, worker thread, checkpoint /
     recompute, gather) with the HIP-kernel LM blocks == nn.Sequential."""
     _pipe_vs_sequential([DEV], checkpoint)
+
+
+@pytest.mark.multigpu
+@pytest.mark.parametrize("ngpu", [2, 4])
+def test_pipe_deferred_wgrad_multi_gpu(ngpu):
+    """Deferred weight gradients queued by several devices' autograd threads are
+    each launched on their own device at fold_grads."""
+    if _ngpu() < ngpu:
+        pytest.skip(f"needs {ngpu} GPUs")
+    _pipe_vs_sequential([torch.device("cuda", d) for d in range(ngpu)], "except_last", defer_wgrad=True)
 
 
 @pytest.mark.multigpu
