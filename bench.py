@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="enc12_d4096")
     ap.add_argument("--micro-batch", type=int, default=None,
-                    help="sequences per micro-batch (default 32 for enc12_d4096 / ref_main, 8 for gpt2_xl)")
+                    help="sequences per micro-batch (default 64 for enc12_d4096, 8 for ref_main (the reference's) "
+                         "and gpt2_xl)")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--num-layers", type=int, default=None, help="override the model's layer count (tests)")
     ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
@@ -437,8 +438,10 @@ def _config(args):
 
 
 def _default_micro_batch(cfg) -> int:
-    # ref_main: the reference's own micro-batch (batch 32 / chunks 4 = 8 sequences)
-    return {"gpt2_xl": 8, "tiny": 8, "ref_main": 8}.get(cfg.name, 32)
+    # ref_main: the reference's own micro-batch (batch 32 / chunks 4 = 8 sequences).
+    # enc12_d4096: 64 x 128 = 8192 tokens per GEMM, sized for 288 GB of HBM (57 GiB peak at
+    # PP=1): +3.5 % over 32 x 128 on the same box (profiles/microbatch_sizing.txt).
+    return {"gpt2_xl": 8, "tiny": 8, "ref_main": 8}.get(cfg.name, 64)
 
 
 def _baseline_note(ref_match: bool, checkpoint: str) -> str:
