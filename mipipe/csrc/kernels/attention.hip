@@ -1117,18 +1117,26 @@ __global__ void __launch_bounds__(kThreads, 1) attn_bwd_s128_kernel(AttnArgs a) 
   bf16_t* dK = reinterpret_cast<bf16_t*>(a.dk) + boff;
   bf16_t* dV = reinterpret_cast<bf16_t*>(a.dv) + boff;
   const int r0 = wave * 16;  // output rows (queries for dQ, keys for dK / dV)
+  // The next chunk's K / Q / dO are loaded into registers while this chunk's
+  // MFMAs run; results leave through the (then free) chunk images as 16-byte
+  // row stores instead of 2-byte scattered ones.
+  uint4 a0, a1, b0, b1, e0, e1;
+  load_chunk(K, a.ld_qkv, 0, tid, a0, a1);
+  load_chunk(Q, a.ld_qkv, 0, tid, b0, b1);
+  load_chunk(dO, a.ld_o, 0, tid, e0, e1);
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) {
     const int d0 = c * kChunk;
-    uint4 a0, a1, b0, b1, e0, e1;
-    load_chunk(K, a.ld_qkv, d0, tid, a0, a1);
-    load_chunk(Q, a.ld_qkv, d0, tid, b0, b1);
-    load_chunk(dO, a.ld_o, d0, tid, e0, e1);
-    __syncthreads();  // previous chunk's readers are done (and phase-1 images for c == 0)
+    __syncthreads();  // previous chunk's output readers are done (and phase-1 images for c == 0)
     store_chunk(kimg, tid, a0, a1);
     store_chunk(qimg, tid, b0, b1);
     store_chunk(dimg, tid, e0, e1);
     __syncthreads();
+    if (c + 1 < NC) {
+      load_chunk(K, a.ld_qkv, d0 + kChunk, tid, a0, a1);
+      load_chunk(Q, a.ld_qkv, d0 + kChunk, tid, b0, b1);
+      load_chunk(dO, a.ld_o, d0 + kChunk, tid, e0, e1);
+    }
     f32x4 dq[4], dk[4], dv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) dq[t] = dk[t] = dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1145,15 +1153,31 @@ __global__ void __launch_bounds__(kThreads, 1) attn_bwd_s128_kernel(AttnArgs a) 
       }
     }
     const int orow = r0 + 4 * (lane >> 4);
+    __syncthreads();  // every wave is done reading the input images
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      const int col = 16 * t + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t o = (int64_t)(orow + r) * a.ld_qkv + d0 + 16 * t + (lane & 15);
-        dQ[o] = f2bf(dq[t][r] * a.scale);
-        dK[o] = f2bf(dk[t][r] * a.scale);
-        dV[o] = f2bf(dv[t][r]);
+        const int at = coff(orow + r, col >> 3) + 2 * (col & 7);
+        *reinterpret_cast<bf16_t*>(kimg + at) = f2bf(dq[t][r] * a.scale);
+        *reinterpret_cast<bf16_t*>(qimg + at) = f2bf(dk[t][r] * a.scale);
+        *reinterpret_cast<bf16_t*>(dimg + at) = f2bf(dv[t][r]);
       }
+    }
+    __syncthreads();
+    {
+      const int r = tid >> 3, cc = tid & 7;  // pieces tid and tid + 512: rows r and r + 64
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int row = r + 64 * h2;
+        const int off = coff(row, cc);
+        const int64_t g = (int64_t)row * a.ld_qkv + d0 + 8 * cc;
+        *reinterpret_cast<uint4*>(dQ + g) = *reinterpret_cast<const uint4*>(kimg + off);
+        *reinterpret_cast<uint4*>(dK + g) = *reinterpret_cast<const uint4*>(qimg + off);
+        *reinterpret_cast<uint4*>(dV + g) = *reinterpret_cast<const uint4*>(dimg + off);
+      }
+    }
   }
 }
 
