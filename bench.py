@@ -279,6 +279,7 @@ def main() -> int:
     armed.__exit__(None, None, None)
     if wd is not None:
         wd.close()
+    stop_n = checkpoint_stop_for(args.checkpoint, m)
     tokens_per_step = m * mb * S * dp
     value = tokens_per_step / (ms / 1e3)
     total_params = sum(int(x) for x in _allsum([n_params_local], device, world)) // dp  # one replica
@@ -319,6 +320,10 @@ def main() -> int:
                 "stage_imbalance": round(plan.imbalance(), 3),
             },
             "bubble_pct": None if bubble is None else round(bubble, 2),
+            "work_note": (f"checkpoint={args.checkpoint!r} re-runs the forward of {stop_n} of {m} micro-batches: "
+                          f"~{1.0 + stop_n / m / 3.0:.2f}x the per-GPU compute of a 'never' step (the PP=1 "
+                          f"default), which bounds weak-scaling efficiency against it")
+            if stop_n else None,
             "bubble_theory_pct": round(100.0 * (pp - 1) / (virtual * m + pp - 1), 2),
             "bubble_gpipe_v1_pct": round(100.0 * (pp - 1) / (m + pp - 1), 2),
             "stage_busy_ms": stage_busy,
