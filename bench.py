@@ -206,7 +206,12 @@ def main() -> int:
         opt.zero_grad()
         if dpg is not None:
             dpg.begin()
-        st = engine.step(inputs, targets)
+        try:
+            st = engine.step(inputs, targets)
+        except BaseException:
+            if dpg is not None:
+                dpg.abort()  # unhook the gradient buckets from the weight-gradient flush
+            raise
         if dpg is not None:
             mark("data-parallel gradient all-reduce")
             dpg.finish()

@@ -131,7 +131,12 @@ def main(argv=None) -> int:
         opt.zero_grad()
         if dpg is not None:
             dpg.begin()
-        st = engine.step(xs if groups.stage == 0 else None, ts)
+        try:
+            st = engine.step(xs if groups.stage == 0 else None, ts)
+        except BaseException:
+            if dpg is not None:
+                dpg.abort()  # unhook the gradient buckets from the weight-gradient flush
+            raise
         if dpg is not None:
             dpg.finish()
         sq = opt.grad_sumsq()

@@ -197,3 +197,33 @@ def test_pipe_wrapped_in_ddp_checkpoint_never():
     for _, grads in results:
         for a, b in zip(grads, ref):
             torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-5, atol=1e-6)
+
+
+def test_listener_unhooked_on_abort_and_finish():
+    """begin() hooks the weight-gradient flush; finish() and abort() unhook it
+    (a failed step must not leave a stale listener behind)."""
+    import importlib
+
+    lin = importlib.import_module("mipipe.ops.linear")
+
+    class _Opt:
+        groups = []
+
+        def fold_grads(self):
+            pass
+
+    from mipipe.parallel.data_parallel import DataParallelGrads
+
+    dpg = DataParallelGrads.__new__(DataParallelGrads)
+    dpg.opt, dpg.group, dpg.world, dpg.average = _Opt(), None, 1, False
+    dpg.buckets, dpg._members, dpg._bucket_of = [], [], {}
+    dpg._left, dpg._works, dpg._issued, dpg._active = [], [], [], False
+    dpg.begin()
+    assert dpg in lin._WGRAD_LISTENERS
+    dpg.abort()
+    assert dpg not in lin._WGRAD_LISTENERS
+    dpg.begin()
+    dpg.finish()
+    assert dpg not in lin._WGRAD_LISTENERS
+    with pytest.raises(RuntimeError):
+        dpg.finish()
