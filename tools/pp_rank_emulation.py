@@ -47,6 +47,9 @@ class Loopback(Channels):
         self.rank, self.world, self.ranks = rank, world, list(range(world))
         self.host_staged = False
 
+    def warmup(self, device) -> None:  # nothing to connect
+        pass
+
     def send_act(self, t):
         return _Done()
 
