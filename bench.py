@@ -353,6 +353,8 @@ def run_pipe(args) -> int:
     one partition per device."""
     if int(os.environ.get("WORLD_SIZE", "1")) != 1:
         raise SystemExit("--impl pipe is one process driving every GPU: run it without torchrun")
+    if args.dp != 1:
+        raise SystemExit("--dp applies to the engine (--impl engine); a Pipe is one pipeline")
     import mipipe
     from mipipe import ops
     from mipipe.optim import FlatAdam
