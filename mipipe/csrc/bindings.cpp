@@ -69,11 +69,15 @@ void py_stream_wait(int64_t waiting, int64_t waited, int64_t device) {
   rt::stream_wait(reinterpret_cast<hipStream_t>(waiting), reinterpret_cast<hipStream_t>(waited), (int)device);
 }
 
-void py_peer_copy(Tensor dst, Tensor src, int64_t src_stream, int64_t dst_stream, int64_t src_dev, int64_t dst_dev) {
+void py_peer_copy(Tensor dst, Tensor src, int64_t src_stream, int64_t dst_stream, int64_t src_dev, int64_t dst_dev,
+                  int64_t engine) {
   MP_CHECK(dst.is_contiguous() && src.is_contiguous(), "peer_copy needs contiguous tensors");
   MP_CHECK(dst.nbytes() == src.nbytes(), "peer_copy size mismatch");
+  MP_CHECK(dst.is_cuda() && src.is_cuda(), "peer_copy needs device tensors");
+  MP_CHECK(dst.get_device() == dst_dev && src.get_device() == src_dev, "peer_copy device mismatch");
+  MP_CHECK(engine == rt::kCopySdma || engine == rt::kCopyBlit, "peer_copy: engine is 0 (sdma) or 1 (blit)");
   rt::peer_copy(dst.data_ptr(), (int)dst_dev, src.data_ptr(), (int)src_dev, src.nbytes(),
-                reinterpret_cast<hipStream_t>(src_stream), reinterpret_cast<hipStream_t>(dst_stream));
+                reinterpret_cast<hipStream_t>(src_stream), reinterpret_cast<hipStream_t>(dst_stream), (int)engine);
 }
 
 void py_gpu_sleep(int64_t us) { mipipe::gpu_sleep(us, at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()); }
@@ -786,13 +790,20 @@ void py_adam(Tensor master, std::optional<Tensor> model, Tensor grad, Tensor m, 
 }  // namespace
 }  // namespace mipipe
 
+// Defined in the build-generated source_digest.cpp (mipipe/build.py): the
+// digest of the sources this binary was compiled from, checked at import by
+// mipipe/_native_loader.py.
+extern "C" const char* mipipe_source_digest();
+
 PYBIND11_MODULE(_C, m) {
+  m.def("source_digest", []() { return std::string(mipipe_source_digest()); });
   using namespace mipipe;
   m.doc() = "mipipe native runtime + CDNA4 HIP kernels (gfx950)";
   // runtime
   m.def("stream_pool_acquire", &py_stream_acquire, py::arg("device"), py::arg("priority") = -1);
   m.def("stream_wait", &py_stream_wait);
-  m.def("peer_copy", &py_peer_copy);
+  m.def("peer_copy", &py_peer_copy, py::arg("dst"), py::arg("src"), py::arg("src_stream"), py::arg("dst_stream"),
+        py::arg("src_device"), py::arg("dst_device"), py::arg("engine") = 0);
   m.def("enable_peer_access", [](std::vector<int> d) { rt::enable_peer_access(d); });
   m.def("can_access_peer", [](int d, int q) { return rt::can_access_peer(d, q); });
   m.def("range_push", [](const std::string& s) { rt::range_push(s); });

@@ -105,8 +105,30 @@ void stream_wait(hipStream_t waiting, hipStream_t waited, int device) {
   check(hipStreamWaitEvent(waiting, e, 0), "hipStreamWaitEvent");
 }
 
+// Grid-stride 16-byte copy.  A launch of <= 4 waves per CU (1024 blocks of
+// 256) saturates HBM / an xGMI link without tying up the whole chip.
+__global__ void __launch_bounds__(256) blit16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                     size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+void blit_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return;
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | bytes) & 15) {
+    check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream), "hipMemcpyAsync(blit fallback)");
+    return;
+  }
+  const size_t n = bytes / 16;
+  const size_t want = (n + 255) / 256;
+  const unsigned blocks = (unsigned)(want < 1024 ? want : 1024);
+  hipLaunchKernelGGL(blit16_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(dst), n);
+  check(hipGetLastError(), "blit16_kernel launch");
+}
+
 void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_t bytes, hipStream_t src_stream,
-               hipStream_t dst_stream) {
+               hipStream_t dst_stream, int engine) {
   if (bytes == 0) return;
   {
     // The destination block may have been freed by work still pending on
@@ -119,7 +141,13 @@ void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_
   }
   {
     DeviceGuard g(src_device);
-    check(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, src_stream), "hipMemcpyPeerAsync");
+    if (engine == kCopyBlit) {
+      blit_copy(dst, src, bytes, src_stream);
+    } else if (dst_device == src_device) {
+      check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, src_stream), "hipMemcpyAsync");
+    } else {
+      check(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, src_stream), "hipMemcpyPeerAsync");
+    }
   }
   {
     EventPool& p = pool(src_device);

@@ -19,11 +19,21 @@ hipStream_t stream_acquire(int device, int priority);
 // enqueued on `waited` so far has finished.  Uses a pooled event.
 void stream_wait(hipStream_t waiting, hipStream_t waited, int device);
 
-// Async peer copy of `bytes` from src (on src_device) to dst (on dst_device).
+// Copy engines for peer_copy.
+enum CopyEngine : int {
+  kCopySdma = 0,  // hipMemcpy(Peer)Async: the DMA engines, no CUs used
+  kCopyBlit = 1,  // a 16-byte-vector copy kernel on src_stream (push into the peer's HBM)
+};
+
+// Async copy of `bytes` from src (on src_device) to dst (on dst_device); the
+// devices may be equal (a stage boundary between two partitions of one GPU).
 // Ordering: dst_stream's prior work -> copy on src_stream -> dst_stream.
-// The copy itself runs on src_stream (SDMA engine over xGMI).
 void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_t bytes, hipStream_t src_stream,
-               hipStream_t dst_stream);
+               hipStream_t dst_stream, int engine = kCopySdma);
+
+// The blit kernel alone, on `stream` of the current device (falls back to
+// hipMemcpyAsync for pointers or sizes that are not 16-byte multiples).
+void blit_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 
 // Enables peer access between every ordered pair of `devices` (idempotent).
 void enable_peer_access(const std::vector<int>& devices);

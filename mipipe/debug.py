@@ -130,13 +130,14 @@ def serialized_pipe(pipe) -> Iterator[None]:
     from .stream import current_stream
 
     pl = pipe.pipeline
-    saved = (pl.copy_streams, pl.sync_debug)
+    saved = (pl.copy_streams, pl.sync_debug, pl.dedicated_streams)
     pl.copy_streams = [[current_stream(d)] * len(s) for d, s in zip(pl.devices, pl.copy_streams)]
+    pl.dedicated_streams = [None] * len(pl.devices)  # every partition of a GPU on its current stream
     pl.sync_debug = True
     try:
         yield
     finally:
-        pl.copy_streams, pl.sync_debug = saved
+        pl.copy_streams, pl.sync_debug, pl.dedicated_streams = saved
 
 
 def check_pipe(pipe, *inputs: Any, loss_fn: Optional[Callable[[Tensor], Tensor]] = None,

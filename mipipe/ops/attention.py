@@ -133,10 +133,10 @@ def _causal_pad(t: Tensor, S: int, D: int) -> Optional[int]:
     return None
 
 
-_KEY_MASK = -32768.0  # exact in bf16; times the query's 1 and any scale >= 2^-4: exp underflows to 0
+_KEY_MASK = -32768.0  # exact in bf16; times the query's 1 and any scale >= 2^-8: exp underflows to 0
 
 
-def _run_shape(t: Tensor, S: int, D: int, causal: bool) -> Optional[Tuple[int, int]]:
+def _run_shape(t: Tensor, S: int, D: int, causal: bool, scale: float) -> Optional[Tuple[int, int]]:
     """(sequence length, head dim) the kernels run a (S, D) attention at, or None (eager path).
 
     * A head dim the kernels do not tile is zero-padded to the next one they do: the
@@ -152,7 +152,8 @@ def _run_shape(t: Tensor, S: int, D: int, causal: bool) -> Optional[Tuple[int, i
     for dp in dims:
         if _gpu_ok(t, S, dp):
             return S, dp
-        sp = _causal_pad(t, S, dp) if (causal or dp > D) else None
+        # the spare-feature key mask needs exp(-32768 * scale) to underflow to 0
+        sp = _causal_pad(t, S, dp) if (causal or (dp > D and scale >= 2.0 ** -8)) else None
         if sp is not None:
             return sp, dp
     return None
@@ -167,7 +168,7 @@ def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, 
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(D)
     if qkv.is_cuda and _gpu_ok(qkv, S, D):
         return _AttentionPacked.apply(qkv.contiguous(), bool(causal), p, scale)
-    run = _run_shape(qkv, S, D, bool(causal)) if qkv.is_cuda else None
+    run = _run_shape(qkv, S, D, bool(causal), scale) if qkv.is_cuda else None
     if run is not None:
         sp, dp = run
         padded = F.pad(qkv, (0, dp - D, 0, 0, 0, 0, 0, sp - S))
@@ -196,7 +197,7 @@ def attention(
         return attention_reference(q, k, v, causal, p, scale)
     S, D = q.shape[2], q.shape[3]
     if not _gpu_ok(q, S, D):
-        run = _run_shape(q, S, D, bool(causal))
+        run = _run_shape(q, S, D, bool(causal), scale)
         if run is None:
             _note_math_path(S, D, q.dtype)
             return attention_reference(q, k, v, causal, p, scale)

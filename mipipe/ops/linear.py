@@ -18,6 +18,7 @@ torch.matmul with the same fused elementwise kernels.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Optional
 
 import torch
@@ -144,6 +145,8 @@ class _Linear(torch.autograd.Function):
             return dres, None, None, None, None, None, None
         k = kernels_for(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        if ctx.fused_tile and not _aligned(d2):
+            d2 = d2.clone()  # a misaligned contiguous view: the tile GEMMs move 16-byte chunks
         need_db = bias is not None and ctx.needs_input_grad[2]
         main_b = accumulable(bias) if need_db else None
         # inside deferred_wgrad(): the bias gradient joins the step's batch too
@@ -228,10 +231,13 @@ def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
     k = kernels_for(dy) if dy.is_cuda else None
     tile = (k is not None and dy.dtype == x.dtype and _gemm_supported(k, dy.dtype, w.shape[0], w.shape[1], dy.shape[0]))
     if main is not None and tile:
+        dy, x = dy.contiguous(), x.contiguous()
+        dy = dy if _aligned(dy) else dy.clone()
+        x = x if _aligned(x) else x.clone()
         if _DEFERRED is not None:
-            _defer(w, dy.contiguous(), x.contiguous())
+            _defer(w, dy, x)
         else:
-            k.linear_wgrad(dy.contiguous(), x.contiguous(), main, _claim(w))
+            k.linear_wgrad(dy, x, main, _claim(w))
         return None
     g = torch.matmul(dy.t(), x)
     if main is not None:
@@ -268,7 +274,8 @@ def flush_wgrad() -> None:
     for w, dys, xs in queue.values():
         k = kernels_for(dys[0])
         # a single-process Pipe queues weights of several devices: launch each on its own
-        with torch.cuda.device(dys[0].device):
+        dev = dys[0].device
+        with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
             if xs is None:  # a bias
                 k.column_sum_segments(dys, w.main_grad, True)
             else:
@@ -293,6 +300,23 @@ def begin_deferred_wgrad() -> bool:
         return False
     _DEFERRED = {}
     return True
+
+
+def deferred_param_ids() -> set:
+    """ids of the weights/biases with queued gradient GEMMs (empty when none)."""
+    return set(_DEFERRED) if _DEFERRED else set()
+
+
+def drop_deferred_wgrad(param_ids: Optional[set] = None) -> None:
+    """Discards queued weight gradients without running them: those of
+    ``param_ids`` (the deferral stays active), or the whole queue and the
+    deferral itself when ``param_ids`` is None."""
+    global _DEFERRED
+    if param_ids is None:
+        _DEFERRED = None
+    elif _DEFERRED:
+        for key in param_ids:
+            _DEFERRED.pop(key, None)
 
 
 def end_deferred_wgrad() -> None:

@@ -114,8 +114,13 @@ class FlatAdam:
         MIPIPE_LAZY_ZERO=0."""
         if lazy is None:
             lazy = os.environ.get("MIPIPE_LAZY_ZERO", "1") != "0"
-        if self._deferring:  # a backward whose gradients were never read: drop its queue
-            self.fold_grads()
+        # A backward whose gradients were never read: discard what it queued
+        # for this optimizer's parameters (without running the GEMMs).
+        from .ops.linear import deferred_param_ids, drop_deferred_wgrad
+
+        mine = self._param_ids()
+        if mine & deferred_param_ids():
+            drop_deferred_wgrad(mine)
         for g in self.groups:
             if lazy and g.n_lazy:
                 g.main_grad[g.n_lazy:].zero_()
@@ -127,20 +132,31 @@ class FlatAdam:
                     p._mg_fresh = False  # type: ignore[attr-defined]
             for p in g.params:
                 p.grad = None
-        if self.defer_wgrad:
+        if self.defer_wgrad and not self._deferring:
             from .ops.linear import begin_deferred_wgrad
 
+            # False when another optimizer's deferral is active: the queue is
+            # shared, and fold_grads() flushes it when it holds our weights.
             self._deferring = begin_deferred_wgrad()
+
+    def _param_ids(self) -> set:
+        return {id(p) for g in self.groups for p in g.params}
 
     def fold_grads(self) -> None:
         """Adds any autograd ``.grad`` (ops without main_grad support) into
         main_grad and zeroes lazily-zeroed gradients nothing wrote this step
-        (after running deferred weight-gradient GEMMs, with ``defer_wgrad``)."""
-        if self._deferring:
-            from .ops.linear import end_deferred_wgrad
+        (after running deferred weight-gradient GEMMs, with ``defer_wgrad``).
 
+        The deferral queue is process-wide: the optimizer that opened it ends
+        it here; any other optimizer whose weights sit in it flushes the queue
+        (running every queued GEMM) and leaves the deferral open."""
+        from .ops.linear import deferred_param_ids, end_deferred_wgrad, flush_wgrad
+
+        if self._deferring:
             self._deferring = False
             end_deferred_wgrad()
+        elif self._param_ids() & deferred_param_ids():
+            flush_wgrad()
         with torch.no_grad():
             for g in self.groups:
                 for p in g.params:

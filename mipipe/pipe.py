@@ -118,20 +118,62 @@ def _flatten_partition(layers: List[nn.Module]) -> PipeSequential:
     return PipeSequential(*flat)
 
 
-def _split_module(module: nn.Sequential) -> Tuple[List[nn.Sequential], List[torch.device]]:
-    """Groups consecutive children by device; each CPU child is its own group."""
-    groups: List[Tuple[torch.device, List[nn.Module]]] = []
+def _placed_children(module: nn.Sequential) -> List[Tuple[Optional[torch.device], nn.Module]]:
+    """(device, child) per child; ``WithDevice`` children are moved to their
+    device.  The device is ``None`` for a child with no parameters or buffers
+    that is not pinned (an activation, a reshape): it runs wherever its
+    partition runs."""
+    out: List[Tuple[Optional[torch.device], nn.Module]] = []
     for _, child in module.named_children():
         if isinstance(child, WithDevice):
-            device = child.device
+            device: Optional[torch.device] = child.device
             child = child.module
             child.to(device)
+        elif next(iter(child.parameters()), None) is None and next(iter(child.buffers()), None) is None:
+            device = None
         else:
             device = _module_device(child)
-        if groups and groups[-1][0] == device and device.type != "cpu":
-            groups[-1][1].append(child)
-        else:
-            groups.append((device, [child]))
+        out.append((device, child))
+    return out
+
+
+def _split_module(module: nn.Sequential, balance: Optional[List[int]] = None
+                  ) -> Tuple[List[nn.Sequential], List[torch.device]]:
+    """Splits ``module`` into partitions.
+
+    Without ``balance`` (the reference rule, ``/root/reference/pipe.py:191-218``):
+    consecutive children on the same device form one partition and every CPU
+    child is its own.  With ``balance`` (torchgpipe's explicit split): partition
+    ``k`` is the next ``balance[k]`` children, which must share one device --
+    several partitions may then sit on the SAME GPU, each computing on a stream
+    of its own, with real stage boundaries (copy streams, Copy/Wait) between
+    them."""
+    placed = _placed_children(module)
+    if balance is None:
+        groups: List[Tuple[torch.device, List[nn.Module]]] = []
+        for device, child in placed:
+            device = device if device is not None else torch.device("cpu")
+            if groups and groups[-1][0] == device and device.type != "cpu":
+                groups[-1][1].append(child)
+            else:
+                groups.append((device, [child]))
+    else:
+        balance = [int(b) for b in balance]
+        if any(b <= 0 for b in balance):
+            raise BalanceError(f"all balance numbers must be positive integer (balance: {balance})")
+        if sum(balance) != len(placed):
+            raise BalanceError(f"module and sum of balance have different length "
+                               f"(module: {len(placed)}, sum of balance: {sum(balance)})")
+        groups = []
+        start = 0
+        for k, b in enumerate(balance):
+            chunk = placed[start:start + b]
+            start += b
+            devs = {d for d, _ in chunk if d is not None}
+            if len(devs) > 1:
+                raise ValueError(f"partition {k} of balance {balance} spans several devices: "
+                                 f"{sorted(str(d) for d in devs)}")
+            groups.append((devs.pop() if devs else torch.device("cpu"), [c for _, c in chunk]))
     partitions = cast(List[nn.Sequential], nn.ModuleList([_flatten_partition(layers) for _, layers in groups]))
     devices = [d for d, _ in groups]
     return partitions, devices
@@ -170,6 +212,26 @@ def _enable_peer_access(devices: List[torch.device]) -> None:
         rt.enable_peer_access(indices)
 
 
+def _check_queues_for_shared_gpu(streams: int) -> None:
+    """Warns when the stage and copy streams of partitions sharing a GPU will
+    alias onto few in-order hardware queues: HIP maps streams onto
+    ``GPU_MAX_HW_QUEUES`` queues (default 4), and two stage streams on one
+    queue run in submission order -- the stages then do not overlap
+    (``profiles/hw_queue_sharing.txt``).  Read at HIP initialisation."""
+    import os
+    import warnings
+
+    try:
+        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    except ValueError:
+        q = 4
+    if q < min(streams, 16):
+        warnings.warn(f"mipipe Pipe: several partitions share a GPU with GPU_MAX_HW_QUEUES={q}; their stage "
+                      f"streams may share in-order hardware queues and not overlap -- export "
+                      f"GPU_MAX_HW_QUEUES={min(streams, 16)} before the process initialises HIP",
+                      RuntimeWarning, stacklevel=3)
+
+
 _MOVING_DENIED = "denied to move parameters and buffers, because Pipe should manage device placement"
 MOVING_DENIED = TypeError(_MOVING_DENIED)
 
@@ -191,6 +253,17 @@ class Pipe(nn.Module):
             A HIP process has few hardware queues (``GPU_MAX_HW_QUEUES``, 4 by
             default), so ``chunks x partitions`` streams alias onto the same
             queues anyway; see ``profiles/copy_streams_ab.txt``.
+        balance: explicit partition sizes (number of top-level children per
+            partition, torchgpipe style).  Lets several partitions share a
+            GPU; each later partition on a device computes on a dedicated
+            stream so neighbouring stages overlap.
+        copy_same_device: make a boundary between two partitions of the same
+            GPU a real device-to-device copy on the copy streams (the native
+            ``peer_copy`` path a multi-GPU boundary takes) instead of handing
+            the tensor over in place.
+        copy_engine: ``"sdma"`` (DMA engines, default) or ``"blit"`` (a copy
+            kernel) for native stage transfers; ``None`` reads
+            ``$MIPIPE_COPY_ENGINE``.
     """
 
     def __init__(
@@ -202,6 +275,9 @@ class Pipe(nn.Module):
         *,
         return_rref: bool = True,
         copy_streams: Optional[int] = None,
+        balance: Optional[List[int]] = None,
+        copy_same_device: bool = False,
+        copy_engine: Optional[str] = None,
     ) -> None:
         super().__init__()
         chunks = int(chunks)
@@ -224,17 +300,29 @@ class Pipe(nn.Module):
         if deferred_batch_norm:
             module = DeferredBatchNorm.convert_deferred_batch_norm(module, chunks)
 
-        self.partitions, self.devices = _split_module(module)
+        from .copy import COPY_ENGINES
+
+        if copy_engine is not None and copy_engine not in COPY_ENGINES:
+            raise ValueError(f"copy_engine must be one of {sorted(COPY_ENGINES)}, got {copy_engine!r}")
+        self.copy_same_device = bool(copy_same_device)
+        self.copy_engine = copy_engine
+
+        self.partitions, self.devices = _split_module(module, balance)
         _verify_splitting(module, self.partitions, self.devices)
         _enable_peer_access(self.devices)
 
         self._copy_streams: List[List[AbstractStream]] = []
         self._skip_layout: SkipLayout = inspect_skip_layout(self.partitions)
         copy_streams = self._ensure_copy_streams()
+        self._compute_streams = self._ensure_compute_streams()
+        if any(st is not None for st in self._compute_streams):
+            _check_queues_for_shared_gpu(len(self.partitions) * (1 + self.chunks))
 
         # The pipeline derives the checkpoint boundary from the actual number of
         # micro-batches at run time (see pipeline.checkpoint_stop_for).
-        self.pipeline = Pipeline(self.partitions, self.devices, copy_streams, self._skip_layout, checkpoint)
+        self.pipeline = Pipeline(self.partitions, self.devices, copy_streams, self._skip_layout, checkpoint,
+                                 compute_streams=self._compute_streams, copy_same_device=self.copy_same_device,
+                                 copy_engine=copy_engine)
 
     # -- sequence façade -------------------------------------------------------
     def __len__(self) -> int:
@@ -279,6 +367,24 @@ class Pipe(nn.Module):
                     pool = [new_stream(device) for _ in range(min(k, self.chunks))]
                     self._copy_streams.append([pool[i % len(pool)] for i in range(self.chunks)])
         return self._copy_streams
+
+    def _ensure_compute_streams(self) -> List[Optional[AbstractStream]]:
+        """Compute stream per partition: ``None`` (= the device's current
+        stream, the reference's choice, ``/root/reference/pipeline.py:158``)
+        for the first partition on each device, a dedicated stream for every
+        later partition on the same GPU -- two stages of one GPU must not
+        share an in-order stream, or micro-batch i+1 of stage j-1 could never
+        overlap micro-batch i of stage j."""
+        seen = set()
+        out: List[Optional[AbstractStream]] = []
+        for device in self.devices:
+            key = (device.type, device.index if device.index is not None else -1)
+            if device.type == "cuda" and key in seen:
+                out.append(new_stream(device))
+            else:
+                out.append(None)
+            seen.add(key)
+        return out
 
     def close(self) -> None:
         self.pipeline.close()

@@ -35,7 +35,7 @@ import torch
 from torch import nn
 
 from .checkpoint import Checkpointing
-from .copy import Copy, Wait
+from .copy import Copy, Wait, transfer_policy
 from .dependency import fork, join
 from .microbatch import Batch
 from .skip.layout import SkipLayout
@@ -113,10 +113,18 @@ class Pipeline:
         copy_streams: Sequence[Sequence[AbstractStream]],
         skip_layout: SkipLayout,
         checkpoint_stop: Union[int, str],
+        compute_streams: Optional[Sequence[Optional[AbstractStream]]] = None,
+        copy_same_device: bool = False,
+        copy_engine: Optional[str] = None,
     ) -> None:
         self.partitions = partitions
         self.devices = list(devices)
         self.copy_streams = copy_streams
+        # per partition: None = the device's current stream at run time
+        self.dedicated_streams: List[Optional[AbstractStream]] = (
+            list(compute_streams) if compute_streams is not None else [None] * len(self.devices))
+        self.copy_same_device = copy_same_device
+        self.copy_engine = copy_engine
         self.skip_layout = skip_layout
         self.checkpoint = checkpoint_stop
         self.in_queues, self.out_queues, entries = create_workers(self.devices)
@@ -141,11 +149,22 @@ class Pipeline:
         if not self.partitions[0].training:
             stop = 0
         trackers = [SkipTrackerThroughPortals(self.skip_layout) for _ in batches]
-        for cells in clock_cycles(m, n):
-            self.fence(batches, cells, trackers)
-            self.compute(batches, cells, trackers, stop)
-            if self.sync_debug:
-                synchronize_all(self.devices)
+        with transfer_policy(self.copy_same_device, self.copy_engine):
+            for cells in clock_cycles(m, n):
+                self.fence(batches, cells, trackers)
+                self.compute(batches, cells, trackers, stop)
+                if self.sync_debug:
+                    synchronize_all(self.devices)
+        last = self.dedicated_streams[n - 1]
+        if last is not None:
+            # The caller reads the output on the device's current stream.
+            out_stream = current_stream(self.devices[n - 1])
+            for batch in batches:
+                _wait(batch, last, out_stream)
+
+    def compute_streams(self) -> List[AbstractStream]:
+        """The stream each partition computes on (for this thread)."""
+        return [s if s is not None else current_stream(d) for s, d in zip(self.dedicated_streams, self.devices)]
 
     def fence(self, batches: List[Batch], cells: List[Cell], trackers: List[SkipTrackerThroughPortals]) -> None:
         """Dependencies and copies that must precede this tick's computation."""
@@ -177,7 +196,7 @@ class Pipeline:
             checkpoint_stop = checkpoint_stop_for(self.checkpoint, len(batches))
             if not partitions[0].training:
                 checkpoint_stop = 0
-        compute_streams = [current_stream(d) for d in devices]
+        compute_streams = self.compute_streams()
 
         for i, j in cells:
             batch = batches[i]

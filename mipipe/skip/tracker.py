@@ -22,7 +22,7 @@ from torch import Tensor
 from ..checkpoint import is_checkpointing
 from ..dependency import fork, join
 from ..microbatch import Batch
-from ..stream import AbstractStream
+from ..stream import AbstractStream, current_stream, record_stream
 from .layout import SkipLayout
 from .namespace import Namespace
 from .portal import Portal
@@ -92,7 +92,12 @@ class SkipTrackerThroughPortals(SkipTracker):
         portal = self.portals[(ns, name)]
         idx = batch.find_tensor_idx()
         batch[idx], phony = fork(batch[idx])
-        return portal.orange(phony)
+        tensor = portal.orange(phony)
+        if tensor is not None and tensor.is_cuda:
+            # popped on this partition's compute stream, which may not be the
+            # stream the portal copy recorded (a dedicated same-GPU stage stream)
+            record_stream(tensor, current_stream(tensor.device))
+        return tensor
 
     def copy(
         self, batch: Batch, prev_stream: AbstractStream, next_stream: AbstractStream, ns: Optional[Namespace], name: str

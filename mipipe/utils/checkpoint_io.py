@@ -13,9 +13,11 @@ is gathered), in safetensors, whose loader executes nothing from the file:
   metadata so a resume into a different partition fails loudly instead of
   scrambling moments;
 * ``adam.<name>.{exp_avg,exp_avg_sq,step}`` -- ``torch.optim.Adam`` state;
-* ``rng.cpu`` / ``rng.cuda.<i>`` -- generator states, so dropout masks after a
-  resume are the ones the uninterrupted run would have drawn (the HIP dropout
-  kernels take their Philox seed/offset from the torch generator).
+* ``rng.cpu`` / ``rng.cuda.local.<k>`` -- generator states, so dropout masks
+  after a resume are the ones the uninterrupted run would have drawn (the HIP
+  dropout kernels take their Philox seed/offset from the torch generator).
+  ``k`` is the position of the GPU among this rank's parameter devices (sorted),
+  so a file saved by a replica on cuda:0 restores onto a replica on cuda:4.
 
 A resumed run is bit-identical to the uninterrupted one
 (``tests/test_checkpoint_io.py``).  Data-parallel replicas hold identical
@@ -43,6 +45,12 @@ def rank_path(directory: str, rank: int) -> str:
 def _host(t: Tensor) -> Tensor:
     t = t.detach()
     return t.to("cpu") if t.device.type != "cpu" else t.clone()
+
+
+def _cuda_devices(params: Iterable[nn.Parameter]) -> list:
+    """Sorted indices of the GPUs holding ``params``."""
+    return sorted({p.device.index if p.device.index is not None else torch.cuda.current_device()
+                   for p in params if p.device.type == "cuda"})
 
 
 def _named(params: Iterable[Tuple[str, nn.Parameter]]) -> Dict[str, nn.Parameter]:
@@ -94,9 +102,11 @@ def save_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
     if rng:
         tensors["rng.cpu"] = torch.get_rng_state()
         if torch.cuda.is_available():
-            devs = sorted({p.device.index for p in params.values() if p.device.type == "cuda"})
-            for d in devs:
-                tensors[f"rng.cuda.{d}"] = torch.cuda.get_rng_state(d)
+            # keyed by position among this rank's parameter devices, not by
+            # device index: a replica on another GPU (cuda:4+s for stage s)
+            # restores the state onto ITS k-th device
+            for k, d in enumerate(_cuda_devices(params.values())):
+                tensors[f"rng.cuda.local.{k}"] = torch.cuda.get_rng_state(d)
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     tmp = path + ".tmp"
     save_file({k: v.contiguous() for k, v in tensors.items()}, tmp, metadata={"mipipe": json.dumps(meta)})
@@ -167,7 +177,14 @@ def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
             grp["lr"] = lr
     if rng and "rng.cpu" in tensors:
         torch.set_rng_state(tensors["rng.cpu"])
-        for key, st in tensors.items():
-            if key.startswith("rng.cuda.") and torch.cuda.is_available():
-                torch.cuda.set_rng_state(st, int(key.rsplit(".", 1)[1]))
+        if torch.cuda.is_available():
+            local = sorted((int(k.rsplit(".", 1)[1]), k) for k in tensors if k.startswith("rng.cuda.local."))
+            if not local:  # files written before the device-independent keys: by saved index order
+                local = sorted((int(k.rsplit(".", 1)[1]), k) for k in tensors if k.startswith("rng.cuda."))
+            mine = _cuda_devices(params.values())
+            if len(local) != len(mine):
+                raise ValueError(f"{path}: RNG states for {len(local)} GPU(s), this rank's parameters are on "
+                                 f"{len(mine)}")
+            for d, (_, key) in zip(mine, local):
+                torch.cuda.set_rng_state(tensors[key], d)
     return {"step": meta.get("step", 0), "extra": meta.get("extra", {})}

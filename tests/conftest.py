@@ -1,6 +1,14 @@
 import os
 import sys
 
+# Stage and copy streams of a multi-partition Pipe on one GPU must not alias
+# onto shared in-order hardware queues (HIP's default is 4; see
+# profiles/hw_queue_sharing.txt): read by HIP at initialisation, so set it
+# before anything touches the GPU.  The GPU boxes export HIP's default (4)
+# explicitly; any other explicit setting wins.
+if os.environ.get("GPU_MAX_HW_QUEUES", "4") in ("", "4"):
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import pytest
 import torch
 

@@ -100,3 +100,27 @@ def test_load_weights_and_layout_check(tmp_path):
 
         save_file({"x": torch.zeros(1)}, str(tmp_path / "foreign.safetensors"))
         load_weights(str(tmp_path / "foreign.safetensors"), other.named_parameters())
+
+
+def test_rng_restores_onto_loaders_own_gpu(tmp_path, monkeypatch):
+    """A file saved by a replica on cuda:0 restores the GPU generator of a
+    replica whose parameters live on cuda:4: keys are positions
+    among the rank's parameter devices, not device indices."""
+    import mipipe.utils.checkpoint_io as cio
+
+    lin = torch.nn.Linear(4, 4)
+    states = {0: torch.arange(16, dtype=torch.uint8), 4: torch.zeros(16, dtype=torch.uint8)}
+    restored = {}
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "get_rng_state", lambda d: states[d].clone())
+    monkeypatch.setattr(torch.cuda, "set_rng_state", lambda st, d: restored.__setitem__(d, st.clone()))
+    monkeypatch.setattr(cio, "_cuda_devices", lambda params: [0])
+    path = rank_path(str(tmp_path), 0)
+    save_training_state(path, lin.named_parameters(), None)
+    monkeypatch.setattr(cio, "_cuda_devices", lambda params: [4])
+    load_training_state(path, lin.named_parameters(), None)
+    assert list(restored) == [4]
+    assert torch.equal(restored[4], states[0])
+    monkeypatch.setattr(cio, "_cuda_devices", lambda params: [4, 5])
+    with pytest.raises(ValueError, match="RNG states for 1 GPU"):
+        load_training_state(path, lin.named_parameters(), None)

@@ -239,8 +239,9 @@ def test_roctx_ranges(k):
 
 
 def test_pipe_on_one_gpu_two_partitions(k):
-    """Single-process Pipe with two partitions on the same GPU (copy streams,
-    Wait events, recompute) matches nn.Sequential."""
+    """Single-process Pipe with two partitions on the same GPU (balance=[1, 1]:
+    copy streams, native D2D boundary copies, Wait events, a dedicated stream
+    for the second stage, recompute) matches nn.Sequential."""
     import copy
 
     from torch import nn
@@ -256,7 +257,8 @@ def test_pipe_on_one_gpu_two_partitions(k):
     for mode in ("never", "always"):
         seq.zero_grad()
         ref.zero_grad()
-        pipe = Pipe(seq, chunks=4, checkpoint=mode)
+        pipe = Pipe(seq, chunks=4, checkpoint=mode, balance=[1, 1], copy_same_device=True)
+        assert len(pipe.partitions) == 2
         out = pipe(x).local_value()
         assert torch.allclose(out, ref(x), atol=1e-5)
         out.sum().backward()

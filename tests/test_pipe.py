@@ -2,6 +2,7 @@
 
 Every CPU child becomes its own partition, so these run real multi-stage
 pipelines with no GPU (SURVEY §4 'CPU devices as a fake backend')."""
+import copy
 from collections import OrderedDict
 import time
 
@@ -495,3 +496,80 @@ def test_shared_params_same_device_ok():
     model = nn.Sequential(lin, nn.Sequential(lin))
     # Both on CPU -> each its own partition, but same device -> allowed.
     Pipe(model)
+
+
+# ------------------------------------------------------------------ explicit balance
+def test_balance_groups_children():
+    """balance=[2, 2]: two partitions of two children each (the reference rule
+    alone would make four CPU partitions)."""
+    model = nn.Sequential(nn.Linear(4, 4), nn.ReLU(), nn.Linear(4, 4), nn.Linear(4, 4))
+    pipe = Pipe(model, chunks=2, balance=[2, 2])
+    assert len(pipe.partitions) == 2
+    assert [len(p) for p in pipe.partitions] == [2, 2]
+    assert len(Pipe(model, chunks=2).partitions) == 4
+    pipe.close()
+
+
+@pytest.mark.parametrize("balance", [[1, 1], [2, 3], [0, 4], [-1, 5]])
+def test_balance_errors(balance):
+    from mipipe import BalanceError
+
+    model = nn.Sequential(*[nn.Linear(2, 2) for _ in range(4)])
+    with pytest.raises(BalanceError):
+        Pipe(model, balance=balance)
+
+
+def test_balance_partition_spanning_devices():
+    model = nn.Sequential(nn.Linear(2, 2), nn.Linear(2, 2, device="meta"))
+    with pytest.raises(ValueError, match="spans several devices"):
+        Pipe(model, balance=[2])
+
+
+def test_balance_parameterless_child_joins_partition():
+    """An unpinned activation has no device of its own: it runs in its partition."""
+    model = nn.Sequential(nn.Linear(2, 2), nn.ReLU(), nn.Linear(2, 2))
+    pipe = Pipe(model, chunks=1, balance=[2, 1])
+    assert [type(m) for m in pipe.partitions[0]] == [nn.Linear, nn.ReLU]
+    pipe.close()
+
+
+@pytest.mark.parametrize("checkpoint", ["never", "except_last", "always"])
+@pytest.mark.parametrize("balance", [[1, 2, 1], [2, 2], [4]])
+def test_balance_transparency(checkpoint, balance):
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(8, 8), nn.Tanh(), nn.Linear(8, 8), nn.Linear(8, 4))
+    ref = copy.deepcopy(model)
+    x = torch.randn(12, 8)
+    pipe = Pipe(model, chunks=3, checkpoint=checkpoint, balance=balance, copy_same_device=True)
+    assert len(pipe.partitions) == len(balance)
+    out = pipe(x).local_value()
+    out.sum().backward()
+    y = ref(x)
+    y.sum().backward()
+    assert torch.allclose(out, y, atol=1e-6)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(p.grad, q.grad, atol=1e-6)
+    pipe.close()
+
+
+def test_copy_engine_validation():
+    with pytest.raises(ValueError, match="copy_engine"):
+        Pipe(nn.Sequential(nn.Linear(2, 2)), copy_engine="tcp")
+
+
+def test_transfer_policy_kept_for_backward():
+    """Copy keeps the policy in force at forward for its backward (which runs
+    later on an autograd thread, outside the pipeline's context)."""
+    from mipipe.copy import Copy, current_policy, transfer_policy
+    from mipipe.stream import CPUStream
+
+    x = torch.randn(3, requires_grad=True)
+    with transfer_policy(True, "blit"):
+        assert current_policy() == (True, 1)
+        (y,) = Copy.apply(CPUStream, CPUStream, x)
+    assert current_policy()[0] is False
+    y.sum().backward()
+    assert torch.equal(x.grad, torch.ones(3))
+    with pytest.raises(ValueError):
+        with transfer_policy(True, "pcie"):
+            pass

@@ -1,8 +1,8 @@
 """Pipe copy-stream layouts on one MI355X: the reference's one copy stream per (partition, micro-batch)
 (``copy_streams=None``, /root/reference/pipe.py:417-429) against a pool of k streams per partition.
 
-All partitions sit on cuda:0 (a one-GPU box), so the boundary copies are same-device copies on the copy
-streams; what differs between the arms is only how many HIP streams the copies and their waits are spread
+All partitions sit on cuda:0 (a one-GPU box, ``balance=``), so the boundary copies are same-device native
+copies on the copy streams (``copy_same_device=True``); what differs between the arms is only how many HIP streams the copies and their waits are spread
 over, which a process maps onto its GPU_MAX_HW_QUEUES (4) hardware queues.  Arms alternate, medians of the
 step times are reported.
 
@@ -46,7 +46,11 @@ def step(pipe):
 
 
 arms = {"per (partition, micro-batch)": None, "pool k=1": 1, "pool k=2": 2, "pool k=4": 4}
-pipes = {name: Pipe(model, chunks=M, checkpoint="never", copy_streams=k) for name, k in arms.items()}
+# balance=[1]*P: one partition per part even though they share cuda:0 (without it the
+# reference's split rule merges same-device children into ONE partition: no boundaries)
+pipes = {name: Pipe(model, chunks=M, checkpoint="never", copy_streams=k, balance=[1] * len(parts),
+                    copy_same_device=True) for name, k in arms.items()}
+assert all(len(p.partitions) == len(parts) for p in pipes.values())
 times = {name: [] for name in arms}
 for _ in range(2):  # warm-up
     for pipe in pipes.values():
