@@ -16,6 +16,7 @@
 #include <tuple>
 
 #include "kernels/kernels.h"
+#include "runtime/ipc.h"
 #include "runtime/runtime.h"
 
 namespace py = pybind11;
@@ -790,6 +791,20 @@ void py_adam(Tensor master, std::optional<Tensor> model, Tensor grad, Tensor m, 
 }  // namespace
 }  // namespace mipipe
 
+// ------------------------------------------------------------------ ipc links
+// Python face of mipipe::ipc::Link (runtime/ipc.h).  Host-blocking calls drop
+// the GIL so watchdog threads keep running while a rank waits for its peer.
+namespace {
+
+namespace ipc = mipipe::ipc;
+
+void ipc_check_tensor(const Tensor& t, const ipc::Link& L) {
+  MP_CHECK(t.is_contiguous(), "ipc link: tensors must be contiguous");
+  MP_CHECK(L.host_mode() ? !t.is_cuda() : t.is_cuda(), "ipc link: host links move CPU tensors, device links GPU tensors");
+}
+
+}  // namespace
+
 // Defined in the build-generated source_digest.cpp (mipipe/build.py): the
 // digest of the sources this binary was compiled from, checked at import by
 // mipipe/_native_loader.py.
@@ -797,6 +812,41 @@ extern "C" const char* mipipe_source_digest();
 
 PYBIND11_MODULE(_C, m) {
   m.def("source_digest", []() { return std::string(mipipe_source_digest()); });
+  py::class_<ipc::Link>(m, "IpcLink")
+      .def_static("create", &ipc::Link::create, py::arg("name"), py::arg("device"), py::arg("nslots"),
+                  py::arg("slot_bytes"), py::arg("ipc_events") = true)
+      .def_static("attach", &ipc::Link::attach, py::arg("name"), py::arg("device"), py::arg("engine") = 0,
+                  py::arg("timeout") = 60.0, py::call_guard<py::gil_scoped_release>())
+      .def("send",
+           [](ipc::Link& L, Tensor src, int64_t producer, double timeout) {
+             ipc_check_tensor(src, L);
+             const void* p = src.data_ptr();
+             const size_t n = src.nbytes();
+             py::gil_scoped_release nogil;
+             return L.send(p, n, reinterpret_cast<hipStream_t>(producer), timeout);
+           },
+           py::arg("src"), py::arg("producer_stream"), py::arg("timeout") = 300.0)
+      .def("post", &ipc::Link::post)
+      .def("wait",
+           [](ipc::Link& L, uint64_t seq, Tensor dst, int64_t consumer, double timeout) {
+             ipc_check_tensor(dst, L);
+             void* p = dst.data_ptr();
+             const size_t n = dst.nbytes();
+             py::gil_scoped_release nogil;
+             L.wait(seq, p, n, reinterpret_cast<hipStream_t>(consumer), timeout);
+           },
+           py::arg("seq"), py::arg("dst"), py::arg("consumer_stream"), py::arg("timeout") = 300.0)
+      .def("done", &ipc::Link::done)
+      .def("abort", &ipc::Link::abort)
+      .def("unlink", &ipc::Link::unlink)
+      .def("describe", &ipc::Link::describe)
+      .def_property_readonly("copy_stream", [](const ipc::Link& L) { return reinterpret_cast<int64_t>(L.copy_stream()); })
+      .def_property_readonly("nslots", &ipc::Link::nslots)
+      .def_property_readonly("slot_bytes", &ipc::Link::slot_bytes)
+      .def_property_readonly("ipc_events", &ipc::Link::ipc_events)
+      .def_property_readonly("host_mode", &ipc::Link::host_mode)
+      .def_property_readonly("is_sender", &ipc::Link::is_sender);
+  m.def("ipc_proxy_shutdown", &ipc::proxy_shutdown, py::call_guard<py::gil_scoped_release>());
   using namespace mipipe;
   m.doc() = "mipipe native runtime + CDNA4 HIP kernels (gfx950)";
   // runtime

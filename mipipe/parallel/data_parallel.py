@@ -171,10 +171,13 @@ class PPDPGroups:
         self.replica, self.stage = replica, stage
 
 
-def make_pp_dp_groups(pp: int, dp: int, wrap: bool = False) -> PPDPGroups:
+def make_pp_dp_groups(pp: int, dp: int, wrap: bool = False, *, transport: str = "rccl",
+                      ipc_options: Optional[dict] = None) -> PPDPGroups:
     """Creates every pipeline's channels, every pipeline group and every
     data-parallel group (``dist.new_group`` is collective: all ranks create all
-    of them, in one order) and returns this rank's."""
+    of them, in one order) and returns this rank's.  ``transport="ipc"``
+    builds :class:`~mipipe.parallel.ipc.IpcChannels` (``ipc_options`` needs
+    ``device`` and ``recv_bytes``) instead of RCCL channels."""
     world = dist.get_world_size()
     if pp * dp != world:
         raise ValueError(f"pp {pp} x dp {dp} != world size {world}")
@@ -183,7 +186,12 @@ def make_pp_dp_groups(pp: int, dp: int, wrap: bool = False) -> PPDPGroups:
     mine_ch = mine_pg = mine_dg = None
     for d in range(dp):
         ranks = list(range(d * pp, (d + 1) * pp))
-        ch = Channels(ranks, wrap=wrap and pp > 1)
+        if transport == "ipc":
+            from .ipc import IpcChannels
+
+            ch = IpcChannels(ranks, wrap=wrap and pp > 1, **(ipc_options or {}))
+        else:
+            ch = Channels(ranks, wrap=wrap and pp > 1)
         if d == replica:
             mine_ch = ch
     for d in range(dp):

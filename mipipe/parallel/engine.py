@@ -55,6 +55,7 @@ from .. import ops
 from ..checkpoint import enable_checkpointing, enable_recomputing
 from ..pipeline import checkpoint_stop_for
 from ..skip.tracker import use_skip_tracker
+from ..worker import label_range
 from .p2p import Channels, DirectLinks
 from .skips import EngineSkipTracker, SkipRoute, gather_routes
 from .watchdog import Watchdog
@@ -149,6 +150,12 @@ class PipelineEngine:
         grad_divisor: the backward is seeded with ``loss / (chunks * grad_divisor)``;
             data-parallel replicas pass their count, so the gradient all-reduce
             SUM is the mean (:mod:`mipipe.parallel.data_parallel`).
+        transport: how activations and gradients move between ranks when the
+            engine builds its own channels: ``"rccl"`` (send/recv of the
+            process group; default) or ``"ipc"`` (device-memory IPC links,
+            :class:`~mipipe.parallel.ipc.IpcChannels`: DMA copies into the
+            receiver's slots, no RCCL kernels; works with several ranks on
+            one GPU).  ``transport_options`` go to the IpcChannels.
     """
 
     def __init__(
@@ -170,6 +177,8 @@ class PipelineEngine:
         watchdog: Union[None, float, Watchdog] = None,
         sync_debug: Optional[bool] = None,
         grad_divisor: float = 1.0,
+        transport: str = "rccl",
+        transport_options: Optional[dict] = None,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
             raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
@@ -203,16 +212,25 @@ class PipelineEngine:
         # step run this way with a scheduled one
         self.sync_debug = (os.environ.get("MIPIPE_SYNC_DEBUG") == "1") if sync_debug is None else bool(sync_debug)
         self._action = "construction"
-        if isinstance(group, Channels):
+        if isinstance(group, Channels) or hasattr(group, "send_act"):  # ready channels (RCCL or IPC)
             self.chan: Optional[Channels] = group
             if group.world > 1:
                 with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
                     group.warmup(device or next(mods[0].parameters()).device)
         elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
-            self.chan = Channels(ranks, wrap=self.virtual > 1)
-            with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
-                self.chan.warmup(device or next(mods[0].parameters()).device)
+            dev = device or next(mods[0].parameters()).device
+            if transport == "ipc":
+                from .ipc import IpcChannels
+
+                self.chan = IpcChannels(ranks, wrap=self.virtual > 1, device=dev,
+                                        recv_bytes=self.recv_bytes(), **(transport_options or {}))
+            elif transport == "rccl":
+                self.chan = Channels(ranks, wrap=self.virtual > 1)
+                with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
+                    self.chan.warmup(dev)
+            else:
+                raise ValueError(f"transport must be 'rccl' or 'ipc', got {transport!r}")
         else:
             self.chan = None
         if self.chan is not None:
@@ -232,6 +250,12 @@ class PipelineEngine:
         if self.watchdog is not None and self.watchdog.describe is None:
             self.watchdog.describe = self.describe
         self._setup_skips(group, skip_shapes, skip_routes)
+
+    def recv_bytes(self) -> int:
+        """Largest activation (bytes) this rank receives per micro-batch."""
+        item = torch.empty((), dtype=self.act_dtype).element_size()
+        sizes = [int(torch.Size(s).numel()) * item for s in self.act_shapes]
+        return max(sizes) if sizes else 0
 
     # ------------------------------------------------------------------ watchdog
     def describe(self) -> str:
@@ -254,7 +278,7 @@ class PipelineEngine:
         """Cross-stage skip routes, the per-chunk key lists and the direct links."""
         if skip_routes is not None:
             routes = dict(skip_routes)
-        elif self.chan is not None and not isinstance(group, Channels):
+        elif self.chan is not None and not (isinstance(group, Channels) or hasattr(group, "send_act")):
             routes = gather_routes(self.modules, self.vstage, self.act_shapes, self.act_dtype, group=group,
                                    skip_shapes=skip_shapes)
         else:
@@ -344,6 +368,18 @@ class PipelineEngine:
     def step(self, inputs: Optional[Sequence[Tensor]] = None, targets: Optional[Sequence[Tensor]] = None) -> StepStats:
         """Forward + backward of one mini-batch given as per-micro-batch lists.
 
+        Every action is a roctx range (``F vs<s> mb<i>``, ``B ...``,
+        ``recompute ...``, ``wait recv act/grad ...``, ``post recvs``, ``wgrad
+        flush``, ``wait sends``) inside one ``engine step`` range, so a
+        rocprofv3 ``--marker-trace`` timeline attributes every idle gap per
+        rank and micro-batch (``tools/engine_timeline.py``).
+        """
+        with label_range("engine step"):
+            return self._step(inputs, targets)
+
+    def _step(self, inputs: Optional[Sequence[Tensor]] = None, targets: Optional[Sequence[Tensor]] = None) -> StepStats:
+        """Forward + backward of one mini-batch given as per-micro-batch lists.
+
         ``inputs`` (rank owning virtual stage 0) and ``targets`` (rank owning
         the last virtual stage, and every rank whose chunks want targets) have
         ``chunks`` entries.  Gradients accumulate
@@ -364,12 +400,13 @@ class PipelineEngine:
         # order the upstream rank sends them (chunk-major, micro-batch minor).
         recv_x = [[None] * m for _ in range(v)]
         recv_w = [[None] * m for _ in range(v)]
-        for c in range(v):
-            if not self._first(c):
-                for i in range(m):
-                    recv_x[c][i] = self._new_act(c)
-                    recv_w[c][i] = self._track(f"recv activation: virtual stage {self.vstage[c]} micro-batch {i} "
-                                               f"from rank {(self.rank - 1) % n}", chan.recv_act(recv_x[c][i]))
+        with label_range("post recvs: activations"):
+            for c in range(v):
+                if not self._first(c):
+                    for i in range(m):
+                        recv_x[c][i] = self._new_act(c)
+                        recv_w[c][i] = self._track(f"recv activation: virtual stage {self.vstage[c]} micro-batch {i} "
+                                                   f"from rank {(self.rank - 1) % n}", chan.recv_act(recv_x[c][i]))
         # ... and every skip receive (each skip has its own directed link).
         sk_rx: Dict = {}
         sk_grad_rx: Dict = {}
@@ -433,7 +470,8 @@ class PipelineEngine:
             if self._first(c):
                 x = inputs[i]
             else:
-                recv_w[c][i].wait()
+                with label_range(f"wait recv act vs{self.vstage[c]} mb{i}"):
+                    recv_w[c][i].wait()
                 x = recv_x[c][i]
                 recv_x[c][i] = recv_w[c][i] = None
                 if training:
@@ -488,7 +526,7 @@ class PipelineEngine:
                 st = rng[c][i]
                 devices = [self.device] if self.device.type == "cuda" else []
                 tracker = skip_tracker(c, i)
-                with torch.random.fork_rng(devices=devices):
+                with label_range(f"recompute vs{self.vstage[c]} mb{i}"), torch.random.fork_rng(devices=devices):
                     torch.set_rng_state(st.cpu)
                     if st.dev is not None:
                         torch.cuda.set_rng_state(st.dev, self.device)
@@ -520,7 +558,8 @@ class PipelineEngine:
                     outs.append(t)
                     seeds.append(g)
             if not last:
-                grad_w[c][i].wait()
+                with label_range(f"wait recv grad vs{self.vstage[c]} mb{i}"):
+                    grad_w[c][i].wait()
             tm = self._timer()
             if tm:
                 tm[0].record()
@@ -561,23 +600,25 @@ class PipelineEngine:
                 self._mark(f"{'forward' if kind == 'F' else 'backward'} virtual stage {self.vstage[c]} "
                            f"micro-batch {i}")
                 if kind == "F":
-                    with torch.set_grad_enabled(training):
+                    with label_range(f"F vs{self.vstage[c]} mb{i}"), torch.set_grad_enabled(training):
                         forward(c, i)
                 else:
                     if not started_backward:
                         started_backward = True
                         if defer is not None:
                             defer.__enter__()
-                        if self.schedule == "gpipe":
-                            # Post all gradient receives of the drain phase at once,
-                            # in the downstream rank's send order (reverse).
-                            for cc in reversed(range(v)):
-                                for k in reversed(range(m)):
-                                    post_grad_recv(cc, k)
-                        if self._skip_links is not None:
-                            self._post_skip_recvs(sk_grad_rx, training, grad=True)
-                    post_grad_recv(c, i)
-                    backward(c, i)
+                        with label_range("post recvs: gradients"):
+                            if self.schedule == "gpipe":
+                                # Post all gradient receives of the drain phase at once,
+                                # in the downstream rank's send order (reverse).
+                                for cc in reversed(range(v)):
+                                    for k in reversed(range(m)):
+                                        post_grad_recv(cc, k)
+                            if self._skip_links is not None:
+                                self._post_skip_recvs(sk_grad_rx, training, grad=True)
+                    with label_range(f"B vs{self.vstage[c]} mb{i}"):
+                        post_grad_recv(c, i)
+                        backward(c, i)
                 if self.sync_debug and self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
             if defer is not None and started_backward:
@@ -585,14 +626,16 @@ class PipelineEngine:
                 tm = self._timer()
                 if tm:
                     tm[0].record()
-                defer.__exit__(None, None, None)  # the deferred weight-gradient GEMMs
+                with label_range("wgrad flush"):
+                    defer.__exit__(None, None, None)  # the deferred weight-gradient GEMMs
                 defer = None
                 if tm:
                     tm[1].record()
                     events.append(("B", tm))
             self._mark("waiting for this step's sends")
-            for w in sends:
-                w.wait()
+            with label_range("wait sends"):
+                for w in sends:
+                    w.wait()
         except BaseException as exc:
             self._on_error(exc)
             raise
@@ -622,6 +665,9 @@ class PipelineEngine:
         import sys
 
         lines = [f"[mipipe engine] rank {self.rank}: {type(exc).__name__} during {self._action}: {exc}"]
+        abort = getattr(self.chan, "abort", None)
+        if abort is not None:
+            abort()  # peers blocked on this rank's IPC links fail fast instead of timing out
         if self.watchdog is not None:
             left = self.watchdog.pending.unfinished()
             if left:

@@ -30,9 +30,15 @@ ENGINE_CASES = [
 SKIP_PAIRS = [(0, 3), (1, 2)]
 
 
+# Modes: "cpu" (gloo, fp32), "nccl" (RCCL, one rank per GPU), "ipc_cpu" (gloo for
+# collectives, activations over shared-memory IPC links), "ipc_gpu" (every rank
+# on cuda:0, activations over device-memory IPC links -- mipipe.parallel.ipc).
+GPU_MODES = ("nccl", "ipc_gpu")
+
+
 def case_cfg(mode):
     base = CONFIGS["tiny"]
-    if mode == "nccl":  # HIP-kernel-sized shapes
+    if mode in GPU_MODES:  # HIP-kernel-sized shapes
         return dataclasses.replace(base, dropout=0.0, num_layers=4, d_model=256, nhead=4, dim_feedforward=512,
                                    vocab=512, seq_len=64)
     return dataclasses.replace(base, dropout=0.0, num_layers=4, d_model=32, nhead=4, dim_feedforward=64,
@@ -40,7 +46,7 @@ def case_cfg(mode):
 
 
 def _setting(mode):
-    if mode == "nccl":
+    if mode in GPU_MODES:
         return torch.bfloat16, 8, 2
     return torch.float32, 8, 2
 
@@ -64,7 +70,9 @@ def _port():
 
 
 def _device(mode, rank):
-    return torch.device("cuda", rank) if mode == "nccl" else torch.device("cpu")
+    if mode == "nccl":
+        return torch.device("cuda", rank)
+    return torch.device("cuda", 0) if mode == "ipc_gpu" else torch.device("cpu")
 
 
 def _grads(params, names):
@@ -75,16 +83,18 @@ def _grads(params, names):
     return out
 
 
-def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q):
+def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropout=0.0, seed=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = _device(mode, rank)
     if mode == "nccl":
         torch.cuda.set_device(dev)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     else:
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = case_cfg(mode)
+        cfg = dataclasses.replace(case_cfg(mode), dropout=dropout)
         dtype, m, mb = _setting(mode)
         torch.manual_seed(0)
         full = torch.nn.Sequential(*build_lm_blocks(cfg))
@@ -107,14 +117,18 @@ def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q):
                              act_shape=[stage_input_shape(cfg, plan, s, mb) for s in plan.vstages(rank)],
                              act_dtype=dtype, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
                              device=dev, watchdog=120.0,
-                             skip_shapes={"skip": ((mb, cfg.seq_len, cfg.d_model), dtype)})
+                             skip_shapes={"skip": ((mb, cfg.seq_len, cfg.d_model), dtype)},
+                             transport="ipc" if mode.startswith("ipc") else "rccl")
+        if mode.startswith("ipc"):
+            assert type(eng.chan).__name__ == "IpcChannels"
         inputs, targets = _data(cfg, m, mb)
+        torch.manual_seed(1000 + seed * 97 + rank)  # dropout streams: per rank, same in every mode
         opt.zero_grad()
         st = eng.step([x.to(dev) for x in inputs] if rank == 0 else None, [t.to(dev) for t in targets])
         opt.fold_grads()
         sq = opt.grad_sumsq()
         dist.all_reduce(sq)
-        if mode == "nccl":
+        if dev.type == "cuda":
             torch.cuda.synchronize()
         q.put((rank, None if st.loss is None else float(st.loss), _grads(stage.parameters(), names), float(sq),
                len(eng.skip_routes)))
@@ -125,7 +139,7 @@ def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q):
 def single_rank_reference(mode, checkpoint, split, skips):
     cfg = case_cfg(mode)
     dtype, m, mb = _setting(mode)
-    dev = torch.device("cuda", 0) if mode == "nccl" else torch.device("cpu")
+    dev = torch.device("cuda", 0) if mode in GPU_MODES else torch.device("cpu")
     torch.manual_seed(0)
     full = torch.nn.Sequential(*build_lm_blocks(cfg))
     names = {id(p): n for n, p in full.named_parameters()}
@@ -159,30 +173,69 @@ def single_rank_reference(mode, checkpoint, split, skips):
     return loss, ref, sq
 
 
-def run_engine_case(mode, world, checkpoint, virtual, split, skips):
-    """Spawns ``world`` ranks and checks loss, every gradient and the global
-    gradient norm against the single-rank engine."""
-    ref_loss, ref, ref_sq = single_rank_reference(mode, checkpoint, split, skips)
-    if mode == "nccl":
-        # the ranks initialise HIP after spawn: give every RCCL stream its own
+def spawn_ranks(mode, world, checkpoint, virtual, split, skips, dropout=0.0, seed=0):
+    """Runs one engine step on ``world`` spawned ranks; returns their results."""
+    if mode in GPU_MODES:
+        # the ranks initialise HIP after spawn: give every stream its own
         # hardware queue (mipipe.parallel.p2p.check_hw_queues)
         os.environ["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, mode, checkpoint, virtual, split, skips, q))
+    procs = [ctx.Process(target=worker, args=(r, world, port, mode, checkpoint, virtual, split, skips, q, dropout,
+                                              seed))
              for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=300) for _ in range(world)]
+    import queue as _queue
+    import time as _time
+
+    results = []
+    deadline = _time.time() + 300
+    try:
+        while len(results) < world:
+            try:
+                results.append(q.get(timeout=1.0))
+            except _queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                if dead or _time.time() > deadline:
+                    raise AssertionError(f"rank(s) failed (exit codes {dead}) or timed out; "
+                                         f"{len(results)}/{world} results")
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
     for p in procs:
-        p.join(timeout=60)
         assert p.exitcode == 0
-    rel = 2e-2 if mode == "nccl" else 1e-4
+    return sorted(results, key=lambda r: r[0])
+
+
+def run_dropout_recompute_case(mode, world, virtual=1):
+    """Dropout 0.2 on every rank: 'except_last' and 'always' recompute with the
+    RNG state each rank saved at its forward, so their gradients are
+    BIT-identical to 'never' on every rank (and a different seed changes them)."""
+    base = spawn_ranks(mode, world, "never", virtual, False, False, dropout=0.2)
+    other = spawn_ranks(mode, world, "never", virtual, False, False, dropout=0.2, seed=1)
+    assert any(not (base[r][2][n] == other[r][2][n]).all() for r in range(world) for n in base[r][2])
+    for ck in ("except_last", "always"):
+        res = spawn_ranks(mode, world, ck, virtual, False, False, dropout=0.2)
+        for (rank, loss, grads, sq, _), (_, loss0, grads0, sq0, _) in zip(res, base):
+            assert loss == loss0, (ck, rank)
+            for name, g in grads.items():
+                assert (g == grads0[name]).all(), (ck, rank, name)
+
+
+def run_engine_case(mode, world, checkpoint, virtual, split, skips):
+    """Spawns ``world`` ranks and checks loss, every gradient and the global
+    gradient norm against the single-rank engine."""
+    ref_loss, ref, ref_sq = single_rank_reference(mode, checkpoint, split, skips)
+    results = spawn_ranks(mode, world, checkpoint, virtual, split, skips)
+    rel = 2e-2 if mode in GPU_MODES else 1e-4
     seen = set()
     for rank, loss, grads, sq, nskips in results:
         if loss is not None:
-            assert abs(loss - ref_loss) < (2e-3 if mode == "nccl" else 1e-5) * abs(ref_loss)
+            assert abs(loss - ref_loss) < (2e-3 if mode in GPU_MODES else 1e-5) * abs(ref_loss)
         for name, g in grads.items():
             g = torch.from_numpy(g)
             r = ref[name]
@@ -192,7 +245,7 @@ def run_engine_case(mode, world, checkpoint, virtual, split, skips):
             scale = r.abs().max().item() + 1e-6
             assert (g - r).abs().max().item() <= rel * scale, name
             seen.add(name)
-        assert abs(sq - ref_sq) / ref_sq < (1e-2 if mode == "nccl" else 1e-4)
+        assert abs(sq - ref_sq) / ref_sq < (1e-2 if mode in GPU_MODES else 1e-4)
         if skips:
             assert nskips > 0, "no skip crossed a stage boundary"
     assert seen == set(ref)

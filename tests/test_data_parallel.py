@@ -54,7 +54,7 @@ def _reference(mode, m_total, mb):
     return loss, _grads(model.parameters(), names), float(opt.grad_sumsq())
 
 
-def _dp_worker(rank, world, port, pp, dp, m, mb, mode, q):
+def _dp_worker(rank, world, port, pp, dp, m, mb, mode, q, transport="rccl"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -66,7 +66,14 @@ def _dp_worker(rank, world, port, pp, dp, m, mb, mode, q):
         cfg, dtype, dev = _mode_setup(mode)
         if dev.type == "cuda":
             torch.cuda.set_device(dev)
-        groups = make_pp_dp_groups(pp, dp)
+        stage_guess = rank % pp
+        _, _, plan0 = _build(cfg, pp, stage_guess)
+        recv = max(torch.Size(stage_input_shape(cfg, plan0, stage_guess, mb)).numel(), 1) * torch.empty(
+            (), dtype=dtype).element_size()
+        groups = make_pp_dp_groups(pp, dp, transport=transport,
+                                   ipc_options={"device": dev, "recv_bytes": recv} if transport == "ipc" else None)
+        if transport == "ipc" and pp > 1:
+            assert type(groups.channels).__name__ == "IpcChannels"
         chunk, names, plan = _build(cfg, pp, groups.stage)
         chunk = chunk.to(dev, dtype)
         opt = FlatAdam(chunk.parameters(), lr=1e-3)
@@ -105,14 +112,15 @@ def _dp_worker(rank, world, port, pp, dp, m, mb, mode, q):
         dist.destroy_process_group()
 
 
-def _run_dp(pp, dp, mode):
+def _run_dp(pp, dp, mode, transport="rccl"):
     m, mb = 4, 2
     ref_loss, ref, ref_sq = _reference(mode, m * dp, mb)
     world = pp * dp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, pp, dp, m, mb, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, pp, dp, m, mb, mode, q, transport))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=300) for _ in range(world)]
@@ -153,6 +161,18 @@ def test_engine_data_parallel_share_gpu(pp, dp):
     """The same on one MI355X (all ranks on cuda:0, bf16 HIP kernels, gloo):
     buckets are issued from inside the deferred weight-gradient flush."""
     _run_dp(pp, dp, "gpu")
+
+
+def test_engine_pp2_dp2_ipc_links_host():
+    """pp2 x dp2 with the pipelines' activations on IPC links (host mode)."""
+    _run_dp(2, 2, "cpu", transport="ipc")
+
+
+@pytest.mark.gpu
+def test_engine_pp2_dp2_ipc_links_share_gpu():
+    """pp2 x dp2, four ranks on cuda:0: stage boundaries over device-memory IPC
+    links (DMA copies into the peer's slots), gradients all-reduced over gloo."""
+    _run_dp(2, 2, "gpu", transport="ipc")
 
 
 def _ddp_worker(rank, world, port, q):

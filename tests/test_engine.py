@@ -399,3 +399,22 @@ def test_planner_unloads_busiest_rank():
     peak = lambda p: max(p.rank_cost(r) for r in range(8))  # noqa: E731
     assert peak(after) < peak(before)
     assert sim(after) <= sim(before) * 1.002
+
+
+# ------------------------------------------------------------------ IPC transport (host mode)
+@pytest.mark.parametrize("world,case", [(2, c) for c in ENGINE_CASES] + [(4, ENGINE_CASES[1]), (4, ENGINE_CASES[3])])
+def test_engine_cases_ipc_links_host(world, case):
+    """transport='ipc' (mipipe.parallel.ipc.IpcChannels): activations and
+    gradients through the native IPC links' slot rings and sequence counters
+    -- here their host mode (shared memory, memcpy), the same protocol the
+    device mode runs on a GPU -- against the single-rank engine, exactly."""
+    run_engine_case("ipc_cpu", world, *case)
+
+
+def test_engine_ipc_dropout_recompute_bit_identical_host():
+    """Dropout 0.2 on both ranks: 'except_last' / 'always' == 'never' bit for bit
+    (each rank recomputes with the RNG state it saved at its forward)."""
+    from helpers.engine_cases import run_dropout_recompute_case
+
+    run_dropout_recompute_case("ipc_cpu", 2)
+

@@ -22,7 +22,7 @@ from mipipe.models import CONFIGS, build_lm_blocks
 from mipipe.optim import FlatAdam
 from mipipe.parallel import PipelineEngine
 
-from helpers.engine_cases import ENGINE_CASES, run_engine_case
+from helpers.engine_cases import ENGINE_CASES, run_dropout_recompute_case, run_engine_case
 
 pytestmark = pytest.mark.gpu
 
@@ -262,3 +262,23 @@ def test_engine_nccl_matches_single_rank(world, checkpoint, virtual, split, skip
     if _ngpu() < world:
         pytest.skip(f"needs {world} GPUs")
     run_engine_case("nccl", world, checkpoint, virtual, split, skips)
+
+
+# ------------------------------------------------------------------ engine over IPC links, ranks sharing cuda:0
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("checkpoint,virtual,split,skips", ENGINE_CASES)
+def test_engine_ipc_links_share_gpu(world, checkpoint, virtual, split, skips):
+    """2 / 4 pipeline ranks on ONE MI355X, transport='ipc': every activation and
+    gradient moves through device memory -- the sender's DMA copy into the
+    receiver's exported slot ring, completion via interprocess events -- no
+    host staging, no RCCL.  Against the single-rank engine (bf16 kernels)."""
+    run_engine_case("ipc_gpu", world, checkpoint, virtual, split, skips)
+
+
+@pytest.mark.parametrize("world,virtual", [(2, 1), (4, 2)])
+def test_engine_ipc_links_dropout_recompute_bit_identical(world, virtual):
+    """Dropout 0.2 on every rank (embedding, attention, GEMM epilogues): the
+    multi-rank 'except_last' / 'always' gradients are BIT-identical to 'never'
+    on every rank -- recompute replays each rank's own Philox stream."""
+    run_dropout_recompute_case("ipc_gpu", world, virtual)
+

@@ -1,0 +1,116 @@
+"""Per-rank pipeline timeline from rocprofv3 databases of a PipelineEngine run.
+
+Record (one database per process; the engine labels every action with roctx,
+see ``PipelineEngine.step``)::
+
+    rocprofv3 --kernel-trace --marker-trace -d gpurun_out/tl -o rank -- python bench.py --steps 2 --warmup 1
+    torchrun ... (each rank under rocprofv3 the same way)
+
+Report::
+
+    python tools/engine_timeline.py gpurun_out/tl/**/*_results.db [--step -1]
+
+For the chosen ``engine step`` range (default: the last one of each rank) the
+window runs from the earliest step start (host clock, shared by every process
+of a node) to the last kernel end of the step on any rank.  Per rank:
+
+* ``busy``     -- union of the rank's kernel intervals in the window (GPU time);
+* ``lead``     -- window start -> the rank's first kernel (fill: waiting for
+  upstream activations);
+* ``tail``     -- the rank's last kernel -> window end (drain);
+* ``bubble``   -- 1 - busy / window;
+* host-side time in each action kind (``F``, ``B``, ``recompute``, ``wait
+  recv act``, ``wait recv grad``, ``wgrad flush``, ``wait sends``): where the
+  rank's launch thread spent the step.
+
+The mean bubble over ranks is the measured counterpart of the
+``bubble_sim_pct`` / ``bubble_theory_pct`` bench.py prints.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import re
+import sqlite3
+from collections import defaultdict
+from typing import Dict, List, Tuple
+
+Interval = Tuple[int, int]
+
+
+def _union(iv: List[Interval]) -> List[Interval]:
+    out: List[Interval] = []
+    for a, b in sorted(iv):
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
+
+
+def _clip(iv: List[Interval], lo: int, hi: int) -> List[Interval]:
+    return [(max(a, lo), min(b, hi)) for a, b in iv if b > lo and a < hi]
+
+
+def _total(iv: List[Interval]) -> int:
+    return sum(b - a for a, b in iv)
+
+
+_KIND = re.compile(r"^(F|B|recompute|wait recv act|wait recv grad|post recvs|wgrad flush|wait sends)")
+
+
+def load(db: str):
+    con = sqlite3.connect(db)
+    regions = con.execute("select name, start, end from regions").fetchall()
+    kernels = con.execute("select start, end from kernels").fetchall()
+    return regions, kernels
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dbs", nargs="+")
+    ap.add_argument("--step", type=int, default=-1, help="which 'engine step' range of each rank (default last)")
+    args = ap.parse_args()
+    paths = sorted({p for pat in args.dbs for p in glob.glob(pat, recursive=True)})
+    ranks = []
+    for p in paths:
+        regions, kernels = load(p)
+        steps = sorted((a, b) for n, a, b in regions if n == "engine step")
+        if not steps:
+            print(f"{p}: no 'engine step' ranges (run with --marker-trace)")
+            continue
+        s0, s1 = steps[args.step]
+        nxt = [a for a, _ in steps if a > s0]
+        limit = nxt[0] if nxt else max(b for _, b in kernels)
+        # kernels of this step: started after the step began, before the next one began
+        ks = [(a, b) for a, b in kernels if s0 <= a < limit]
+        acts = [(n, a, b) for n, a, b in regions if s0 <= a and b <= s1 and n != "engine step"]
+        ranks.append((p, s0, s1, ks, acts))
+    if not ranks:
+        return
+    w0 = min(r[1] for r in ranks)
+    w1 = max(max((b for _, b in r[3]), default=r[2]) for r in ranks)
+    span = w1 - w0
+    print(f"# window {span / 1e6:.3f} ms over {len(ranks)} rank(s)")
+    print(f"{'rank db':<40} {'busy ms':>8} {'lead ms':>8} {'tail ms':>8} {'bubble':>7}   host ms per action kind")
+    bubbles = []
+    for p, s0, s1, ks, acts in ranks:
+        busy = _union(_clip(ks, w0, w1))
+        b = _total(busy)
+        lead = (busy[0][0] - w0) if busy else span
+        tail = (w1 - busy[-1][1]) if busy else span
+        bub = 1 - b / span if span else 0.0
+        bubbles.append(bub)
+        kinds: Dict[str, int] = defaultdict(int)
+        for n, a, e in acts:
+            m = _KIND.match(n)
+            if m:
+                kinds[m.group(1)] += e - a
+        host = ", ".join(f"{k} {v / 1e6:.2f}" for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]))
+        name = p if len(p) <= 40 else "..." + p[-37:]
+        print(f"{name:<40} {b / 1e6:8.2f} {lead / 1e6:8.2f} {tail / 1e6:8.2f} {100 * bub:6.1f}%   {host}")
+    print(f"mean bubble {100 * sum(bubbles) / len(bubbles):.2f}%")
+
+
+if __name__ == "__main__":
+    main()
