@@ -85,6 +85,14 @@ def parse():
     ap.add_argument("--dp", type=int, default=1,
                     help="data-parallel replicas of the pipeline (world = PP x DP; gradients averaged by bucketed "
                          "RCCL all-reduces overlapped with the deferred weight gradients). Default 1: PP = world")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
+                    help="stage-boundary transport of the engine: rccl = send/recv of the process group; ipc = "
+                         "device-memory IPC links (DMA copies into the receiver's slots, no RCCL kernels; "
+                         "mipipe.parallel.ipc)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="every rank on cuda:0 (gloo for the small collectives, --transport ipc for the stage "
+                         "boundaries): a one-GPU rehearsal of the multi-rank step for timelines "
+                         "(tools/profile_ranks.py); NOT a throughput number for n_gpus ranks")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -101,11 +109,17 @@ def main() -> int:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     on_gpu = args.device == "cuda"
+    if args.shared_gpu:
+        args.transport = "ipc"  # RCCL refuses two ranks on one GPU
     if on_gpu:
+        local = 0 if args.shared_gpu else local
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
         if world > 1:
-            dist.init_process_group("nccl", device_id=device)
+            if args.shared_gpu:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=device)
     else:
         device = torch.device("cpu")
         args.dtype = "fp32"
@@ -168,10 +182,16 @@ def main() -> int:
 
     is_last = prank == pp - 1
     groups = dpg = None
+    act_shapes = [stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(prank)]
     if dp > 1:
         from mipipe.parallel.data_parallel import DataParallelGrads, make_pp_dp_groups
 
-        groups = make_pp_dp_groups(pp, dp, wrap=virtual > 1)
+        ipc_opts = None
+        if args.transport == "ipc":
+            item = torch.empty((), dtype=dtype).element_size()
+            ipc_opts = {"device": device, "slots": m * virtual,
+                        "recv_bytes": max(torch.Size(s_).numel() for s_ in act_shapes) * item}
+        groups = make_pp_dp_groups(pp, dp, wrap=virtual > 1, transport=args.transport, ipc_options=ipc_opts)
         dpg = DataParallelGrads(opt, groups.dp_group)
 
     def loss_fn(y, t):
@@ -180,12 +200,11 @@ def main() -> int:
     from mipipe.parallel.watchdog import Watchdog
 
     wd = Watchdog(args.watchdog) if args.watchdog > 0 else None
-    engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint,
-                            act_shape=[stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(prank)],
+    engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint, act_shape=act_shapes,
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device,
                             skip_shapes={"skip": ((mb, S, E), dtype)}, watchdog=wd,
                             group=groups.channels if groups is not None else None,
-                            grad_divisor=dp)
+                            grad_divisor=dp, transport=args.transport)
     # explicit recompute (issued before each gradient wait, as the engine does)
     from mipipe.pipeline import checkpoint_stop_for
     sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
@@ -320,7 +339,10 @@ def main() -> int:
                 "skips": args.skips if not skip_pairs else f"{args.skips}: {len(skip_pairs)} long residuals, "
                                                            f"{len(engine.skip_routes)} cross-stage",
                 "parallelism": f"pp{pp}" + (f"dp{dp}" if dp > 1 else ""),
-                "impl": "engine (one process per GPU, RCCL send/recv)",
+                "impl": ("engine (one process per GPU, RCCL send/recv)" if args.transport == "rccl" else
+                         "engine (one process per GPU, device-memory IPC links: DMA into the receiver's slots)"),
+                "transport": args.transport,
+                "shared_gpu": bool(args.shared_gpu),
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
             },

@@ -223,8 +223,14 @@ class PipelineEngine:
             if transport == "ipc":
                 from .ipc import IpcChannels
 
-                self.chan = IpcChannels(ranks, wrap=self.virtual > 1, device=dev,
-                                        recv_bytes=self.recv_bytes(), **(transport_options or {}))
+                opts = dict(transport_options or {})
+                # one slot per message a link carries in a step: a sender never
+                # blocks inside a step (with fewer, a looping placement can
+                # deadlock: rank 0 would wait for a slot rank 1 frees only
+                # after rank 0's own later chunk has run)
+                opts.setdefault("slots", self.chunks * self.virtual)
+                self.chan = IpcChannels(ranks, wrap=self.virtual > 1, device=dev, recv_bytes=self.recv_bytes(),
+                                        **opts)
             elif transport == "rccl":
                 self.chan = Channels(ranks, wrap=self.virtual > 1)
                 with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):

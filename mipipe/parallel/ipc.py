@@ -96,8 +96,9 @@ class IpcChannels:
         recv_bytes: the largest activation (bytes) this rank RECEIVES; the
             gradients it receives are sized by its downstream neighbour's.
         slots: messages in flight per link (default: 64); a sender blocks
-            only when all are unreleased.  ``chunks x virtual`` never blocks
-            within a step.
+            its host only when all are unreleased.  ``chunks x virtual`` (what
+            the engine passes) never blocks within a step; fewer is safe for
+            a plain GPipe chain but can deadlock a looping placement.
         engine: ``"sdma"`` (DMA engines) or ``"blit"`` (copy kernel) for the
             sender's copy.
         ipc_events: complete through interprocess events (default, unless

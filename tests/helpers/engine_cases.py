@@ -83,7 +83,7 @@ def _grads(params, names):
     return out
 
 
-def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropout=0.0, seed=0):
+def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropout=0.0, seed=0, steps=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = _device(mode, rank)
     if mode == "nccl":
@@ -118,13 +118,18 @@ def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropou
                              act_dtype=dtype, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
                              device=dev, watchdog=120.0,
                              skip_shapes={"skip": ((mb, cfg.seq_len, cfg.d_model), dtype)},
-                             transport="ipc" if mode.startswith("ipc") else "rccl")
+                             transport="ipc" if mode.startswith("ipc") else "rccl",
+                             # several steps of a plain chain: a 2-slot ring is reused many times over
+                             # (a looping placement keeps one slot per message of the step)
+                             transport_options={"slots": 2} if (mode.startswith("ipc") and steps > 1
+                                                                and virtual == 1) else None)
         if mode.startswith("ipc"):
             assert type(eng.chan).__name__ == "IpcChannels"
         inputs, targets = _data(cfg, m, mb)
-        torch.manual_seed(1000 + seed * 97 + rank)  # dropout streams: per rank, same in every mode
-        opt.zero_grad()
-        st = eng.step([x.to(dev) for x in inputs] if rank == 0 else None, [t.to(dev) for t in targets])
+        for _ in range(steps):  # no optimizer step: every step computes the same gradients
+            torch.manual_seed(1000 + seed * 97 + rank)  # dropout streams: per rank, same in every mode
+            opt.zero_grad()
+            st = eng.step([x.to(dev) for x in inputs] if rank == 0 else None, [t.to(dev) for t in targets])
         opt.fold_grads()
         sq = opt.grad_sumsq()
         dist.all_reduce(sq)
@@ -173,7 +178,7 @@ def single_rank_reference(mode, checkpoint, split, skips):
     return loss, ref, sq
 
 
-def spawn_ranks(mode, world, checkpoint, virtual, split, skips, dropout=0.0, seed=0):
+def spawn_ranks(mode, world, checkpoint, virtual, split, skips, dropout=0.0, seed=0, steps=1):
     """Runs one engine step on ``world`` spawned ranks; returns their results."""
     if mode in GPU_MODES:
         # the ranks initialise HIP after spawn: give every stream its own
@@ -183,7 +188,7 @@ def spawn_ranks(mode, world, checkpoint, virtual, split, skips, dropout=0.0, see
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=worker, args=(r, world, port, mode, checkpoint, virtual, split, skips, q, dropout,
-                                              seed))
+                                              seed, steps))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -226,11 +231,11 @@ def run_dropout_recompute_case(mode, world, virtual=1):
                 assert (g == grads0[name]).all(), (ck, rank, name)
 
 
-def run_engine_case(mode, world, checkpoint, virtual, split, skips):
+def run_engine_case(mode, world, checkpoint, virtual, split, skips, steps=1):
     """Spawns ``world`` ranks and checks loss, every gradient and the global
-    gradient norm against the single-rank engine."""
+    gradient norm against the single-rank engine (after ``steps`` steps)."""
     ref_loss, ref, ref_sq = single_rank_reference(mode, checkpoint, split, skips)
-    results = spawn_ranks(mode, world, checkpoint, virtual, split, skips)
+    results = spawn_ranks(mode, world, checkpoint, virtual, split, skips, steps=steps)
     rel = 2e-2 if mode in GPU_MODES else 1e-4
     seen = set()
     for rank, loss, grads, sq, nskips in results:

@@ -41,6 +41,9 @@ CASES = [
     # enc12_d4096 at PP=8 (2 chunks per rank, split head, except_last at 32 micro-batches)
     (8, ["--num-layers", "4"], {"virtual_chunks_per_rank": 2, "vocab_split_decoder": True,
                                 "checkpoint": "except_last", "chunks": 32}),
+    # the IPC-link transport (host-mode links on CPU): looping placement over shared-memory slot rings
+    (4, ["--transport", "ipc", "--chunks-per-rank", "2", "--split-decoder", "on"],
+     {"transport": "ipc", "virtual_chunks_per_rank": 2}),
 ]
 
 
@@ -120,11 +123,12 @@ def test_vs_baseline_only_on_reference_config():
     assert not bench.matches_reference(CONFIGS["ref_main"], ns, 8, 4)
 
 
-def test_bench_data_parallel_contract():
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_bench_data_parallel_contract(transport):
     """--dp 2 on 4 ranks: two 2-stage pipeline replicas; the JSON counts both
     replicas' tokens and names the layout."""
     args = ["--gpus", "4", "--dp", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--config", "tiny",
-            "--micro-batch", "2"]
+            "--micro-batch", "2", "--transport", transport]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py")] + args
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp",

@@ -418,3 +418,10 @@ def test_engine_ipc_dropout_recompute_bit_identical_host():
 
     run_dropout_recompute_case("ipc_cpu", 2)
 
+
+@pytest.mark.parametrize("virtual,split", [(1, False), (2, True)])
+def test_engine_ipc_links_host_slot_reuse_over_steps(virtual, split):
+    """Three steps: 2-slot host rings wrap within a step (plain chain), or the
+    slots are reused step after step (looping placement)."""
+    run_engine_case("ipc_cpu", 2, "except_last", virtual, split, False, steps=3)
+

@@ -282,3 +282,12 @@ def test_engine_ipc_links_dropout_recompute_bit_identical(world, virtual):
     on every rank -- recompute replays each rank's own Philox stream."""
     run_dropout_recompute_case("ipc_gpu", world, virtual)
 
+
+@pytest.mark.parametrize("world,virtual", [(2, 1), (4, 2)])
+def test_engine_ipc_links_slot_reuse_over_steps(world, virtual):
+    """Three steps: every slot, its interprocess events and its sequence
+    counters are reused (2-slot rings within the step for the plain chain,
+    step after step for the looping one) -- the last step still equals the
+    single-rank engine."""
+    run_engine_case("ipc_gpu", world, "except_last", virtual, virtual > 1, False, steps=3)
+
