@@ -63,6 +63,7 @@ struct Shared {
   int32_t use_events;
   std::atomic<uint32_t> aborted;
   std::atomic<uint32_t> sender_ready;
+  std::atomic<uint32_t> sender_detached;     // the sender has closed its mapping of the ring
   hipIpcMemHandle_t mem;                     // the slot ring
   hipIpcEventHandle_t freed_ev[kMaxSlots];   // receiver's events, waited by the sender
   hipIpcEventHandle_t full_ev[kMaxSlots];    // sender's events, waited by the receiver
@@ -188,6 +189,7 @@ std::unique_ptr<Link> Link::create(const std::string& name, int device, int64_t 
   sh->use_events = (!host && use_ipc_events) ? 1 : 0;
   sh->aborted.store(0);
   sh->sender_ready.store(0);
+  sh->sender_detached.store(0);
   for (int k = 0; k < nslots; ++k) {
     sh->slots[k].full.store(0);
     sh->slots[k].freed.store(0);
@@ -282,9 +284,15 @@ Link::~Link() {
       if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
       if (sender_) {
         (void)hipIpcCloseMemHandle(data_);
+        sh_->sender_detached.store(1, std::memory_order_release);
       } else if (owns_data_) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(data_);
+        // Free the ring only once no sender maps it: freeing memory a peer
+        // process still maps can block until that peer lets go, and two
+        // ranks tearing down their receivers first would wait on each other.
+        // A ring still mapped is left to the process teardown.
+        const bool mapped = sh_->sender_ready.load(std::memory_order_acquire) &&
+                            !sh_->sender_detached.load(std::memory_order_acquire);
+        if (!mapped) (void)hipFree(data_);
       }
       const int64_t n = sh_ ? sh_->nslots : 0;
       if (local_events_)

@@ -257,6 +257,13 @@ class PipelineEngine:
             self.watchdog.describe = self.describe
         self._setup_skips(group, skip_shapes, skip_routes)
 
+    def close(self) -> None:
+        """Releases the transport (IPC links: senders unmap, then receivers
+        free; collective).  RCCL channels need nothing."""
+        close = getattr(self.chan, "close", None)
+        if close is not None:
+            close()
+
     def recv_bytes(self) -> int:
         """Largest activation (bytes) this rank receives per micro-batch."""
         item = torch.empty((), dtype=self.act_dtype).element_size()

@@ -221,5 +221,14 @@ class IpcChannels:
         return self._recv(self._grad_in, t)
 
     def close(self) -> None:
+        """Tears the links down: every sender unmaps its peer's ring, then (after
+        a barrier, when a process group is up) every receiver frees its own.
+        Collective when ``dist`` is initialised."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self._act_out = self._grad_out = None
+        self._links = [x for x in self._links if not x.is_sender]
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
         self._links = []
-        self._act_in = self._act_out = self._grad_in = self._grad_out = None
+        self._act_in = self._grad_in = None

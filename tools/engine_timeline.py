@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import json
 import re
 import sqlite3
 from collections import defaultdict
@@ -60,8 +61,17 @@ _KIND = re.compile(r"^(F|B|recompute|wait recv act|wait recv grad|post recvs|wgr
 
 
 def load(db: str):
+    """(label, start, end) of the roctx ranges and (start, end) of the kernels.
+    rocpd keeps a roctx range's text in ``extdata`` ({"message": ...}); the
+    ``name`` column is the API (``roctxThreadRangeA``)."""
     con = sqlite3.connect(db)
-    regions = con.execute("select name, start, end from regions").fetchall()
+    regions = []
+    for name, ext, a, b in con.execute("select name, extdata, start, end from regions"):
+        try:
+            label = json.loads(ext or "{}").get("message") or name
+        except ValueError:
+            label = name
+        regions.append((label, a, b))
     kernels = con.execute("select start, end from kernels").fetchall()
     return regions, kernels
 
@@ -110,6 +120,11 @@ def main() -> None:
         name = p if len(p) <= 40 else "..." + p[-37:]
         print(f"{name:<40} {b / 1e6:8.2f} {lead / 1e6:8.2f} {tail / 1e6:8.2f} {100 * bub:6.1f}%   {host}")
     print(f"mean bubble {100 * sum(bubbles) / len(bubbles):.2f}%")
+    if len(ranks) > 1:
+        # ranks sharing one GPU (--shared-gpu): how full the device was
+        dev = _union([iv for r in ranks for iv in _clip(r[3], w0, w1)])
+        print(f"union of every rank's kernels: {_total(dev) / 1e6:.2f} ms = {100 * _total(dev) / span:.1f}% of the "
+              f"window (the device's busy share when the ranks share one GPU)")
 
 
 if __name__ == "__main__":
