@@ -11,10 +11,11 @@ handles with ``wait()``), built on the native :class:`mipipe._C.IpcLink`
   DMA engines (``hipMemcpyAsync``) or a blit kernel -- no RCCL kernel
   occupies CUs next to the GEMMs, and several ranks may share ONE GPU (RCCL
   refuses that: ``profiles/nccl_probe_one_gpu.txt``);
-* completion crosses the process boundary through interprocess events (the
-  receiver's compute stream waits for the sender's copy on the GPU) or, where
-  the runtime lacks them, through a proxy thread that publishes the slot once
-  the copy has completed;
+* completion crosses the process boundary through a proxy thread that
+  publishes the slot once the sender's copy has completed (default), or
+  through interprocess events (``ipc_events=True``: the receiver's compute
+  stream waits for the sender's copy on the GPU -- limited on ROCm 7.2 to
+  about 32 records per event, see ``_ipc_events_default``);
 * the receiver's ``wait()`` copies the slot into the engine's tensor on the
   current stream and releases the slot.
 
@@ -45,7 +46,13 @@ ENGINES = {"sdma": 0, "blit": 1}
 
 
 def _ipc_events_default() -> bool:
-    return os.environ.get("MIPIPE_IPC_EVENTS", "1") != "0"
+    # Off by default: ROCm 7.2's interprocess events stop working after about
+    # 32 records of one event (a record then blocks, a wait fails with
+    # "invalid argument"; tools/ipc_bw.py --events reproduces it), and a
+    # training run re-records every slot's event once per step.  The proxy
+    # thread completes a message once its copy is done, at the price of a
+    # host-side wait in the receiver.
+    return os.environ.get("MIPIPE_IPC_EVENTS", "0") == "1"
 
 
 class _SendWork:
@@ -101,8 +108,8 @@ class IpcChannels:
             a plain GPipe chain but can deadlock a looping placement.
         engine: ``"sdma"`` (DMA engines) or ``"blit"`` (copy kernel) for the
             sender's copy.
-        ipc_events: complete through interprocess events (default, unless
-            ``MIPIPE_IPC_EVENTS=0``) or the proxy thread.
+        ipc_events: complete through interprocess events (``MIPIPE_IPC_EVENTS=1``)
+            instead of the proxy thread (default).
         timeout: seconds a host wait may block before it raises (the engine's
             watchdog usually fires first).
     """
