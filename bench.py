@@ -360,7 +360,6 @@ def main() -> int:
             "baseline_note": _baseline_note(ref_match, args.checkpoint),
         }
         print(json.dumps(out), flush=True)
-    engine.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -2,6 +2,8 @@
 #include "ipc.h"
 
 #include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -276,15 +278,36 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
   return L;
 }
 
+static bool ipc_debug() {
+  static const bool on = [] {
+    const char* v = getenv("MIPIPE_IPC_DEBUG");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
+}
+
+#define IPC_TRACE(...)                                     \
+  do {                                                     \
+    if (ipc_debug()) {                                     \
+      fprintf(stderr, "[mipipe ipc %d] ", (int)getpid());  \
+      fprintf(stderr, __VA_ARGS__);                        \
+      fprintf(stderr, "\n");                               \
+    }                                                      \
+  } while (0)
+
 Link::~Link() {
+  IPC_TRACE("destroy %s %s", sender_ ? "sender" : "receiver", name_.c_str());
   try {
     if (!host_mode() && sh_ != nullptr && !ipc_events()) Proxy::get().drain();  // no publish into a dead map
+    IPC_TRACE("  proxy drained");
     if (!host_mode() && data_ != nullptr) {
       DeviceGuard g(device_);
       if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
+      IPC_TRACE("  copy stream synchronized");
       if (sender_) {
         (void)hipIpcCloseMemHandle(data_);
         sh_->sender_detached.store(1, std::memory_order_release);
+        IPC_TRACE("  unmapped the peer's ring");
       } else if (owns_data_) {
         // Free the ring only once no sender maps it: freeing memory a peer
         // process still maps can block until that peer lets go, and two
@@ -293,6 +316,7 @@ Link::~Link() {
         const bool mapped = sh_->sender_ready.load(std::memory_order_acquire) &&
                             !sh_->sender_detached.load(std::memory_order_acquire);
         if (!mapped) (void)hipFree(data_);
+        IPC_TRACE("  ring %s", mapped ? "left mapped by the peer (not freed)" : "freed");
       }
       const int64_t n = sh_ ? sh_->nslots : 0;
       if (local_events_)
@@ -303,6 +327,7 @@ Link::~Link() {
     }
   } catch (...) {
   }
+  IPC_TRACE("  events destroyed");
   delete[] local_events_;
   delete[] remote_events_;
   if (sh_) munmap(sh_, map_bytes_);

@@ -137,6 +137,8 @@ def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropou
             torch.cuda.synchronize()
         q.put((rank, None if st.loss is None else float(st.loss), _grads(stage.parameters(), names), float(sq),
                len(eng.skip_routes)))
+        q.close()
+        q.join_thread()  # delivered before any teardown
     finally:
         dist.destroy_process_group()
 

@@ -99,11 +99,13 @@ def _worker(rank, ports, kinds, peer, iters, q, cpu=False):
                     assert float(rx[-1]) == 0.0  # rank 1 returned rank 0's payload
                     one_way = statistics.median(times) / 2
                     out[(kind, mib)] = (one_way * 1e6, (mib << 20) / one_way / 1e9)
+            q.put(out)  # before any teardown
+            q.close()
+            q.join_thread()
             if hasattr(ch, "close"):
                 ch.close()
         finally:
             dist.destroy_process_group()
-    q.put(out)
 
 
 def main():
