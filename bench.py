@@ -164,7 +164,7 @@ def main() -> int:
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
     bwd_ratio = 2.0 + recompute
     if args.virtual == "auto":
-        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio)
+        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb)
     else:
         virtual = int(args.virtual)
         plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1, bwd_ratio=bwd_ratio)

@@ -680,10 +680,13 @@ bool use_long(const Tensor& q, int S, int D) {
 // [B*H, S/32, S]) is non-empty only for the long-sequence kernels with p > 0
 // and must be handed back to attention_bwd.
 std::tuple<Tensor, Tensor, int64_t, int64_t, Tensor> py_attention_fwd(Tensor q, Tensor k, Tensor v, bool causal,
-                                                                      double p, double scale) {
+                                                                      double p, double scale, int64_t kv_len) {
   AttnArgs a;
   fill_qkv(a, q, k, v);
   MP_CHECK(p >= 0.0 && p < 1.0, "attention: bad dropout p");
+  MP_CHECK(kv_len == 0 || (q.scalar_type() == at::kFloat && kv_len > 0 && kv_len <= a.S),
+           "attention: kv_len (a key-length bound) is for fp32, 0 < kv_len <= S");
+  a.kv_len = (int)kv_len;
   at::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   auto o = at::empty({a.B, a.S, a.H, a.D}, q.options());
   auto lse = at::empty({a.B, a.H, a.S}, q.options().dtype(at::kFloat));
@@ -709,9 +712,12 @@ std::tuple<Tensor, Tensor, int64_t, int64_t, Tensor> py_attention_fwd(Tensor q, 
 
 void py_attention_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, double p,
                       double scale, int64_t seed, int64_t offset, Tensor dq, Tensor dk, Tensor dv,
-                      std::optional<Tensor> bits) {
+                      std::optional<Tensor> bits, int64_t kv_len) {
   AttnArgs a;
   fill_qkv(a, q, k, v);
+  MP_CHECK(kv_len == 0 || (q.scalar_type() == at::kFloat && kv_len > 0 && kv_len <= a.S),
+           "attention_bwd: kv_len (a key-length bound) is for fp32, 0 < kv_len <= S");
+  a.kv_len = (int)kv_len;
   check_bshd(o, "o");
   check_bshd(dout, "dout");
   MP_CHECK(o.strides() == dout.strides() && o.sizes() == dout.sizes(), "attention_bwd: o/dout layout differs");
@@ -881,10 +887,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_bwd", &py_embed_bwd);
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });
   m.def("attention_f32_supported", [](int64_t S, int64_t D) { return attention_f32_supported((int)S, (int)D); });
-  m.def("attention_fwd", &py_attention_fwd);
+  m.def("attention_fwd", &py_attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"), py::arg("p"),
+        py::arg("scale"), py::arg("kv_len") = 0);
   m.def("attention_bwd", &py_attention_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("p"), py::arg("scale"), py::arg("seed"), py::arg("offset"),
-        py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none());
+        py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none(), py::arg("kv_len") = 0);
   m.def("attention_long_supported", [](int64_t S, int64_t D) { return attention_long_supported((int)S, (int)D); });
   m.def("attention_long_set_fused_rng", &attention_long_set_fused_rng,
         "long-sequence attention: make the dropout keep words inside the forward kernel (true, default) or in a "

@@ -29,6 +29,11 @@
 // forward and dQ kernels.  Masks are regenerated in backward, so activation
 // recompute replays them bit-exactly.
 //
+// Key-length bound: with AttnArgs::kv_len = L < S (a sequence of L tokens
+// zero-padded to S, the reference's short tail window) keys >= L get no
+// weight (score -inf in the forward, P = 0 in the backward) and the key loops
+// stop at the last block holding a valid key.
+//
 // Supported: fp32, S % 32 == 0, D = 64, causal or not.
 #include "common.h"
 #include "kernels.h"
@@ -171,7 +176,8 @@ __global__ void __launch_bounds__(kThreads, D <= 64 ? 2 : 1) attn_f32_fwd_kernel
   float m = -INFINITY, l = 0.f;
   const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
 
-  const int kend = CAUSAL ? min(a.S, (int)blockIdx.x * 128 + 128) : a.S;
+  const int kl = a.kv_len > 0 ? a.kv_len : a.S;  // valid keys
+  const int kend = min(CAUSAL ? min(a.S, (int)blockIdx.x * 128 + 128) : a.S, (kl + 31) & ~31);
   const int nkb = kend / 32;
   BlockStage<D> sk, sv;
   sk.load(Kb, a.ld_qkv, 0, tid);
@@ -190,10 +196,11 @@ __global__ void __launch_bounds__(kThreads, D <= 64 ? 2 : 1) attn_f32_fwd_kernel
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (CAUSAL && 32 * kb + arow(r, h) > q0 + li) s[r] = -INFINITY;
+        if (32 * kb + arow(r, h) >= kl) s[r] = -INFINITY;  // padded key
         mx = fmaxf(mx, s[r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);  // finite: key 32 kb <= every query of this wave
+      const float mnew = fmaxf(m, mx);  // finite: key 0 is valid for every query and seen first
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float psum = 0.f;
 #pragma unroll
@@ -283,7 +290,8 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
 
-  const int kend = CAUSAL ? min(a.S, (int)blockIdx.x * 128 + 128) : a.S;
+  const int kl = a.kv_len > 0 ? a.kv_len : a.S;  // valid keys
+  const int kend = min(CAUSAL ? min(a.S, (int)blockIdx.x * 128 + 128) : a.S, (kl + 31) & ~31);
   const int nkb = kend / 32;
   BlockStage<D> sk, sv;
   sk.load(Kb, a.ld_qkv, 0, tid);
@@ -313,6 +321,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dq_kernel(AttnArgs a) {
       for (int r = 0; r < 16; ++r) {
         float pr = __builtin_amdgcn_exp2f(s[r] - lse2);
         if (CAUSAL && 32 * kb + arow(r, h) > q0 + li) pr = 0.f;
+        if (32 * kb + arow(r, h) >= kl) pr = 0.f;  // padded key
         float d = dp[r];
         if (a.p > 0.f) d = ws[r] >= a.threshold ? d * pscale : 0.f;
         s[r] = pr * (d - dlt);  // dS^T
@@ -360,6 +369,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) 
     dv[t] = zero16();
   }
 
+  const int kl = a.kv_len > 0 ? a.kv_len : a.S;  // valid keys
   const int qb0 = CAUSAL ? (int)blockIdx.x * 4 : 0;  // first query block that sees any of these keys
   const int nqb = a.S / 32;
   BlockStage<D> sq, so;
@@ -393,6 +403,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) 
         const int qg = 32 * qb + qr;
         float pr = __builtin_amdgcn_exp2f(s[r] - ldsL[qr]);
         if (CAUSAL && k0 + li > qg) pr = 0.f;
+        if (k0 + li >= kl) pr = 0.f;  // padded key: no weight, no gradient
         float keep = 1.f;
         if (a.p > 0.f) {
           const int kk = k0 + li;

@@ -160,6 +160,9 @@ struct AttnArgs {
   uint32_t threshold = 0;
   uint64_t seed = 0, offset = 0;
   bool causal = false;
+  // valid keys (0 = all S): keys >= kv_len are masked out (a zero-padded
+  // non-causal sequence; fp32 kernels)
+  int kv_len = 0;
   // long-sequence kernels with dropout: keep bits, one uint32 per (b*h, 32-query
   // block, key) written by the forward and read by the backward
   uint32_t* dmask = nullptr;

@@ -18,7 +18,9 @@ CPU path is eager math.  Any smaller head dim (e.g. 32, 80, 96, 160) runs on
 the kernels zero-padded to the next supported one (the scale stays that of the
 real head dim; the padded columns are sliced off), and a non-causal sequence of
 an unsupported length runs padded too when its head dim leaves a spare padded
-feature to mask the padded keys with (``_run_shape``).  A CAUSAL sequence of any other length (the
+feature to mask the padded keys with (bf16), or with the kernels' own key bound
+(fp32: ``kv_len``, so the reference's fp32 D=64 tail window runs on the kernels;
+``_run_shape``).  A CAUSAL sequence of any other length (the
 reference's ``get_batch`` tail window, /root/reference/main.py:108-113) is
 zero-padded at the end to the next supported length: under the causal mask
 no real query sees a padded key, so the real rows are exact; the padded rows
@@ -58,12 +60,12 @@ class _AttentionPacked(torch.autograd.Function):
     backward produces the packed ``dqkv`` in one buffer."""
 
     @staticmethod
-    def forward(ctx, qkv, causal, p, scale):  # type: ignore[override]
+    def forward(ctx, qkv, causal, p, scale, kv_len=0):  # type: ignore[override]
         kern = kernels_for(qkv)
         q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
-        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale)
+        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale, kv_len)
         ctx.save_for_backward(qkv, o, lse, bits)
-        ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
+        ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, ctx.kv_len = causal, p, scale, seed, offset, kv_len
         return o
 
     @staticmethod
@@ -75,19 +77,19 @@ class _AttentionPacked(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         kern.attention_bwd(do, qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2), o, lse, ctx.causal, ctx.p,
                            ctx.scale, ctx.seed, ctx.offset, dqkv.select(2, 0), dqkv.select(2, 1), dqkv.select(2, 2),
-                           bits if bits.numel() else None)
-        return dqkv, None, None, None
+                           bits if bits.numel() else None, ctx.kv_len)
+        return dqkv, None, None, None, None
 
 
 class _Attention(torch.autograd.Function):
     """Separate q, k, v as [B, S, H, D] views sharing one layout."""
 
     @staticmethod
-    def forward(ctx, q, k, v, causal, p, scale):  # type: ignore[override]
+    def forward(ctx, q, k, v, causal, p, scale, kv_len=0):  # type: ignore[override]
         kern = kernels_for(q)
-        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale)
+        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale, kv_len)
         ctx.save_for_backward(q, k, v, o, lse, bits)
-        ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset = causal, p, scale, seed, offset
+        ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, ctx.kv_len = causal, p, scale, seed, offset, kv_len
         return o
 
     @staticmethod
@@ -98,8 +100,8 @@ class _Attention(torch.autograd.Function):
             do = do.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         kern.attention_bwd(do, q, k, v, o, lse, ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, dq, dk, dv,
-                           bits if bits.numel() else None)
-        return dq, dk, dv, None, None, None
+                           bits if bits.numel() else None, ctx.kv_len)
+        return dq, dk, dv, None, None, None, None
 
 
 _noted = set()
@@ -136,8 +138,11 @@ def _causal_pad(t: Tensor, S: int, D: int) -> Optional[int]:
 _KEY_MASK = -32768.0  # exact in bf16; times the query's 1 and any scale >= 2^-8: exp underflows to 0
 
 
-def _run_shape(t: Tensor, S: int, D: int, causal: bool, scale: float) -> Optional[Tuple[int, int]]:
-    """(sequence length, head dim) the kernels run a (S, D) attention at, or None (eager path).
+def _run_shape(t: Tensor, S: int, D: int, causal: bool, scale: float) -> Optional[Tuple[int, int, int]]:
+    """(sequence length, head dim, key bound) the kernels run a (S, D) attention
+    at, or None (eager path).  The key bound (``kv_len``, 0 = none) is set for a
+    non-causal fp32 sequence padded at the end: the fp32 kernels mask keys past
+    it themselves.
 
     * A head dim the kernels do not tile is zero-padded to the next one they do: the
       padded features add 0 to every score (the softmax scale stays 1/sqrt(D) of the
@@ -151,11 +156,16 @@ def _run_shape(t: Tensor, S: int, D: int, causal: bool, scale: float) -> Optiona
     dims = [D] + [d for d in ((64, 128, 256) if t.dtype == torch.bfloat16 else (64,)) if d > D]
     for dp in dims:
         if _gpu_ok(t, S, dp):
-            return S, dp
+            return S, dp, 0
+        if t.dtype == torch.float32 and not causal:  # key bound inside the kernel
+            sp = _causal_pad(t, S, dp)
+            if sp is not None:
+                return sp, dp, S
+            continue
         # the spare-feature key mask needs exp(-32768 * scale) to underflow to 0
         sp = _causal_pad(t, S, dp) if (causal or (dp > D and scale >= 2.0 ** -8)) else None
         if sp is not None:
-            return sp, dp
+            return sp, dp, 0
     return None
 
 
@@ -170,8 +180,10 @@ def attention_packed(qkv: Tensor, causal: bool = False, dropout_p: float = 0.0, 
         return _AttentionPacked.apply(qkv.contiguous(), bool(causal), p, scale)
     run = _run_shape(qkv, S, D, bool(causal), scale) if qkv.is_cuda else None
     if run is not None:
-        sp, dp = run
+        sp, dp, kv_len = run
         padded = F.pad(qkv, (0, dp - D, 0, 0, 0, 0, 0, sp - S))
+        if kv_len:  # the kernel masks keys >= S itself
+            return _AttentionPacked.apply(padded, bool(causal), p, scale, kv_len)[:, :S, :, :D]
         if sp != S and not causal:  # mask the padded keys through the spare feature D
             # [B, S, 3, H, D]: index (b, s, which, h, d) -> q = which 0, k = which 1, sequence dim 1
             c = torch.zeros_like(padded)
@@ -201,9 +213,13 @@ def attention(
         if run is None:
             _note_math_path(S, D, q.dtype)
             return attention_reference(q, k, v, causal, p, scale)
-        sp, dp = run
+        sp, dp, kv_len = run
         pad = lambda t: F.pad(t, (0, dp - D, 0, sp - S))  # noqa: E731
         qp, kp = pad(q), pad(k)
+        if kv_len:  # the kernel masks keys >= S itself
+            qs, ks, vs = (t.transpose(1, 2) for t in (qp, kp, pad(v)))
+            qs, ks, vs = (t.contiguous() for t in (qs, ks, vs))
+            return _Attention.apply(qs, ks, vs, bool(causal), p, scale, kv_len).transpose(1, 2)[:, :, :S, :D]
         if sp != S and not causal:  # mask the padded keys through the spare feature D ([B, H, S, D])
             cq, ck = torch.zeros_like(qp), torch.zeros_like(kp)
             cq[..., D] = 1.0

@@ -88,23 +88,31 @@ def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
     per-group min-max split and move single boundaries while that improves."""
     groups = ranks * virtual
     bal = balance_cost(costs, groups)
+    prefix = [0.0]
+    for c in costs:
+        prefix.append(prefix[-1] + c)
 
     def score(b: List[int]) -> Tuple[float, float]:
-        gc, pos = [], 0
-        for k in b:
-            gc.append(sum(costs[pos:pos + k]))
+        per_rank = [0.0] * ranks
+        top, pos = 0.0, 0
+        for i, k in enumerate(b):
+            x = prefix[pos + k] - prefix[pos]
             pos += k
-        per_rank = [sum(gc[c * ranks + r] for c in range(virtual)) for r in range(ranks)]
-        return max(per_rank), max(gc)
+            per_rank[i % ranks] += x
+            top = max(top, x)
+        return max(per_rank), top
 
-    def descend(b: List[int]) -> Tuple[Tuple[float, float], List[int]]:
+    def descend(b: List[int], window: int = 0) -> Tuple[Tuple[float, float], List[int]]:
+        """Coordinate descent: each boundary over its whole feasible range
+        (``window`` 0) or within +-window units of where it is."""
         best = score(b)
         improved = True
-        while improved:  # coordinate descent: each boundary over its whole feasible range
+        while improved:
             improved = False
             for g in range(groups - 1):
                 pair = b[g] + b[g + 1]
-                for left in range(1, pair):
+                lo, hi = (1, pair) if not window else (max(1, b[g] - window), min(pair, b[g] + window + 1))
+                for left in range(lo, hi):
                     if left == b[g]:
                         continue
                     t = list(b)
@@ -120,7 +128,9 @@ def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
 
     rnd = random.Random(0)
     best, bal = descend(bal)
-    for _ in range(200):
+    # restarts: plenty for the enc12 plans (<= 24 groups), fewer for GPT-2-XL's
+    # deep loops, whose 195 units make every descent long
+    for _ in range(200 if groups <= 24 else 60):
         t = list(bal)
         for _ in range(3):
             g = rnd.randrange(groups - 1)
@@ -128,7 +138,7 @@ def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
             if t[g] + d >= 1 and t[g + 1] - d >= 1:
                 t[g] += d
                 t[g + 1] -= d
-        sc, t = descend(t)
+        sc, t = descend(t, window=4)  # a kick moves boundaries by <= 2: refine locally
         if sc < best:
             best, bal = sc, t
     return bal
@@ -136,7 +146,8 @@ def _rank_balanced(costs: List[float], ranks: int, virtual: int) -> List[int]:
 
 def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks: int,
                   bwd_ratio: float = 2.0, deferred_w: float = 0.0,
-                  checkpoint_stop: Optional[int] = None) -> Tuple[float, List[float]]:
+                  checkpoint_stop: Optional[int] = None, transfer: float = 0.0,
+                  launch: float = 0.0) -> Tuple[float, List[float]]:
     """Event simulation of one synchronous step (breadth-first looping order,
     as :class:`~mipipe.parallel.engine.PipelineEngine` runs it; transfers free).
 
@@ -151,7 +162,14 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
     run a recompute (one forward) right before their backward, and -- as the
     engine issues it before its gradient wait -- the recompute does not wait
     for the downstream gradient.  ``stage_costs`` then price forward +
-    ``bwd_ratio`` x forward WITHOUT recompute."""
+    ``bwd_ratio`` x forward WITHOUT recompute.
+
+    ``transfer``: latency of a stage-boundary message (activation or gradient)
+    between ranks, in the units of ``stage_costs``: a dependency on another
+    rank's output is ready that much after it was produced (the sender does
+    not wait).  ``launch``: fixed cost of every F / B / R action (kernel-launch
+    gaps of a chunk).  Both are what more virtual chunks per rank pay for their
+    shorter fill and drain."""
     nv = ranks * virtual
     fwd = [c / (1.0 + bwd_ratio) for c in stage_costs]
     bwd_all = [c * bwd_ratio / (1.0 + bwd_ratio) for c in stage_costs]
@@ -180,16 +198,21 @@ def simulate_step(stage_costs: Sequence[float], ranks: int, virtual: int, chunks
         for r in range(ranks):
             while pos[r] < len(order[r]):
                 kind, s, i = order[r][pos[r]]
+                hop = transfer if ranks > 1 else 0.0
                 if kind == "F":
                     dep = 0.0 if s == 0 else f_done[s - 1][i]
-                    dur = fwd[s]
+                    if dep is not None and s > 0:
+                        dep += hop
+                    dur = fwd[s] + launch
                 elif kind == "W":
                     dep, dur = 0.0, wgt[s]
                 elif kind == "R":
-                    dep, dur = 0.0, fwd[s]
+                    dep, dur = 0.0, fwd[s] + launch
                 else:
                     dep = f_done[s][i] if s == nv - 1 else b_done[s + 1][i]
-                    dur = bwd[s]
+                    if dep is not None and s < nv - 1:
+                        dep += hop
+                    dur = bwd[s] + launch
                 if dep is None:
                     break
                 start = max(clock[r], dep)
@@ -211,7 +234,7 @@ DEFERRED_W = 0.5
 
 
 def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int, start: List[int],
-                      bwd_ratio: float = 2.0) -> List[int]:
+                      bwd_ratio: float = 2.0, window: int = 3) -> List[int]:
     """Coordinate descent on the simulated step time (:func:`simulate_step`)."""
     groups = ranks * virtual
 
@@ -228,7 +251,9 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
         improved = False
         for g in range(groups - 1):
             pair = bal[g] + bal[g + 1]
-            for left in range(1, pair):
+            # local moves: the start is already balanced, and the simulation
+            # dominates planning time (GPT-2-XL has 195 units)
+            for left in range(max(1, bal[g] - window), min(pair, bal[g] + window + 1)):
                 if left == bal[g]:
                     continue
                 t = list(bal)
@@ -370,21 +395,63 @@ def build_stage(cfg: LMConfig, plan: StagePlan, vstage: int, *, device, dtype,
     return stage
 
 
-def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Sequence[int] = (1, 2, 3),
-                   split_options: Sequence[bool] = (False, True), bwd_ratio: float = 2.0) -> Tuple[int, StagePlan]:
+# Prices of the boundary terms of simulate_step, in the planner's unit
+# (training FLOPs per token): a PP boundary carries d_model bf16 values per
+# token over one xGMI link (~64 GB/s one direction for a single peer stream),
+# against ~1.2 PF/s of achieved GEMM rate; every chunk action costs ~30 us of
+# launch gaps, spread over the micro-batch's tokens.
+LINK_BYTES_PER_S = 64e9
+ACHIEVED_FLOP_PER_S = 1.2e15
+LAUNCH_GAP_S = 30e-6
+
+
+def boundary_terms(cfg: LMConfig, micro_batch: Optional[int]) -> Tuple[float, float]:
+    """(transfer, launch) for :func:`simulate_step`, in per-token FLOP-equivalents."""
+    transfer = 2.0 * cfg.d_model / LINK_BYTES_PER_S * ACHIEVED_FLOP_PER_S
+    tokens = (micro_batch or 8) * cfg.seq_len
+    return transfer, LAUNCH_GAP_S * ACHIEVED_FLOP_PER_S / tokens
+
+
+def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional[Sequence[int]] = None,
+                   split_options: Sequence[bool] = (False, True), bwd_ratio: float = 2.0,
+                   micro_batch: Optional[int] = None, max_virtual: int = 8) -> Tuple[int, StagePlan]:
     """Chunks per rank (and whether to split the decoder) with the shortest
     simulated step; ties (within 0.5 %) keep the simpler plan.  ``bwd_ratio``
-    is backward / forward cost (2, or 3 when every micro-batch is recomputed)."""
-    best = None
+    is backward / forward cost (2, or 3 when every micro-batch is recomputed).
+
+    ``candidates`` default: every v from 1 to ``max_virtual`` that leaves each
+    virtual stage at least one pipeline unit.  The simulation charges each
+    stage-boundary message and each chunk action (:func:`boundary_terms`), so a
+    deeper looping placement is chosen only when its shorter fill/drain pays
+    for its extra boundaries."""
+    transfer, launch = boundary_terms(cfg, micro_batch)
+
+    def sim(plan: StagePlan, v: int) -> float:
+        return simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks, bwd_ratio,
+                             deferred_w=1.0 / bwd_ratio, transfer=transfer, launch=launch)[0]
+
+    # screen every (split, v) on its rank-balanced split (cheap), then run the
+    # simulation-refined planner on the few best (the refinement is the
+    # expensive part: coordinate descent over the boundaries)
+    screened = []
     for split in split_options:
         if split and stages == 1:
             continue
-        for v in candidates:
-            if stages * v > len(block_costs(cfg, split)) or (v > 1 and stages == 1):
+        costs = block_costs(cfg, split)
+        units = len(costs)
+        cands = candidates if candidates is not None else range(1, max(1, min(max_virtual, units // stages)) + 1)
+        for v in cands:
+            if stages * v > units or (v > 1 and stages == 1):
                 continue
-            plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio)
-            t, _ = simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks, bwd_ratio,
-                                 deferred_w=1.0 / bwd_ratio)
-            if best is None or t < best[0] * 0.995:
-                best = (t, v, plan)
+            quick = StagePlan(balance_cost(costs, stages * v), costs, v, split)
+            screened.append((sim(quick, v), v, split))
+    screened.sort()
+    best = None
+    for _, v, split in screened[:6]:
+        plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio)
+        t = sim(plan, v)
+        # ties (within 0.5 %) keep the simpler plan: fewer chunks, no split
+        key = (v, split)
+        if best is None or t < best[0] * 0.995 or (t <= best[0] * 1.005 and key < best[3]):
+            best = (t, v, plan, key)
     return best[1], best[2]

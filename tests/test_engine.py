@@ -67,7 +67,7 @@ def test_looping_plans():
     assert len(p.balance) == 8 and p.virtual == 2 and p.ranks == 4
     assert p.vstages(1) == [1, 5]
     assert sum(p.balance) == len(block_costs(cfg))
-    v, plan = choose_virtual(cfg, 2, 8)
+    v, plan = choose_virtual(cfg, 2, 8, micro_batch=64)
     assert v >= 2 and plan.virtual == v  # looping wins at PP=2
     v1, _ = choose_virtual(cfg, 1, 4)
     assert v1 == 1
@@ -383,7 +383,7 @@ def test_planner_unloads_busiest_rank():
 
     cfg = CONFIGS["enc12_d4096"]
     bwd = 2.0 + 31 / 32
-    v, plan = choose_virtual(cfg, 8, 32, bwd_ratio=bwd)
+    v, plan = choose_virtual(cfg, 8, 32, bwd_ratio=bwd, micro_batch=64)
     assert v == 2 and plan.split_decoder
     assert plan.balance[6:8] == [4, 4]
     assert plan.imbalance() < 1.03
@@ -424,4 +424,27 @@ def test_engine_ipc_links_host_slot_reuse_over_steps(virtual, split):
     """Three steps: 2-slot host rings wrap within a step (plain chain), or the
     slots are reused step after step (looping placement)."""
     run_engine_case("ipc_cpu", 2, "except_last", virtual, split, False, steps=3)
+
+
+def test_planner_boundary_terms_and_wide_candidates():
+    """choose_virtual tries v beyond 3 and prices every
+    stage-boundary message and chunk action: with the boundary terms at zero a
+    deep GPT-2-XL loop simulates faster than v = 2; charged for its extra
+    boundaries (26 MB per message at micro-batch 8 x 1024) it does not."""
+    from mipipe.parallel.stage import boundary_terms, choose_virtual, plan_stages, simulate_step
+
+    cfg = CONFIGS["gpt2_xl"]
+    tr, la = boundary_terms(cfg, 8)
+    assert tr > 0 and la > 0
+    p2, p4 = plan_stages(cfg, 8, 2, 8, False, 3.0), plan_stages(cfg, 8, 4, 8, True, 3.0)
+
+    def sim(p, v, t=0.0, lch=0.0):
+        return simulate_step([p.stage_cost(g) for g in range(8 * v)], 8, v, 8, 3.0, deferred_w=1 / 3.0, transfer=t,
+                             launch=lch)[0]
+
+    assert sim(p4, 4) < sim(p2, 2)                    # free boundaries: the deep loop wins
+    assert sim(p4, 4, tr, la) > sim(p2, 2, tr, la)    # priced boundaries: it does not
+    # the planner considers v up to units / stages (capped at 8)
+    v, _ = choose_virtual(CONFIGS["enc12_d4096"], 2, 8, micro_batch=64)
+    assert v > 3
 

@@ -283,27 +283,63 @@ def test_peer_copy_two_gpus(k):
 
 
 # ------------------------------------------------------------------ model / engine
-def test_transformer_layer_eager_fallback_shape(k):
-    """A shape outside both attention kernels' tiling (S = 40) falls back to eager
-    attention math (with a warning) and still matches nn.TransformerEncoderLayer
-    (fp32, no dropout).  The fp32 kernel path is tests/test_gpu_fp32.py."""
+@pytest.mark.parametrize("S", [37, 40, 100])
+def test_fp32_tail_window_runs_on_kernels(k, S):
+    """The reference's own fp32 model on its short tail window (get_batch yields
+    S < 128 at the end of an epoch, /root/reference/main.py:108-113): fp32,
+    head dim 64, NON-causal, S not a multiple of 32.  The sequence is padded to
+    the next multiple of 32 and the fp32 kernels mask the padded keys with a
+    key-length bound -- NO eager fallback -- and a TransformerEncoderLayer
+    matches nn.TransformerEncoderLayer forward and backward (fp32 PyTorch)."""
+    import warnings
+
     from torch import nn
 
     from mipipe.models import TransformerEncoderLayer
+    from mipipe.ops import attention
 
     torch.manual_seed(0)
-    E, H, F_, B, S = 256, 4, 512, 3, 40
+    E, H, F_, B = 256, 4, 512, 3  # head dim 64
     ref = nn.TransformerEncoderLayer(E, H, F_, dropout=0.0, batch_first=True).to(DEV)
     ours = TransformerEncoderLayer(E, H, F_, dropout=0.0, device=DEV).load_from_torch(ref)
     x = torch.randn(B, S, E, device=DEV, requires_grad=True)
     xr = x.detach().clone().requires_grad_()
-    y = ours(x)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # the eager-path note would raise here
+        y = ours(x)
+        g = torch.randn_like(y)
+        y.backward(g)
     yr = ref(xr)
-    assert torch.allclose(y, yr, atol=2e-4), (y - yr).abs().max()
-    g = torch.randn_like(y)
-    y.backward(g)
     yr.backward(g)
-    assert torch.allclose(x.grad, xr.grad, atol=2e-3)
+    assert torch.allclose(y, yr, atol=2e-4), (y - yr).abs().max()
+    assert torch.allclose(x.grad, xr.grad, atol=2e-3), (x.grad - xr.grad).abs().max()
+    # the op itself against fp32 math, q/k/v gradients included
+    q, kk, v = (torch.randn(2, H, S, 64, device=DEV, requires_grad=True) for _ in range(3))
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        o = attention(q, kk, v, causal=False)
+    qr, kr, vr = (t.detach().clone().requires_grad_() for t in (q, kk, v))
+    orf = torch.softmax(qr @ kr.transpose(-1, -2) / 8.0, -1) @ vr
+    assert torch.allclose(o, orf, atol=1e-4), (o - orf).abs().max()
+    go = torch.randn_like(o)
+    o.backward(go)
+    orf.backward(go)
+    for a_, b_ in ((q, qr), (kk, kr), (v, vr)):
+        assert torch.allclose(a_.grad, b_.grad, atol=1e-4), (a_.grad - b_.grad).abs().max()
+
+
+def test_attention_custom_scale_padding(k):
+    """A tiny user scale must not let the bf16 spare-feature key mask leak weight
+    onto padded keys: such shapes take a path that stays exact."""
+    from mipipe.ops import attention
+
+    torch.manual_seed(0)
+    S, D = 40, 48
+    q, kk, v = (torch.randn(2, 2, S, D, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    for scale in (1e-3, 0.125):
+        o = attention(q, kk, v, causal=False, scale=scale).float()
+        orf = torch.softmax(q.float() @ kk.float().transpose(-1, -2) * scale, -1) @ v.float()
+        assert torch.allclose(o, orf, atol=3e-2), (scale, (o - orf).abs().max())
 
 
 def test_engine_one_gpu_step(k):

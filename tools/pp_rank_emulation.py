@@ -77,7 +77,7 @@ def main() -> int:
     cfg = CONFIGS["enc12_d4096"]
     pp, m, mb = args.pp, args.chunks, args.micro_batch
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
-    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute)
+    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb)
     rank = args.rank if args.rank >= 0 else max(range(pp), key=plan.rank_cost)
     torch.manual_seed(0)
     stages = [build_stage(cfg, plan, vs, device=dev, dtype=torch.bfloat16).train() for vs in plan.vstages(rank)]
