@@ -140,17 +140,22 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
   const int stride = gridDim.x * G;
   const int iters = (rows + stride - 1) / stride;  // uniform over the block (barriers inside)
   auto row_of = [&](int it) { return it * stride + blockIdx.x * G + grp; };
-  float zn[MAXV][8], dn[MAXV][8];
+  // The fan-out addend (the residual stream's other gradient) is prefetched
+  // with z and dy: loaded in the store loop it was a dependent HBM round trip
+  // on every row.
+  float zn[MAXV][8], dn[MAXV][8], an[MAXV][8];
+  const bool has_add = addend != nullptr;
   auto load_row = [&](int row) {
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
       const int vi = t + k * kThreads;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) zn[k][i] = dn[k][i] = 0.f;
+      for (int i = 0; i < 8; ++i) zn[k][i] = dn[k][i] = an[k][i] = 0.f;
       if (vi < nvec && row < rows) {
         const size_t e = (size_t)row * cols + (size_t)vi * 8;
         Io<T>::load8(z + e, zn[k]);
         Io<T>::load8(dy + e, dn[k]);
+        if (has_add) Io<T>::load8(addend + e, an[k]);
       }
     }
   };
@@ -163,13 +168,14 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
     const float mean = valid ? mean_in[row] : 0.f;
     const float rstd = valid ? rstd_in[row] : 0.f;
     if (!kPrefetch) load_row(row);
-    float zc[MAXV][8], dc[MAXV][8];
+    float zc[MAXV][8], dc[MAXV][8], ac[MAXV][8];
 #pragma unroll
     for (int k = 0; k < MAXV; ++k)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         zc[k][i] = zn[k][i];
         dc[k][i] = dn[k][i];
+        ac[k][i] = an[k][i];
       }
     if (kPrefetch && it + 1 < iters) load_row(row_of(it + 1));
     float xh[MAXV][8], gy[MAXV][8];
@@ -198,13 +204,7 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
           const size_t e = base + (size_t)vi * 8;
           float o[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = rstd * (gy[k][i] - a - xh[k][i] * b);
-          if (addend != nullptr) {
-            float ad[8];
-            Io<T>::load8(addend + e, ad);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] += ad[i];
-          }
+          for (int i = 0; i < 8; ++i) o[i] = rstd * (gy[k][i] - a - xh[k][i] * b) + ac[k][i];
           Io<T>::store8(dz + e, o);
           if (dx != nullptr) {
             const uint32_t keep = dropout_keep8(seed, offset, e, threshold);

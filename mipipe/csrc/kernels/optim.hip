@@ -107,10 +107,10 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
   // parameters) could keep main_grad cache-resident between the two passes --
   // see profiles/optim_nt_pp8_ab.txt.  Stores stay regular (nt stores
   // measured 3% slower on MI355X).
-  for (int64_t i = tid; i < n4; i += stride) {
-    float4 p = nt_load(P + i), mm = nt_load(Mo + i),
-           vv = nt_load(V + i);
-    const float4 g = nt_load(G + i);
+  // U vectors per thread per iteration, all 4U loads issued before any math:
+  // one vector's loads alone left HBM underfed (4.9 TB/s of 30 B/param).
+  constexpr int U = 2;
+  auto update = [&](int64_t i, float4 p, float4 mm, float4 vv, const float4 g) {
     adam_one(p.x, g.x, mm.x, vv.x, h, c);
     adam_one(p.y, g.y, mm.y, vv.y, h, c);
     adam_one(p.z, g.z, mm.z, vv.z, h, c);
@@ -127,7 +127,21 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
         reinterpret_cast<float4*>(model)[i] = p;
       }
     }
+  };
+  int64_t i = tid;
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    float4 p[U], mm[U], vv[U], g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      p[u] = nt_load(P + i + u * stride);
+      mm[u] = nt_load(Mo + i + u * stride);
+      vv[u] = nt_load(V + i + u * stride);
+      g[u] = nt_load(G + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) update(i + u * stride, p[u], mm[u], vv[u], g[u]);
   }
+  for (; i < n4; i += stride) update(i, nt_load(P + i), nt_load(Mo + i), nt_load(V + i), nt_load(G + i));
   for (int64_t i = n4 * 4 + tid; i < n; i += stride) {
     float p = master[i], mi = m[i], vi = v[i];
     adam_one(p, grad[i], mi, vi, h, c);
@@ -161,7 +175,7 @@ void adam_step(float* master, M* model, const float* grad, float* m, float* v, i
   if (n == 0) return;
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks < 1) blocks = 1;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 4096) blocks = 4096;  // 16 blocks (64 waves) per CU queued; each thread loops
   hipLaunchKernelGGL((adam_kernel<M>), dim3((unsigned)blocks), dim3(256), 0, s, master, model, grad, m, v, n, h,
                      sumsq_ptr);
 }
