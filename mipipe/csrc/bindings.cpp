@@ -818,6 +818,7 @@ extern "C" const char* mipipe_source_digest();
 
 PYBIND11_MODULE(_C, m) {
   m.def("source_digest", []() { return std::string(mipipe_source_digest()); });
+  m.def("adam_set_variant", &mipipe::adam_set_variant);
   py::class_<ipc::Link>(m, "IpcLink")
       .def_static("create", &ipc::Link::create, py::arg("name"), py::arg("device"), py::arg("nslots"),
                   py::arg("slot_bytes"), py::arg("ipc_events") = true)

@@ -152,7 +152,75 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
   }
 }
 
+// One-shot variant (no grid-stride loop): each thread owns U consecutive-by-
+// stride vectors of one block-sized tile; 4U loads in flight, then the math
+// and the stores.  Selected by adam_set_variant(1) for A/B runs.
+template <typename M, int U>
+__global__ void __launch_bounds__(256) adam_tile_kernel(float* __restrict__ master, M* __restrict__ model,
+                                                        const float* __restrict__ grad, float* __restrict__ m,
+                                                        float* __restrict__ v, int64_t n, AdamHyper h,
+                                                        const float* __restrict__ sumsq) {
+  AdamScalars c;
+  c.coef = 1.f;
+  if (sumsq != nullptr && h.max_norm > 0.f) {
+    const float norm = sqrtf(*sumsq);
+    c.coef = fminf(1.f, h.max_norm / (norm + 1e-6f));
+  }
+  c.step_size = h.lr / h.bias_correction1;
+  c.inv_bc2_sqrt = 1.f / sqrtf(h.bias_correction2);
+  const int64_t n4 = n >> 2;
+  const int64_t base = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  float4* P = reinterpret_cast<float4*>(master);
+  const float4* G = reinterpret_cast<const float4*>(grad);
+  float4* Mo = reinterpret_cast<float4*>(m);
+  float4* V = reinterpret_cast<float4*>(v);
+  float4 p[U], mm[U], vv[U], g[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = min(base + u * 256, n4 - 1);  // clamped: loads stay in bounds, stores are masked
+    p[u] = nt_load(P + i);
+    mm[u] = nt_load(Mo + i);
+    vv[u] = nt_load(V + i);
+    g[u] = nt_load(G + i);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i >= n4) break;
+    adam_one(p[u].x, g[u].x, mm[u].x, vv[u].x, h, c);
+    adam_one(p[u].y, g[u].y, mm[u].y, vv[u].y, h, c);
+    adam_one(p[u].z, g[u].z, mm[u].z, vv[u].z, h, c);
+    adam_one(p[u].w, g[u].w, mm[u].w, vv[u].w, h, c);
+    P[i] = p[u];
+    Mo[i] = mm[u];
+    V[i] = vv[u];
+    if (model != nullptr) {
+      if constexpr (sizeof(M) == 2) {
+        bf16x4 o;
+        o[0] = (__bf16)p[u].x; o[1] = (__bf16)p[u].y; o[2] = (__bf16)p[u].z; o[3] = (__bf16)p[u].w;
+        *reinterpret_cast<bf16x4*>(model + 4 * i) = o;
+      } else {
+        reinterpret_cast<float4*>(model)[i] = p[u];
+      }
+    }
+  }
+  if (blockIdx.x == 0) {  // scalar tail (n % 4)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += 256) {
+      float pp = master[i], mi = m[i], vi = v[i];
+      adam_one(pp, grad[i], mi, vi, h, c);
+      m[i] = mi;
+      v[i] = vi;
+      master[i] = pp;
+      if (model != nullptr) Io<M>::store(model + i, pp);
+    }
+  }
+}
+
+int g_adam_variant = 0;
+
 }  // namespace
+
+void adam_set_variant(int v) { g_adam_variant = v; }
 
 int sumsq_parts(int64_t n) {
   int64_t b = (n / 4 + 255) / 256;
@@ -173,6 +241,13 @@ template <typename M>
 void adam_step(float* master, M* model, const float* grad, float* m, float* v, int64_t n, const AdamHyper& h,
                const float* sumsq_ptr, hipStream_t s) {
   if (n == 0) return;
+  if (g_adam_variant == 1 && n >= 4) {
+    constexpr int U = 4;
+    const int64_t tiles = (n / 4 + 256 * U - 1) / (256 * U);
+    hipLaunchKernelGGL((adam_tile_kernel<M, U>), dim3((unsigned)tiles), dim3(256), 0, s, master, model, grad, m, v,
+                       n, h, sumsq_ptr);
+    return;
+  }
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;  // 16 blocks (64 waves) per CU queued; each thread loops
