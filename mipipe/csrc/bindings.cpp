@@ -298,10 +298,10 @@ void check_rows(const Tensor& t, const char* name) {
   MP_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) >= t.size(1), name, " must be 2-D with unit column stride");
 }
 
-std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignore_index) {
+std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignore_index, int64_t t_offset) {
   check_rows(logits, "logits");
   check_cuda(target, "target");
-  MP_CHECK(target.scalar_type() == at::kLong, "cross_entropy: target must be int64");
+  MP_CHECK(target.scalar_type() == at::kLong && target.is_contiguous(), "cross_entropy: target must be contiguous int64");
   MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0), "cross_entropy: expects [N, V] logits and [N] target");
   at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
   const int64_t rows = logits.size(0), V = logits.size(1);
@@ -312,44 +312,128 @@ std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignor
   dispatch_fb(logits, "cross_entropy_fwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     cross_entropy_fwd<T>(cptr<T>(logits), cptr<int64_t>(target), rows, V, logits.stride(0), ignore_index,
-                         ptr<float>(loss), ptr<float>(lse), s);
+                         ptr<float>(loss), ptr<float>(lse), s, t_offset);
   });
   return {loss, lse};
+}
+
+// A per-row fp32 vector, possibly strided (a column of a packed message's
+// statistic slots): its stride in floats.
+int64_t row_vector(const Tensor& t, int64_t rows, const char* name) {
+  MP_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 1 && t.size(0) == rows, name,
+           " must be a [rows] fp32 GPU tensor");
+  return rows > 1 ? t.stride(0) : 1;
+}
+
+// The statistic slots of a packed split-decoder message: `slots` is the
+// [rows, n] column slice after the hidden values, in the activation dtype.
+// Returns (fp32 word pointer, row stride in words, words per row).
+std::tuple<float*, int64_t, int> stat_slots(const Tensor& slots, int64_t rows, const char* name) {
+  MP_CHECK(slots.is_cuda(), name, " must be a GPU tensor");
+  MP_CHECK(slots.dim() == 2 && slots.size(0) == rows && slots.stride(1) == 1, name, " must be [rows, n] with unit column stride");
+  const int64_t es = slots.element_size();
+  const int64_t ld = rows > 1 ? slots.stride(0) : slots.size(1);
+  MP_CHECK((ld * es) % 4 == 0 && (slots.size(1) * es) % 4 == 0 && reinterpret_cast<uintptr_t>(slots.data_ptr()) % 4 == 0,
+           name, ": slots must hold whole, aligned fp32 words");
+  const int nslot = (int)(slots.size(1) * es / 4);
+  MP_CHECK(nslot >= 2 && nslot <= 256, name, ": need 2..256 fp32 words per row");
+  return {reinterpret_cast<float*>(slots.data_ptr()), ld * es / 4, nslot};
 }
 
 // out (optional): [N, >= V] destination with unit column stride (e.g. a
 // zero-padded vocabulary buffer); row_scale (optional): per-row scale, see loss.hip.
 // zero_pad: columns [V, out.size(1)) of `out` are zeroed (padded-vocabulary gradient).
+// lse / row_scale may be strided; scale and row_scale together multiply.
+// stat_out (optional): [N, n] slots receiving (lse, row scale) (split decoder).
 Tensor py_ce_bwd(Tensor logits, Tensor target, Tensor lse, std::optional<Tensor> scale, int64_t ignore_index,
-                 std::optional<Tensor> row_scale, std::optional<Tensor> out, bool zero_pad) {
+                 std::optional<Tensor> row_scale, std::optional<Tensor> out, bool zero_pad, int64_t t_offset,
+                 std::optional<Tensor> stat_out) {
   check_rows(logits, "logits");
-  MP_CHECK(logits.dim() == 2 && target.numel() == logits.size(0) && lse.numel() == logits.size(0),
-           "cross_entropy_bwd: shape mismatch");
-  MP_CHECK(scale.has_value() != row_scale.has_value(), "cross_entropy_bwd: give exactly one of scale / row_scale");
+  const int64_t rows = logits.size(0);
+  check_cuda(target, "target");
+  MP_CHECK(target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == rows,
+           "cross_entropy_bwd: target must be contiguous int64 [N]");
+  const int64_t ld_lse = row_vector(lse, rows, "lse");
+  MP_CHECK(scale.has_value() || row_scale.has_value(), "cross_entropy_bwd: give scale and/or row_scale");
   if (scale)
     MP_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->is_cuda(), "cross_entropy_bwd: bad scale");
-  if (row_scale)
-    MP_CHECK(row_scale->scalar_type() == at::kFloat && row_scale->numel() == logits.size(0) && row_scale->is_cuda() &&
-                 row_scale->is_contiguous(), "cross_entropy_bwd: bad row_scale");
+  const int64_t ld_rs = row_scale ? row_vector(*row_scale, rows, "row_scale") : 1;
   at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
   Tensor d;
   if (out) {
-    MP_CHECK(out->dim() == 2 && out->size(0) == logits.size(0) && out->size(1) >= logits.size(1) &&
+    MP_CHECK(out->dim() == 2 && out->size(0) == rows && out->size(1) >= logits.size(1) &&
                  out->stride(1) == 1 && out->scalar_type() == logits.scalar_type() && out->is_cuda(),
              "cross_entropy_bwd: bad out");
     d = *out;
   } else {
-    d = at::empty({logits.size(0), logits.size(1)}, logits.options());
+    d = at::empty({rows, logits.size(1)}, logits.options());
   }
+  float* st = nullptr;
+  int64_t ld_st = 0;
+  int nslot = 0;
+  if (stat_out) std::tie(st, ld_st, nslot) = stat_slots(*stat_out, rows, "stat_out");
   auto s = cur_stream(logits);
   dispatch_fb(logits, "cross_entropy_bwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     cross_entropy_bwd<T>(cptr<T>(logits), cptr<int64_t>(target), cptr<float>(lse),
                          scale ? cptr<float>(*scale) : nullptr, row_scale ? cptr<float>(*row_scale) : nullptr,
-                         logits.size(0), logits.size(1), logits.stride(0), d.stride(0), ignore_index, ptr<T>(d),
-                         zero_pad ? d.size(1) : logits.size(1), s);
+                         rows, logits.size(1), logits.stride(0), d.stride(0), ignore_index, ptr<T>(d),
+                         zero_pad ? d.size(1) : logits.size(1), s, t_offset, ld_lse, ld_rs, st, ld_st, nslot);
   });
   return d;
+}
+
+// Split-decoder head forward (mipipe/models/vocab_split.py): packs x into
+// out[:, :E] and (lse, target logit) into the slots out[:, E:].
+void py_vsplit_head_fwd(Tensor logits, Tensor target, Tensor x, Tensor out) {
+  check_rows(logits, "logits");
+  check_rows(x, "x");
+  check_rows(out, "out");
+  const int64_t rows = logits.size(0), E = x.size(1);
+  MP_CHECK(x.size(0) == rows && out.size(0) == rows && out.size(1) > E, "vsplit_head_fwd: shape mismatch");
+  MP_CHECK(x.scalar_type() == logits.scalar_type() && out.scalar_type() == x.scalar_type(), "vsplit_head_fwd: dtypes differ");
+  MP_CHECK(target.is_cuda() && target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == rows,
+           "vsplit_head_fwd: target must be contiguous int64 [N]");
+  const int64_t es = x.element_size();
+  MP_CHECK((E * es) % 16 == 0 && (x.stride(0) * es) % 16 == 0 && (out.stride(0) * es) % 16 == 0 &&
+               reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+               reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+           "vsplit_head_fwd: x / out rows must be 16-byte aligned");
+  auto [st, ld_st, nslot] = stat_slots(out.narrow(1, E, out.size(1) - E), rows, "out slots");
+  (void)st;
+  (void)ld_st;
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  auto s = cur_stream(logits);
+  dispatch_fb(logits, "vsplit_head_fwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    vsplit_head_fwd<T>(cptr<T>(logits), logits.stride(0), rows, logits.size(1), cptr<int64_t>(target), cptr<T>(x),
+                       x.stride(0), E, ptr<T>(out), out.stride(0), nslot, s);
+  });
+}
+
+// Split-decoder tail forward: returns (loss [] fp32, lse [N], weight [N] = valid / count).
+std::tuple<Tensor, Tensor, Tensor> py_vsplit_tail_fwd(Tensor logits, Tensor target, int64_t t_offset,
+                                                      int64_t ignore_index, Tensor slots) {
+  check_rows(logits, "logits");
+  const int64_t rows = logits.size(0);
+  MP_CHECK(target.is_cuda() && target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == rows,
+           "vsplit_tail_fwd: target must be contiguous int64 [N]");
+  auto [st, ld_st, nslot] = stat_slots(slots, rows, "slots");
+  (void)nslot;
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({}, fopt);
+  auto lse = at::empty({rows}, fopt);
+  auto loss_row = at::empty({rows}, fopt);
+  auto weight = at::empty({rows}, fopt);
+  auto s = cur_stream(logits);
+  dispatch_fb(logits, "vsplit_tail_fwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    vsplit_tail_fwd<T>(cptr<T>(logits), logits.stride(0), rows, logits.size(1), cptr<int64_t>(target), t_offset,
+                       ignore_index, st, ld_st, ptr<float>(lse), ptr<float>(loss_row), ptr<float>(weight),
+                       ptr<float>(loss), s);
+  });
+  return {loss, lse, weight};
 }
 
 // ------------------------------------------------------------------ embedding
@@ -378,29 +462,51 @@ std::tuple<Tensor, int64_t, int64_t> py_embed_fwd(Tensor tokens, Tensor weight, 
   return {out, (int64_t)seed, (int64_t)offset};
 }
 
-void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, double p, int64_t seed, int64_t offset) {
+// dpe (optional): fp32 [max_len, E] gradient of a learned position table, accumulated.
+void py_embed_bwd(Tensor tokens, Tensor dout, Tensor dweight, double scale, double p, int64_t seed, int64_t offset,
+                  std::optional<Tensor> dpe) {
   check_cuda(dout, "dout");
   check_cuda(dweight, "dweight");
+  check_cuda(tokens, "tokens");
+  MP_CHECK(tokens.scalar_type() == at::kLong && tokens.dim() == 2, "embedding_bwd: tokens must be int64 [B, S]");
   MP_CHECK(dweight.scalar_type() == at::kFloat && dweight.dim() == 2, "embedding_bwd: dweight must be fp32 [V, E]");
   const int64_t E = dweight.size(1), V = dweight.size(0);
   MP_CHECK(dout.numel() == tokens.numel() * E, "embedding_bwd: shape mismatch");
   MP_CHECK(E % 8 == 0 && E <= 8192, "embedding_bwd: E must be a multiple of 8 and at most 8192");
+  if (dpe) {
+    check_cuda(*dpe, "dpe");
+    MP_CHECK(dpe->scalar_type() == at::kFloat && dpe->dim() == 2 && dpe->size(1) == E &&
+                 dpe->size(0) >= tokens.size(1), "embedding_bwd: dpe must be fp32 [>= S, E]");
+  }
   at::hip::HIPGuardMasqueradingAsCUDA guard(dout.device());
   auto s = cur_stream(dout);
   dispatch_fb(dout, "embedding_bwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     embedding_bwd<T>(cptr<int64_t>(tokens), cptr<T>(dout), ptr<float>(dweight), tokens.numel(), (int)E, V,
-                     (float)scale, (float)p, (uint64_t)seed, (uint64_t)offset, s);
+                     (float)scale, (float)p, (uint64_t)seed, (uint64_t)offset, s, dpe ? ptr<float>(*dpe) : nullptr,
+                     (int)tokens.size(1));
   });
 }
 
 // ------------------------------------------------------------------ GEMM
 // GEMM operands: bf16 (v_mfma_f32_16x16x32_bf16 kernel) or fp32 (v_mfma_f32_32x32x2_f32 kernel).
+// Layout (unit column stride, aligned row stride) is checked by row_stride().
 void check_gemm_2d(const Tensor& t, const char* name) {
-  check_cuda(t, name);
+  MP_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   MP_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name, " must be bf16 or fp32");
   MP_CHECK(t.dim() == 2, name, " must be 2-D");
   MP_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+// Row stride of a 2-D GEMM operand / output: unit column stride and 16-byte
+// aligned rows (the tile kernels move 16-byte chunks), so row-strided views
+// -- a column slice of a packed activation -- need no copy.
+int64_t row_stride(const Tensor& t, const char* name) {
+  MP_CHECK(t.dim() == 2 && (t.stride(1) == 1 || t.size(1) == 1), name, " must have unit column stride");
+  const int64_t ld = t.size(0) > 1 ? t.stride(0) : t.size(1);
+  MP_CHECK(ld >= t.size(1) && (ld * (int64_t)t.element_size()) % 16 == 0, name,
+           ": rows must be 16-byte aligned (row stride ", ld, ")");
+  return ld;
 }
 
 void check_same_dtype(const Tensor& a, const Tensor& b, const char* what) {
@@ -439,7 +545,7 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   if (res) {
     check_gemm_2d(*res, "res");
     check_same_dtype(x, *res, "linear_fwd res");
-    MP_CHECK(res->size(0) == M && res->size(1) == N && res->is_contiguous(), "linear_fwd: res must be contiguous [M, N]");
+    MP_CHECK(res->size(0) == M && res->size(1) == N, "linear_fwd: res must be [M, N]");
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty({M, N}, x.options());
@@ -450,8 +556,11 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   GemmArgs g;
   g.A = x.data_ptr(); g.B = w.data_ptr(); g.C = y.data_ptr();
   g.bias = bias ? bias->data_ptr() : nullptr; g.aux = pre ? pre->data_ptr() : nullptr;
-  if (res) g.res = res->data_ptr();  // y = res + dropout(act(x . w^T + b)): the residual add in the epilogue
-  g.lda = K; g.ldb = K; g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  if (res) {
+    g.res = res->data_ptr();  // y = res + dropout(act(x . w^T + b)): the residual add in the epilogue
+    g.ldr = row_stride(*res, "res");
+  }
+  g.lda = row_stride(x, "x"); g.ldb = row_stride(w, "w"); g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreAct; g.act = (int)act; g.p = (float)p;
   g.seed = seed; g.offset = offset;
   gemm_run(dt, g, cur_stream(x));
@@ -474,7 +583,11 @@ Tensor split_k_workspace(GemmArgs& g, at::ScalarType dt, const Tensor& like) {
 // dx[M,K] = dy[M,N] . w[N,K]
 // dx = dy . w (+ res): `res` is the gradient the input receives from its
 // other consumer (a residual branch), added in the epilogue.
-Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
+// act (optional, with `saved`): the output is the gradient of the activation's
+// INPUT -- act'(saved) (and the forward's dropout mask: p, seed, offset) applied
+// in the epilogue (GELU: saved = the pre-activation; ReLU: saved = the output).
+Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res, std::optional<Tensor> out, int64_t act,
+                       std::optional<Tensor> saved, double p, int64_t seed, int64_t offset) {
   check_gemm_2d(dy, "dy");
   check_gemm_2d(w, "w");
   check_same_dtype(dy, w, "linear_dgrad");
@@ -485,15 +598,47 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res) {
   if (res) {
     check_gemm_2d(*res, "res");
     check_same_dtype(dy, *res, "linear_dgrad res");
-    MP_CHECK(res->size(0) == M && res->size(1) == K && res->is_contiguous(), "linear_dgrad: res must be contiguous [M, K]");
+    MP_CHECK(res->size(0) == M && res->size(1) == K, "linear_dgrad: res must be [M, K]");
+  }
+  MP_CHECK(act == kActNone || act == kActRelu || act == kActGelu, "linear_dgrad: bad act");
+  if (act != kActNone) {
+    MP_CHECK(saved.has_value() && dt == at::kBFloat16 && !res, "linear_dgrad: the activation backward needs bf16 "
+             "operands, the saved tensor and no residual addend");
+    check_gemm_2d(*saved, "saved");
+    check_same_dtype(dy, *saved, "linear_dgrad saved");
+    MP_CHECK(saved->size(0) == M && saved->size(1) == K, "linear_dgrad: saved must be [M, K]");
+    MP_CHECK(p >= 0.0 && p < 1.0, "linear_dgrad: bad p");
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
-  auto dx = at::empty({M, K}, dy.options());
+  Tensor dx;
+  if (out) {  // a (row-strided) destination, e.g. the columns of a packed gradient message
+    check_gemm_2d(*out, "out");
+    MP_CHECK(out->size(0) == M && out->size(1) == K && out->scalar_type() == dt, "linear_dgrad: bad out");
+    dx = *out;
+  } else {
+    dx = at::empty({M, K}, dy.options());
+  }
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = w.data_ptr(); g.C = dx.data_ptr();
-  if (res) g.res = res->data_ptr();
-  g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)M; g.N = (int)K; g.K = (int)N;
+  if (res) {
+    g.res = res->data_ptr();
+    g.ldr = row_stride(*res, "res");
+  }
+  g.lda = row_stride(dy, "dy"); g.ldb = row_stride(w, "w"); g.ldc = row_stride(dx, "out");
+  g.M = (int)M; g.N = (int)K; g.K = (int)N;
   g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreAct;
+  if (act != kActNone) {
+    g.dact_in = saved->data_ptr();
+    g.ldd = row_stride(*saved, "saved");
+    g.dact = (int)act;
+    if (act == kActRelu) {  // the saved output's sign is the mask as well
+      g.dact_scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+    } else {
+      g.p = (float)p;
+      g.seed = (uint64_t)seed;
+      g.offset = (uint64_t)offset;
+    }
+  }
   Tensor ws = split_k_workspace(g, dt, dy);
   gemm_run(dt, g, cur_stream(dy));
   return dx;
@@ -513,7 +658,7 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad, bool accumulate) {
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = x.data_ptr(); g.C = main_grad.data_ptr();
-  g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)T;
+  g.lda = row_stride(dy, "dy"); g.ldb = row_stride(x, "x"); g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)T;
   g.a_kc = false; g.b_kc = false; g.epi = accumulate ? kEpiAccumF32 : kEpiStoreF32;
   Tensor ws = split_k_workspace(g, dt, dy);
   gemm_run(dt, g, cur_stream(dy));
@@ -594,13 +739,17 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
              "linear_wgrad_segments: every micro-batch needs the same [T, N] / [T, K] shapes");
   }
   MP_CHECK(T % 64 == 0 && gemm_ok(dt, N, K, T), "linear_wgrad_segments: unsupported shape");
+  const int64_t lda = row_stride(dys[0], "dy"), ldb = row_stride(xs[0], "x");
+  for (size_t i = 1; i < dys.size(); ++i)
+    MP_CHECK(row_stride(dys[i], "dy") == lda && row_stride(xs[i], "x") == ldb,
+             "linear_wgrad_segments: every micro-batch needs the same row strides");
   at::hip::HIPGuardMasqueradingAsCUDA guard(main_grad.device());
   const int total = (int)dys.size();
   for (int first = 0; first < total; first += GemmArgs::kMaxSegs) {
     const int n = std::min(GemmArgs::kMaxSegs, total - first);
     GemmArgs g;
     g.C = main_grad.data_ptr();
-    g.lda = N; g.ldb = K; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)(T * n);
+    g.lda = lda; g.ldb = ldb; g.ldc = K; g.M = (int)N; g.N = (int)K; g.K = (int)(T * n);
     g.a_kc = false; g.b_kc = false; g.epi = (accumulate || first > 0) ? kEpiAccumF32 : kEpiStoreF32;
     g.seg_k = (int)T;
     for (int i = 0; i < n; ++i) {
@@ -629,7 +778,7 @@ Tensor py_gemm_f32(Tensor a, Tensor b, bool a_kc, bool b_kc) {
   auto c = at::empty({M, N}, a.options().dtype(at::kFloat));
   GemmArgs g;
   g.A = a.data_ptr(); g.B = b.data_ptr(); g.C = c.data_ptr();
-  g.lda = a.size(1); g.ldb = b.size(1); g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.lda = row_stride(a, "a"); g.ldb = row_stride(b, "b"); g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.a_kc = a_kc; g.b_kc = b_kc; g.epi = kEpiStoreF32;
   gemm_run(dt, g, cur_stream(a));
   return c;
@@ -880,12 +1029,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_act_bwd", &py_bias_act_bwd, py::arg("dy"), py::arg("saved"), py::arg("bias"), py::arg("act"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dbias"), py::arg("dbias_acc") = py::none());
   m.def("column_sum", &py_column_sum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
-  m.def("cross_entropy_fwd", &py_ce_fwd);
+  m.def("cross_entropy_fwd", &py_ce_fwd, py::arg("logits"), py::arg("target"), py::arg("ignore_index"),
+        py::arg("t_offset") = 0);
   m.def("cross_entropy_bwd", &py_ce_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("scale"),
         py::arg("ignore_index"), py::arg("row_scale") = py::none(), py::arg("out") = py::none(),
-        py::arg("zero_pad") = false);
+        py::arg("zero_pad") = false, py::arg("t_offset") = 0, py::arg("stat_out") = py::none());
+  m.def("vsplit_head_fwd", &py_vsplit_head_fwd);
+  m.def("vsplit_tail_fwd", &py_vsplit_tail_fwd);
   m.def("embedding_fwd", &py_embed_fwd);
-  m.def("embedding_bwd", &py_embed_bwd);
+  m.def("embedding_bwd", &py_embed_bwd, py::arg("tokens"), py::arg("dout"), py::arg("dweight"), py::arg("scale"),
+        py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("dpe") = py::none());
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });
   m.def("attention_f32_supported", [](int64_t S, int64_t D) { return attention_f32_supported((int)S, (int)D); });
   m.def("attention_fwd", &py_attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"), py::arg("p"),
@@ -906,7 +1059,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none());
-  m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none());
+  m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none(),
+        py::arg("out") = py::none(), py::arg("act") = 0, py::arg("saved") = py::none(), py::arg("p") = 0.0,
+        py::arg("seed") = 0, py::arg("offset") = 0);
   m.def("linear_wgrad", &py_linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("main_grad"),
         py::arg("accumulate") = true);
   m.def("linear_wgrad_segments", &py_linear_wgrad_segments, py::arg("dys"), py::arg("xs"), py::arg("main_grad"),

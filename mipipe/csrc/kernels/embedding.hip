@@ -53,15 +53,20 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restric
 // lane-contiguous float atomics: one 256-byte request per wave-instruction
 // (memory-side atomics run at ~1.3 TB/s of added bytes; a lane stride of 32 B
 // would cut that 8x).  Rows of E <= 8192 elements.
+// dpe (optional): the learned position table's fp32 gradient -- the same
+// masked row (without the token scale) is added at the row's position, so
+// GPT-2's position embedding needs no separate reduction over the batch.
 template <typename T>
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restrict__ tokens, const T* __restrict__ dout,
-                                                        float* __restrict__ dweight, int E, int64_t V, float scale,
-                                                        float p, uint32_t threshold, uint64_t seed, uint64_t offset) {
+                                                        float* __restrict__ dweight, float* __restrict__ dpe,
+                                                        int seq_len, int E, int64_t V, float scale, float p,
+                                                        uint32_t threshold, uint64_t seed, uint64_t offset) {
   __shared__ float rowbuf[8192];
   const int64_t row = blockIdx.x;
   const int64_t tok = tokens[row];
-  if (tok < 0 || tok >= V) return;
-  const float pscale = p > 0.f ? scale / (1.f - p) : scale;
+  const bool tok_ok = tok >= 0 && tok < V;
+  if (!tok_ok && dpe == nullptr) return;
+  const float pscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   for (int vi = threadIdx.x; vi < E / 8; vi += blockDim.x) {
     float g[8];
     const int64_t e = row * E + vi * 8;
@@ -72,8 +77,14 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restric
     for (int i = 0; i < 8; ++i) rowbuf[vi * 8 + i] = ((keep >> i) & 1) ? g[i] * pscale : 0.f;
   }
   __syncthreads();
-  float* dst = dweight + tok * E;
-  for (int c = threadIdx.x; c < E; c += blockDim.x) atomicAdd(dst + c, rowbuf[c]);
+  if (tok_ok) {
+    float* dst = dweight + tok * E;
+    for (int c = threadIdx.x; c < E; c += blockDim.x) atomicAdd(dst + c, rowbuf[c] * scale);
+  }
+  if (dpe != nullptr) {
+    float* dst = dpe + (row % seq_len) * E;
+    for (int c = threadIdx.x; c < E; c += blockDim.x) atomicAdd(dst + c, rowbuf[c]);
+  }
 }
 
 }  // namespace
@@ -88,15 +99,15 @@ void embedding_fwd(const int64_t* tokens, const T* weight, const float* pe, T* o
 
 template <typename T>
 void embedding_bwd(const int64_t* tokens, const T* dout, float* dweight, int64_t rows, int E, int64_t V, float scale,
-                   float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+                   float p, uint64_t seed, uint64_t offset, hipStream_t s, float* dpe, int seq_len) {
   if (rows == 0 || E > 8192) return;  // callers check embedding_supported
-  hipLaunchKernelGGL((embed_bwd_kernel<T>), dim3((unsigned)rows), dim3(256), 0, s, tokens, dout, dweight, E, V, scale,
-                     p, dropout_threshold(p), seed, offset);
+  hipLaunchKernelGGL((embed_bwd_kernel<T>), dim3((unsigned)rows), dim3(256), 0, s, tokens, dout, dweight, dpe,
+                     seq_len > 0 ? seq_len : 1, E, V, scale, p, dropout_threshold(p), seed, offset);
 }
 
 template void embedding_fwd<float>(const int64_t*, const float*, const float*, float*, int64_t, int, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
 template void embedding_fwd<bf16_t>(const int64_t*, const bf16_t*, const float*, bf16_t*, int64_t, int, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
-template void embedding_bwd<float>(const int64_t*, const float*, float*, int64_t, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
-template void embedding_bwd<bf16_t>(const int64_t*, const bf16_t*, float*, int64_t, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
+template void embedding_bwd<float>(const int64_t*, const float*, float*, int64_t, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t, float*, int);
+template void embedding_bwd<bf16_t>(const int64_t*, const bf16_t*, float*, int64_t, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t, float*, int);
 
 }  // namespace mipipe

@@ -134,6 +134,13 @@ __device__ __forceinline__ float erf_as(float x) {
   return copysignf(y, x);
 }
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erf_as(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+// act'(s) for the activation-backward epilogue (GemmArgs::dact): ReLU's from its output.
+__device__ __forceinline__ float dact_f(int dact, float s) {
+  return dact == kActRelu ? (s > 0.f ? 1.f : 0.f) : gelu_grad_f(s);
+}
 
 // Bijective XCD-aware remap + grouped (8 tile-rows) ordering.
 __device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn, int G = 8) {
@@ -251,7 +258,10 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (g.res != nullptr) out[r] += bf2f(reinterpret_cast<const bf16_t*>(g.res)[(int64_t)(row0 + r) * g.ldc + col]);
+          if (g.dact_in != nullptr)
+            out[r] *= g.dact_scale *
+                      dact_f(g.dact, bf2f(reinterpret_cast<const bf16_t*>(g.dact_in)[(int64_t)(row0 + r) * g.ldd + col]));
+          if (g.res != nullptr) out[r] += bf2f(reinterpret_cast<const bf16_t*>(g.res)[(int64_t)(row0 + r) * g.ldr + col]);
           C[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out[r]);
           if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre[r]);
         }
@@ -424,7 +434,8 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
 template <int EPI, int W>
 __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W / 64], int wm, int wn, int lane,
                                              int tid, int m0, int n0, int M, int N, int64_t ldc, void* out,
-                                             const bf16_t* res) {
+                                             const bf16_t* res, int64_t ldr = 0, const bf16_t* dact_in = nullptr,
+                                             int64_t ldd = 0, int dact = 0, float dact_scale = 1.f) {
   constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512;
   const int quad = lane >> 4, col_in = lane & 15;
   float* stg = reinterpret_cast<float*>(smem);
@@ -453,8 +464,13 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
         const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8 + 4);
         const int64_t at = (int64_t)(rbase + row) * ldc + n0 + 8 * c8;
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dact_in != nullptr) {  // activation backward: x act'(saved)
+          const bf16x8 sv = *reinterpret_cast<const bf16x8*>(dact_in + (int64_t)(rbase + row) * ldd + n0 + 8 * c8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= dact_scale * dact_f(dact, (float)sv[e]);
+        }
         if (res != nullptr) {
-          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + at);
+          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (int64_t)(rbase + row) * ldr + n0 + 8 * c8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
         }
@@ -686,8 +702,13 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   void* out = EPI == kEpiStoreBf16 ? g.C
                                    : reinterpret_cast<void*>(reinterpret_cast<float*>(g.C) +
                                                              (int64_t)blockIdx.y * g.M * g.ldc);  // split-K partial y
-  staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
-                       EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr);
+  if (EPI == kEpiStoreBf16 && g.dact_in != nullptr)
+    staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+                         reinterpret_cast<const bf16_t*>(g.res), g.ldr, reinterpret_cast<const bf16_t*>(g.dact_in),
+                         g.ldd, g.dact, g.dact_scale);
+  else
+    staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+                         EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
 }
 
 }  // namespace big
@@ -770,7 +791,7 @@ void launch(const GemmArgs& gi, hipStream_t s) {
 // C[M, N] (bf16, row stride ldc) = sum of the k_splits fp32 partials [s][M][N]
 // (+ res): 8 columns per thread, 16-byte loads and stores.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                                            int64_t ldc, const bf16_t* __restrict__ res,
+                                                            int64_t ldc, const bf16_t* __restrict__ res, int64_t ldr,
                                                             bf16_t* __restrict__ C) {
   const int64_t chunks = (int64_t)M * (N / 8);
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -786,7 +807,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   const int64_t out = (int64_t)row * ldc + col;
   if (res != nullptr) {
-    const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + out);
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + (int64_t)row * ldr + col);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
   }
@@ -854,7 +875,7 @@ int gemm_splitk_factor(const GemmArgs& g) {
   }
   if (g_gemm_splitk == 0) return 1;
   const bool plain_bf16 = g.epi == kEpiStoreBf16 && g.act == kActNone && g.bias == nullptr && g.p <= 0.f &&
-                          g.aux == nullptr;
+                          g.aux == nullptr && g.dact_in == nullptr;
   const bool f32_out = g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32;
   if (!(plain_bf16 || f32_out) || !use_big(g) || g.K < 8192) return 1;
   const int tiles = big_tiles(g, 256);
@@ -915,6 +936,7 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
       c.bias = byte_off(g.bias, (int64_t)lo * 2);
       c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * 2));
       c.res = byte_off(g.res, (int64_t)lo * 2);
+      c.dact_in = byte_off(g.dact_in, (int64_t)lo * 2);
     } else {
       c.M = hi - lo;
       c.mask_row0 = g.mask_row0 + lo;
@@ -923,7 +945,8 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
       for (int i = 0; i < GemmArgs::kMaxSegs; ++i) c.a_seg[i] = byte_off(g.a_seg[i], aoff);
       c.C = const_cast<char*>(byte_off(g.C, (int64_t)lo * g.ldc * cbytes));
       c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * g.ldc * 2));
-      c.res = byte_off(g.res, (int64_t)lo * g.ldc * 2);
+      c.res = byte_off(g.res, (int64_t)lo * g.ldr * 2);
+      c.dact_in = byte_off(g.dact_in, (int64_t)lo * g.ldd * 2);
     }
     run(c);
   }
@@ -933,6 +956,8 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
 void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
   GemmArgs g = gi;
   g.threshold = dropout_threshold(g.p);
+  if (g.ldr == 0) g.ldr = g.ldc;
+  if (g.ldd == 0) g.ldd = g.ldc;
   if (g.k_splits > 1) {
     // fp32 partials into the caller's workspace, then one reduction (+ res)
     GemmArgs p = g;
@@ -947,7 +972,7 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
     if (g.epi == kEpiStoreBf16) {
       const int64_t chunks = (int64_t)g.M * (g.N / 8);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws,
-                         g.k_splits, g.M, g.N, g.ldc, reinterpret_cast<const bf16_t*>(g.res),
+                         g.k_splits, g.M, g.N, g.ldc, reinterpret_cast<const bf16_t*>(g.res), g.ldr,
                          reinterpret_cast<bf16_t*>(g.C));
     } else {
       const int64_t chunks = (int64_t)g.M * (g.N / 4);

@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (Cfg<WM, WN, TM, TN>::kBlocksPer
             if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
             if (col_ok && row < g.M) {
               const int64_t o = (int64_t)row * g.ldc + col;
-              if (g.res != nullptr) out += reinterpret_cast<const float*>(g.res)[o];
+              if (g.res != nullptr) out += reinterpret_cast<const float*>(g.res)[(int64_t)row * g.ldr + col];
               C[o] = out;
               if (g.aux != nullptr) reinterpret_cast<float*>(g.aux)[o] = pre;
             }
@@ -374,6 +374,7 @@ bool gemm_f32_supported(int64_t M, int64_t N, int64_t K) {
 void gemm_f32(const GemmArgs& gi, hipStream_t s) {
   GemmArgs g = gi;
   g.threshold = dropout_threshold(g.p);
+  if (g.ldr == 0) g.ldr = g.ldc;
   if (g.epi == kEpiStoreAct) launch_layout<kEpiStoreAct>(g, s);
   else if (g.epi == kEpiAccumF32) launch_layout<kEpiAccumF32>(g, s);
   else launch_layout<kEpiStoreF32>(g, s);

@@ -96,8 +96,18 @@ struct GemmArgs {
   void* C = nullptr;        // bf16 or fp32 (epilogue)
   const void* bias = nullptr;  // bf16 [N] (kEpiStoreBf16 only)
   void* aux = nullptr;         // bf16 pre-activation output (optional)
-  const void* res = nullptr;   // bf16 [M, ldc] added to the bf16 output (optional, kEpiStoreBf16)
+  const void* res = nullptr;   // bf16 [M, ldr] added to the bf16 output (optional, kEpiStoreBf16)
   int64_t lda = 0, ldb = 0, ldc = 0;
+  int64_t ldr = 0;             // row stride of res (0: ldc)
+  // Activation backward in the bf16 epilogue (a dgrad GEMM whose output is the
+  // gradient of an activation's output): C = acc [x dropout mask (p, seed,
+  // offset: the forward's)] x act'(dact_in) x dact_scale.  dact_in is the
+  // forward's saved pre-activation (GELU) or output (ReLU: its sign carries the
+  // dropout mask too, so p = 0 and dact_scale = 1 / (1 - p)); row stride ldd.
+  const void* dact_in = nullptr;
+  int dact = 0;
+  float dact_scale = 1.f;
+  int64_t ldd = 0;
   int M = 0, N = 0, K = 0;
   bool a_kc = true;   // A stored [M, K] (true) or [K, M] (false)
   bool b_kc = true;   // B stored [N, K] (true) or [K, N] (false)
@@ -184,21 +194,39 @@ void attention_f32_fwd(const AttnArgs& a, hipStream_t s);
 void attention_f32_bwd(const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ loss
+// t_offset: logits are vocabulary columns [t_offset, t_offset + V) (split decoder).
 template <typename T>
 void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
-                       int64_t ignore_index, float* loss, float* lse, hipStream_t s);
+                       int64_t ignore_index, float* loss, float* lse, hipStream_t s, int64_t t_offset = 0);
+// lse / row_scale read with strides ld_lse / ld_rs (floats); stat_out: (lse,
+// scale) written to nslot fp32 words per row (split-decoder gradient slots).
 template <typename T>
 void cross_entropy_bwd(const T* logits, const int64_t* target, const float* lse, const float* scale,
                        const float* row_scale, int64_t rows, int64_t V, int64_t ld, int64_t ld_out,
-                       int64_t ignore_index, T* dlogits, int64_t zero_to, hipStream_t s);
+                       int64_t ignore_index, T* dlogits, int64_t zero_to, hipStream_t s, int64_t t_offset = 0,
+                       int64_t ld_lse = 1, int64_t ld_rs = 1, float* stat_out = nullptr, int64_t ld_stat = 0,
+                       int nslot = 0);
+// Split-decoder head forward: out[r] = [x[r] (E values) | lse, target logit, 0 ...]
+// (nslot fp32 words); E * sizeof(T) % 16 == 0, 16-byte aligned rows.
+template <typename T>
+void vsplit_head_fwd(const T* logits, int64_t ld, int64_t rows, int64_t V, const int64_t* target, const T* x,
+                     int64_t ldx, int64_t E, T* out, int64_t ldo, int nslot, hipStream_t s);
+// Split-decoder tail forward: full lse per row from this slice and the head's
+// slot statistics (stats: lse_a, t_a at stride ld_st floats), the mean loss
+// into loss[0] and per-row weights valid / count.
+template <typename T>
+void vsplit_tail_fwd(const T* logits, int64_t ld, int64_t rows, int64_t V, const int64_t* target, int64_t t_offset,
+                     int64_t ignore_index, const float* stats, int64_t ld_st, float* lse, float* loss_row,
+                     float* weight_row, float* loss, hipStream_t s);
 
 // ------------------------------------------------------------------ embedding
 template <typename T>
 void embedding_fwd(const int64_t* tokens, const T* weight, const float* pe, T* out, int64_t rows, int seq_len, int E,
                    int64_t V, float scale, float p, uint64_t seed, uint64_t offset, hipStream_t s);
+// dpe (optional): fp32 [>= seq_len, E] learned-position gradient, += the masked rows by position.
 template <typename T>
 void embedding_bwd(const int64_t* tokens, const T* dout, float* dweight, int64_t rows, int E, int64_t V, float scale,
-                   float p, uint64_t seed, uint64_t offset, hipStream_t s);
+                   float p, uint64_t seed, uint64_t offset, hipStream_t s, float* dpe = nullptr, int seq_len = 0);
 
 // ------------------------------------------------------------------ optimizer
 struct AdamHyper {

@@ -74,12 +74,8 @@ class Encoder(nn.Module):
                 self.pe.copy_(sinusoidal_positions(self.max_len, self.d_model))
 
     def forward(self, tokens: Tensor) -> Tensor:
+        # learned positions: the fused kernels add them and accumulate their gradient
         pe = self.pos_weight if self.learned_positions else self.pe
-        if self.learned_positions and tokens.is_cuda:
-            # Learned positions need a gradient: add them outside the fused kernel.
-            x = ops.embed_scale_posenc_dropout(tokens, self.weight, None, self.scale, 0.0, self.training)
-            x = x + pe[: tokens.shape[1]].to(x.dtype)
-            return torch.nn.functional.dropout(x, self.dropout, self.training)
         return ops.embed_scale_posenc_dropout(tokens, self.weight, pe, self.scale, self.dropout, self.training)
 
     def flops_per_token(self, seq_len: int) -> float:

@@ -29,11 +29,14 @@ import torch
 from torch import Tensor, nn
 
 from .. import ops
-from ..ops.linear import mark_gemm_weight
+from ..ops.linear import ActFold, mark_gemm_weight
 
 # Fan-out fusion of the residual-branch gradient (see AttentionCore.forward_fanout);
 # MIPIPE_FANOUT=0 turns it off (A/B measurements).
 FANOUT = os.environ.get("MIPIPE_FANOUT", "1") != "0"
+# MLP activation backward in fc_out's dgrad epilogue (ops.linear.ActFold);
+# MIPIPE_FOLD_ACT=0 turns it off (A/B measurements).
+FOLD_ACT = os.environ.get("MIPIPE_FOLD_ACT", "1") != "0"
 
 __all__ = [
     "AttentionCore",
@@ -274,8 +277,9 @@ class FeedForwardIn(nn.Module):
     def forward(self, x: Tensor) -> Tensor:
         return self.forward_fanout(x, fanout=False)[0]
 
-    def forward_fanout(self, x: Tensor, fanout: bool = True):
-        """``(h, x')`` -- see :meth:`AttentionCore.forward_fanout`."""
+    def forward_fanout(self, x: Tensor, fanout: bool = True, fold: Optional[ActFold] = None):
+        """``(h, x')`` -- see :meth:`AttentionCore.forward_fanout`.  ``fold``: h's
+        only consumer applies the activation backward (:class:`ActFold`)."""
         p = self.dropout if self.training else 0.0
         w, b, act = self.linear1_weight, self.linear1_bias, self.activation
         if self.norm_first:
@@ -284,10 +288,10 @@ class FeedForwardIn(nn.Module):
             else:
                 xn, xr = ops.add_dropout_layer_norm(x, None, self.norm_weight, self.norm_bias, self.eps, 0.0,
                                                     self.training), x
-            return ops.linear(xn, w, b, act, p, self.training), xr
+            return ops.linear(xn, w, b, act, p, self.training, act_fold_out=fold), xr
         if fanout:
-            return ops.linear_fanout(x, w, b, act, p, self.training)
-        return ops.linear(x, w, b, act, p, self.training), x
+            return ops.linear_fanout(x, w, b, act, p, self.training, act_fold_out=fold)
+        return ops.linear(x, w, b, act, p, self.training, act_fold_out=fold), x
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2 * self.d_model * self.dim_feedforward
@@ -317,11 +321,12 @@ class FeedForwardOut(nn.Module):
             nn.init.ones_(self.norm_weight)
             nn.init.zeros_(self.norm_bias)
 
-    def forward(self, x: Tensor, h: Tensor) -> Tensor:
+    def forward(self, x: Tensor, h: Tensor, fold: Optional[ActFold] = None) -> Tensor:
         p = self.dropout if self.training else 0.0
         if self.norm_first:
-            return ops.linear_residual(h, self.linear2_weight, self.linear2_bias, x, p, self.training)
-        h = ops.linear(h, self.linear2_weight, self.linear2_bias)
+            return ops.linear_residual(h, self.linear2_weight, self.linear2_bias, x, p, self.training,
+                                       act_fold_in=fold)
+        h = ops.linear(h, self.linear2_weight, self.linear2_bias, act_fold_in=fold)
         return ops.add_dropout_layer_norm(h, x, self.norm_weight, self.norm_bias, self.eps, p, self.training)
 
     def flops_per_token(self, seq_len: int) -> float:
@@ -357,8 +362,10 @@ class FeedForwardBlock(nn.Module):
         self.fc_out.reset_parameters()
 
     def forward(self, x: Tensor) -> Tensor:
-        h, xr = self.fc_in.forward_fanout(x, FANOUT)
-        return self.fc_out(xr, h)
+        # h's only consumer is fc_out: its dgrad applies the activation backward
+        fold = ActFold() if FOLD_ACT else None
+        h, xr = self.fc_in.forward_fanout(x, FANOUT, fold)
+        return self.fc_out(xr, h, fold)
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2 * 2 * self.d_model * self.dim_feedforward

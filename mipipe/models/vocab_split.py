@@ -30,7 +30,7 @@ import torch
 from torch import Tensor, nn
 
 from ..ops._util import kernels_for
-from ..ops.linear import accumulable, accumulate_wgrad, mark_gemm_weight
+from ..ops.linear import accumulable, accumulate_wgrad, gemm_operand, mark_gemm_weight
 
 __all__ = ["DecoderHead", "DecoderTail", "split_point", "split_decoder", "STAT_SLOTS"]
 
@@ -51,8 +51,14 @@ def _tile_linear(k, x2: Tensor, w: Tensor, b: Tensor) -> Tuple[Tensor, bool]:
     return torch.addmm(b, x2, w.t()), False
 
 
-def _dgrad(k, tile: bool, d: Tensor, w: Tensor) -> Tensor:
-    return k.linear_dgrad(d, w) if tile else torch.matmul(d, w)
+def _dgrad_into(k, tile: bool, d: Tensor, w: Tensor, res: Optional[Tensor], out: Tensor) -> None:
+    """out = d . w (+ res), written in place (out may be a column slice)."""
+    if tile:
+        k.linear_dgrad(d, w, res, out)
+    elif res is not None:
+        out.copy_(torch.addmm(res, d, w))
+    else:
+        out.copy_(torch.mm(d, w))
 
 
 def _bias_grad(k, d: Tensor, b: Tensor) -> Optional[Tensor]:
@@ -66,27 +72,25 @@ def _bias_grad(k, d: Tensor, b: Tensor) -> Optional[Tensor]:
     return d.sum(0).to(b.dtype)
 
 
-def _lse_and_target(k, logits: Tensor, tgt: Tensor) -> Tuple[Tensor, Tensor]:
-    """Row log-sum-exp and the logit at ``tgt`` (rows with tgt < 0: undefined)."""
-    if k is not None:
-        loss_rows, lse = k.cross_entropy_fwd(logits, tgt, -1)
-        return lse, lse - loss_rows
-    lf = logits.float()
-    lse = torch.logsumexp(lf, dim=-1)
-    return lse, lf.gather(1, tgt.clamp(min=0)[:, None])[:, 0]
+def _slot_words(t2: Tensor, e: int) -> Tensor:
+    """The statistic slots of packed rows ``t2 = [h (e values) | slots]`` as a
+    [rows, words] fp32 view -- no copy."""
+    if t2.dtype == torch.float32:
+        return t2[:, e:]
+    return t2.view(torch.float32)[:, e * t2.element_size() // 4:]
 
 
-def _softmax_grad(k, logits: Tensor, tgt: Tensor, lse: Tensor, g_row: Tensor, out: Tensor) -> Tensor:
-    """out[:, :V] = (exp(logits - lse) - onehot(tgt)) * g_row (tgt < 0: no one-hot)."""
-    if k is not None:
-        return k.cross_entropy_bwd(logits, tgt, lse, None, -1, row_scale=g_row, out=out)
-    p = torch.exp(logits.float() - lse[:, None])
-    rows = torch.nonzero(tgt >= 0)[:, 0]
-    p[rows, tgt[rows]] -= 1.0
-    out[:, : logits.shape[1]] = (p * g_row[:, None]).to(out.dtype)
-    return out
+def _targets(target: Tensor, device) -> Tensor:
+    return target.reshape(-1).to(device=device, dtype=torch.int64).contiguous()
 
 
+def _native(k, x2: Tensor) -> bool:
+    """The HIP path: pack / statistics kernels move 16-byte row chunks."""
+    es = x2.element_size()
+    return k is not None and (x2.shape[1] * es) % 16 == 0 and (STAT_SLOTS * es) % 16 == 0
+
+
+# ---------------------------------------------------------------- CPU (reference) path
 def _stats_to_slots(a: Tensor, b: Tensor, dtype: torch.dtype) -> Tensor:
     buf = torch.zeros(a.shape[0], STAT_SLOTS, dtype=dtype, device=a.device)
     f = buf.view(torch.float32)
@@ -95,76 +99,123 @@ def _stats_to_slots(a: Tensor, b: Tensor, dtype: torch.dtype) -> Tensor:
     return buf
 
 
-def _slots_to_stats(slots: Tensor) -> Tuple[Tensor, Tensor]:
-    f = slots.contiguous().view(torch.float32)
-    return f[:, 0].contiguous(), f[:, 1].contiguous()
+def _softmax_grad(logits: Tensor, tgt: Tensor, lse: Tensor, g_row: Tensor, out: Tensor) -> None:
+    """out[:, :V] = (exp(logits - lse) - onehot(tgt)) * g_row (tgt outside [0, V): no one-hot)."""
+    p = torch.exp(logits.float() - lse[:, None])
+    rows = torch.nonzero((tgt >= 0) & (tgt < logits.shape[1]))[:, 0]
+    p[rows, tgt[rows]] -= 1.0
+    out[:, : logits.shape[1]] = (p * g_row[:, None]).to(out.dtype)
 
 
 class _HeadFn(torch.autograd.Function):
+    """Forward: logits_a = x . w^T + b; out = [x | lse_a, logit_a[target]].
+    On the GPU: the tile GEMM, then ONE kernel packing x and the statistics
+    (``vsplit_head_fwd``).  Backward: one softmax-gradient kernel reading lse and
+    dL/dloss_row straight from the message slots, the dgrad GEMM adding the
+    incoming dx in its epilogue (residual read from the message in place)."""
+
     @staticmethod
     def forward(ctx, x, w, b, target):  # type: ignore[override]
-        k = kernels_for(x) if x.is_cuda else None
         e = x.shape[-1]
-        x2 = x.reshape(-1, e).contiguous()
-        logits, tile = _tile_linear(k, x2, w, b)
-        t = target.reshape(-1).to(x2.device)
+        x2 = x.reshape(-1, e)
+        k = kernels_for(x2) if x2.is_cuda else None
+        t = _targets(target, x2.device)
         va = w.shape[0]
-        ta = torch.where((t >= 0) & (t < va), t, torch.full_like(t, -1)).contiguous()
-        lse, tlog = _lse_and_target(k, logits, ta)
-        out = torch.cat((x2, _stats_to_slots(lse, tlog, x2.dtype)), dim=-1)
-        ctx.save_for_backward(x2, w, b, logits, ta)
+        ctx.native = _native(k, x2)
+        if ctx.native:
+            x2 = gemm_operand(x2)
+            logits, tile = _tile_linear(k, x2, w, b)
+            out = torch.empty(x2.shape[0], e + STAT_SLOTS, dtype=x2.dtype, device=x2.device)
+            k.vsplit_head_fwd(logits, t, x2, out)
+        else:
+            logits, tile = _tile_linear(k, x2, w, b)
+            lf = logits.float()
+            lse = torch.logsumexp(lf, dim=-1)
+            ta = torch.where((t >= 0) & (t < va), t, torch.zeros_like(t))
+            tlog = torch.where((t >= 0) & (t < va), lf.gather(1, ta[:, None])[:, 0], torch.zeros_like(lse))
+            out = torch.cat((x2, _stats_to_slots(lse, tlog, x2.dtype)), dim=-1)
+        ctx.save_for_backward(x2, w, b, logits, t)
         ctx.tile, ctx.shape = tile, x.shape
         return out.view(*x.shape[:-1], e + STAT_SLOTS)
 
     @staticmethod
     def backward(ctx, dout):  # type: ignore[override]
-        x2, w, b, logits, ta = ctx.saved_tensors
+        x2, w, b, logits, t = ctx.saved_tensors
         k = kernels_for(x2) if x2.is_cuda else None
         e = x2.shape[1]
         d2 = dout.reshape(-1, e + STAT_SLOTS)
-        lse, g_row = _slots_to_stats(d2[:, e:])
         dlog = torch.empty_like(logits)
-        _softmax_grad(k, logits, ta, lse, g_row, dlog)
-        dx = d2[:, :e] + _dgrad(k, ctx.tile, dlog, w)
+        dx = torch.empty(x2.shape, dtype=x2.dtype, device=x2.device)
+        if ctx.native:
+            d2 = gemm_operand(d2)
+            words = _slot_words(d2, e)
+            k.cross_entropy_bwd(logits, t, words[:, 0], None, -1, row_scale=words[:, 1], out=dlog)
+        else:
+            words = _slot_words(d2.contiguous(), e)
+            _softmax_grad(logits, t, words[:, 0], words[:, 1], dlog)
+        _dgrad_into(k, ctx.tile, dlog, w, d2[:, :e], dx)
         dw = accumulate_wgrad(dlog, x2, w)
         db = _bias_grad(k, dlog, b)
         return dx.view(ctx.shape), dw, db, None
 
 
 class _TailFn(torch.autograd.Function):
+    """Forward: logits_b over the padded tail rows, then ``vsplit_tail_fwd``:
+    merged lse, row losses, the mean (a fixed-order one-block reduction) and the
+    per-row weights valid / count.  Backward: one softmax-gradient kernel
+    (scale = dL x weight, zeroed pad columns) that also writes (lse, dL/dloss_row)
+    into the gradient message's slots; the dgrad GEMM writes dx into the same
+    message -- no concatenation."""
+
     @staticmethod
     def forward(ctx, packed, w, b, target, va, vb, ignore_index):  # type: ignore[override]
-        k = kernels_for(packed) if packed.is_cuda else None
         e = packed.shape[-1] - STAT_SLOTS
         p2 = packed.reshape(-1, e + STAT_SLOTS)
-        x2 = p2[:, :e].contiguous()
-        lse_a, t_a = _slots_to_stats(p2[:, e:])
-        logits, tile = _tile_linear(k, x2, w, b)
-        lv = logits[:, :vb]
-        t = target.reshape(-1).to(x2.device)
-        in_b = (t >= va) & (t < va + vb)
-        tb = torch.where(in_b, t - va, torch.full_like(t, -1)).contiguous()
-        lse_b, t_b = _lse_and_target(k, lv, tb)
-        lse = torch.logaddexp(lse_a, lse_b)
-        tl = torch.where(in_b, t_b, t_a)
-        valid = (t != ignore_index) & (t >= 0) & (t < va + vb)
-        count = valid.sum().clamp_min(1).to(torch.float32)
-        loss = ((lse - tl) * valid).sum() / count
-        ctx.save_for_backward(x2, w, b, logits, tb, lse, valid, count)
-        ctx.tile, ctx.vb, ctx.shape = tile, vb, packed.shape
+        k = kernels_for(p2) if p2.is_cuda else None
+        t = _targets(target, p2.device)
+        ctx.native = _native(k, p2[:, :e])
+        if ctx.native:
+            p2 = gemm_operand(p2)
+            x2 = p2[:, :e]
+            logits, tile = _tile_linear(k, x2, w, b)
+            loss, lse, weight = k.vsplit_tail_fwd(logits[:, :vb], t, va, ignore_index, _slot_words(p2, e))
+        else:
+            x2 = p2[:, :e].contiguous()
+            words = _slot_words(p2.contiguous(), e)
+            lse_a, t_a = words[:, 0], words[:, 1]
+            logits, tile = _tile_linear(k, x2, w, b)
+            lf = logits[:, :vb].float()
+            lse = torch.logaddexp(lse_a, torch.logsumexp(lf, dim=-1))
+            in_b = (t >= va) & (t < va + vb)
+            tb = torch.where(in_b, t - va, torch.zeros_like(t))
+            tl = torch.where(in_b, lf.gather(1, tb[:, None])[:, 0], t_a)
+            valid = ((t != ignore_index) & (t >= 0) & (t < va + vb)).to(torch.float32)
+            count = valid.sum().clamp_min(1.0)
+            loss = ((lse - tl) * valid).sum() / count
+            weight = valid / count
+        ctx.save_for_backward(x2, w, b, logits, t, lse, weight)
+        ctx.tile, ctx.va, ctx.vb, ctx.ignore, ctx.shape = tile, va, vb, ignore_index, packed.shape
         return loss
 
     @staticmethod
     def backward(ctx, g):  # type: ignore[override]
-        x2, w, b, logits, tb, lse, valid, count = ctx.saved_tensors
+        x2, w, b, logits, t, lse, weight = ctx.saved_tensors
         k = kernels_for(x2) if x2.is_cuda else None
-        g_row = (valid.to(torch.float32) * (g.to(torch.float32) / count)).contiguous()
-        dlog = torch.zeros_like(logits)  # padded vocabulary columns stay zero
-        _softmax_grad(k, logits[:, : ctx.vb], tb, lse, g_row, dlog)
-        dx = _dgrad(k, ctx.tile, dlog, w)
+        e, vb = x2.shape[1], ctx.vb
+        dpacked = torch.empty(x2.shape[0], e + STAT_SLOTS, dtype=x2.dtype, device=x2.device)
+        dlog = torch.empty_like(logits)
+        if ctx.native:
+            gs = g.to(torch.float32).reshape(1)
+            k.cross_entropy_bwd(logits[:, :vb], t, lse, gs, ctx.ignore, row_scale=weight, out=dlog, zero_pad=True,
+                                t_offset=ctx.va, stat_out=dpacked[:, e:])
+        else:
+            g_row = weight * g.to(torch.float32)
+            dlog[:, vb:] = 0  # padded vocabulary rows of the weight get no gradient
+            _softmax_grad(logits[:, :vb], t - ctx.va, lse, g_row, dlog)
+            dpacked[:, e:] = _stats_to_slots(lse, g_row, x2.dtype)
+        _dgrad_into(k, ctx.tile, dlog, w, None, dpacked[:, :e])
         dw = accumulate_wgrad(dlog, x2, w)
         db = _bias_grad(k, dlog, b)
-        dpacked = torch.cat((dx.to(x2.dtype), _stats_to_slots(lse, g_row, x2.dtype)), dim=-1)
         return dpacked.view(ctx.shape), dw, db, None, None, None, None
 
 

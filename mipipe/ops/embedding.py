@@ -3,6 +3,12 @@
 The backward accumulates straight into ``weight.main_grad`` (fp32) when the
 parameter has one (flat-buffer optimizer, :mod:`mipipe.optim`) and returns no
 dense gradient; otherwise it builds a dense fp32 gradient and casts it.
+
+A positional table that requires a gradient (GPT-2's learned positions, fp32)
+rides through the same kernels: the forward adds it in the gather, the
+backward's scatter-add also accumulates each masked row at its position (into
+the table's ``main_grad`` when it has one) -- no separate add, dropout or
+batch reduction.
 """
 from __future__ import annotations
 
@@ -23,23 +29,26 @@ class _Embed(torch.autograd.Function):
     def forward(ctx, tokens, weight, pe, scale, p):  # type: ignore[override]
         k = kernels_for(weight)
         out, seed, offset = k.embedding_fwd(tokens.contiguous(), weight, pe, scale, p)
-        ctx.save_for_backward(tokens)
-        ctx.weight = weight
+        ctx.save_for_backward(tokens.contiguous())
+        ctx.weight, ctx.pe = weight, (pe if ctx.needs_input_grad[2] else None)
         ctx.scale, ctx.p, ctx.seed, ctx.offset = scale, p, seed, offset
         return out
 
     @staticmethod
     def backward(ctx, dout):  # type: ignore[override]
         (tokens,) = ctx.saved_tensors
-        weight = ctx.weight
+        weight, pe = ctx.weight, ctx.pe
         k = kernels_for(dout)
         main = accumulable(weight)
-        if main is not None:
-            k.embedding_bwd(tokens, dout.contiguous(), main, ctx.scale, ctx.p, ctx.seed, ctx.offset)
-            return None, None, None, None, None
-        acc = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
-        k.embedding_bwd(tokens, dout.contiguous(), acc, ctx.scale, ctx.p, ctx.seed, ctx.offset)
-        return None, acc.to(weight.dtype), None, None, None
+        acc = main if main is not None else torch.zeros(weight.shape, dtype=torch.float32, device=weight.device)
+        dpe = dpe_main = None
+        if pe is not None:
+            dpe_main = accumulable(pe)
+            dpe = dpe_main if dpe_main is not None else torch.zeros(pe.shape, dtype=torch.float32, device=pe.device)
+        k.embedding_bwd(tokens, dout.contiguous(), acc, ctx.scale, ctx.p, ctx.seed, ctx.offset, dpe)
+        dw = None if main is not None else acc.to(weight.dtype)
+        dp = None if (pe is None or dpe_main is not None) else dpe.to(pe.dtype)
+        return None, dw, dp, None, None
 
 
 def embed_scale_posenc_dropout(

@@ -80,6 +80,17 @@ def _aligned(t: Tensor) -> bool:
     return t.data_ptr() % 16 == 0
 
 
+def gemm_operand(t: Tensor) -> Tensor:
+    """``t`` itself when the tile GEMMs can read it in place -- 2-D, unit column
+    stride, 16-byte aligned rows (a column slice of a packed message is fine) --
+    else an aligned contiguous copy."""
+    if (t.dim() == 2 and t.stride(1) == 1 and (t.stride(0) * t.element_size()) % 16 == 0
+            and t.stride(0) >= t.shape[1] and _aligned(t)):
+        return t
+    t = t.contiguous()
+    return t if _aligned(t) else t.clone()
+
+
 def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
     """All three GEMMs of the layer (fwd [T,N,K], dgrad [T,K,N], wgrad [N,K,T]) fit the tile kernel."""
     t, (n, kk) = x2.shape[0], weight.shape
@@ -94,9 +105,36 @@ def _tile_ok(k, x2: Tensor, weight: Tensor) -> bool:
     )
 
 
+class ActFold:
+    """Hand-off between an activation layer ``h = drop(act(x W1^T + b1))`` and
+    the ONE layer consuming ``h`` (an MLP's two halves): the consumer's dgrad
+    GEMM applies the activation's backward (act' of the saved tensor and the
+    dropout mask) in its epilogue, so the producer's backward receives the
+    gradient of its pre-activation and skips its own elementwise pass -- one
+    write and one read of the [tokens, d_ff] gradient fewer, and no separate
+    kernel.  Only valid when ``h`` has no other consumer: the caller (e.g.
+    :class:`~mipipe.models.transformer.FeedForwardBlock`) guarantees that; the
+    producer checks it receives exactly the tensor the consumer produced.
+    """
+
+    __slots__ = ("act", "saved", "p", "seed", "offset", "done_ptr")
+
+    def __init__(self) -> None:
+        self.act, self.saved, self.p, self.seed, self.offset = 0, None, 0.0, 0, 0
+        self.done_ptr: Optional[int] = None
+
+    def offer(self, act: int, saved: Tensor, p: float, seed: int, offset: int) -> None:
+        self.act, self.saved, self.p, self.seed, self.offset = act, saved, p, seed, offset
+
+    def ready_for(self, x2: Tensor) -> bool:
+        s = self.saved
+        return s is not None and s.shape == x2.shape and s.dtype == x2.dtype == torch.bfloat16
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, act, p, fanout=False, res=None):  # type: ignore[override]
+    def forward(ctx, x, weight, bias, act, p, fanout=False, res=None, fold_out=None,
+                fold_in=None):  # type: ignore[override]
         ctx.set_materialize_grads(False)
         k = kernels_for(x)
         shape = x.shape
@@ -127,6 +165,13 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x2, w, bias, saved)
         ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
         ctx.fused_tile = fused_tile
+        # activation backward folded into the consumer's dgrad (ActFold)
+        ctx.fold_out = ctx.fold_in = None
+        if fold_out is not None and fused_tile and act != 0 and x2.dtype == torch.bfloat16 and saved is not None:
+            fold_out.offer(act, saved, p, seed, offset)
+            ctx.fold_out = fold_out
+        if fold_in is not None and fused_tile and fold_in.ready_for(x2) and torch.is_grad_enabled():
+            ctx.fold_in = fold_in
         ctx.in_shape = shape
         y = y.view(*shape[:-1], w.shape[0])
         if res is not None:
@@ -152,6 +197,15 @@ class _Linear(torch.autograd.Function):
         # inside deferred_wgrad(): the bias gradient joins the step's batch too
         defer_b = main_b is not None and _DEFERRED is not None and d2.shape[-1] % 8 == 0
         act, p = ctx.act, ctx.p
+        fold = ctx.fold_out
+        folded = fold is not None and fold.done_ptr is not None
+        if folded:
+            if fold.done_ptr != d2.data_ptr():
+                raise RuntimeError("mipipe: an activation's backward was folded into its consumer's dgrad, but the "
+                                   "gradient reaching the activation is a different tensor (the activation output "
+                                   "has another consumer): do not pass one ActFold to such a graph")
+            fold.done_ptr = None
+            act, p = 0, 0.0  # d2 is already the pre-activation gradient
         if act != 0 or p > 0.0:
             # GEMM-saved GELU pre-activation already includes the bias.
             bias_for_bwd = None if ctx.fused_tile else bias
@@ -176,7 +230,11 @@ class _Linear(torch.autograd.Function):
                 r2 = dres.reshape(-1, dres.shape[-1])
                 if not (ctx.fused_tile and r2.dtype == dpre.dtype and r2.is_contiguous() and _aligned(r2)):
                     r2 = None
-            if ctx.fused_tile:
+            fin = ctx.fold_in
+            if ctx.fused_tile and fin is not None and r2 is None and dres is None:
+                dx = k.linear_dgrad(dpre, w, None, None, fin.act, fin.saved, fin.p, fin.seed, fin.offset)
+                fin.done_ptr = dx.data_ptr()
+            elif ctx.fused_tile:
                 dx = k.linear_dgrad(dpre, w, r2)
             else:
                 dx = torch.matmul(dpre, w)
@@ -195,7 +253,7 @@ class _Linear(torch.autograd.Function):
                 _add_or_copy(main, torch.matmul(dpre.t(), x2), w)
             else:
                 dw = torch.matmul(dpre.t(), x2)
-        return dx, dw, db, None, None, None, dres_in
+        return dx, dw, db, None, None, None, dres_in, None, None
 
 
 # ---------------------------------------------------------------- deferred wgrad
@@ -231,9 +289,7 @@ def accumulate_wgrad(dy: Tensor, x: Tensor, w: Tensor) -> Optional[Tensor]:
     k = kernels_for(dy) if dy.is_cuda else None
     tile = (k is not None and dy.dtype == x.dtype and _gemm_supported(k, dy.dtype, w.shape[0], w.shape[1], dy.shape[0]))
     if main is not None and tile:
-        dy, x = dy.contiguous(), x.contiguous()
-        dy = dy if _aligned(dy) else dy.clone()
-        x = x if _aligned(x) else x.clone()
+        dy, x = gemm_operand(dy), gemm_operand(x)
         if _DEFERRED is not None:
             _defer(w, dy, x)
         else:
@@ -280,7 +336,8 @@ def flush_wgrad() -> None:
                 k.column_sum_segments(dys, w.main_grad, True)
             else:
                 T = dys[0].shape[0]
-                uniform = all(d.shape == dys[0].shape for d in dys) and all(x.shape == xs[0].shape for x in xs)
+                uniform = (all(d.shape == dys[0].shape and d.stride() == dys[0].stride() for d in dys)
+                           and all(x.shape == xs[0].shape and x.stride() == xs[0].stride() for x in xs))
                 if uniform and T % 64 == 0:
                     k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
                 else:
@@ -355,13 +412,17 @@ def linear(
     activation: Optional[str] = None,
     dropout_p: float = 0.0,
     training: bool = True,
+    *,
+    act_fold_out: Optional[ActFold] = None,
+    act_fold_in: Optional[ActFold] = None,
 ) -> Tensor:
-    """``dropout(act(x @ weight.T + bias))``."""
+    """``dropout(act(x @ weight.T + bias))``.  ``act_fold_out`` / ``act_fold_in``:
+    see :class:`ActFold` (this layer's activation / its input's activation)."""
     p = float(dropout_p) if training else 0.0
     if not x.is_cuda:
         y = F.linear(x, weight)
         return bias_act_reference(y, bias, activation, p, True)
-    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p)
+    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p, False, None, act_fold_out, act_fold_in)
 
 
 def linear_residual(
@@ -371,6 +432,8 @@ def linear_residual(
     res: Tensor,
     dropout_p: float = 0.0,
     training: bool = True,
+    *,
+    act_fold_in: Optional[ActFold] = None,
 ) -> Tensor:
     """``res + dropout(x @ weight.T + bias)`` -- a pre-norm residual branch's
     output projection with the residual add folded into the GEMM epilogue (no
@@ -378,7 +441,7 @@ def linear_residual(
     p = float(dropout_p) if training else 0.0
     if not x.is_cuda:
         return res + linear(x, weight, bias, None, p, True)
-    return _Linear.apply(x, weight, bias, 0, p, False, res)
+    return _Linear.apply(x, weight, bias, 0, p, False, res, None, act_fold_in)
 
 
 def linear_fanout(
@@ -388,6 +451,8 @@ def linear_fanout(
     activation: Optional[str] = None,
     dropout_p: float = 0.0,
     training: bool = True,
+    *,
+    act_fold_out: Optional[ActFold] = None,
 ):
     """``(linear(x, ...), x')`` where ``x'`` is ``x`` for the input's OTHER
     consumer (a post-norm residual branch).  Mathematically the identity; the
@@ -395,6 +460,6 @@ def linear_fanout(
     the dgrad GEMM's epilogue instead of by a separate autograd add kernel
     (one full read/write pass of the activation per fan-out)."""
     if not x.is_cuda or not torch.is_grad_enabled() or not x.requires_grad:
-        return linear(x, weight, bias, activation, dropout_p, training), x
+        return linear(x, weight, bias, activation, dropout_p, training, act_fold_out=act_fold_out), x
     p = float(dropout_p) if training else 0.0
-    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p, True)
+    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p, True, None, act_fold_out)

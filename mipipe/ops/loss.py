@@ -45,7 +45,8 @@ class _CrossEntropy(torch.autograd.Function):
         _ZERO_PADDED.clear()  # marks live from a CE backward to the slice backward of the same pass
         k = kernels_for(logits)
         lc = logits if (logits.dim() == 2 and logits.stride(1) == 1) else logits.contiguous()
-        loss_rows, lse = k.cross_entropy_fwd(lc, target.contiguous(), ignore_index)
+        target = target.contiguous()
+        loss_rows, lse = k.cross_entropy_fwd(lc, target, ignore_index)
         count = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
         ctx.save_for_backward(lc, target, lse, count)
         ctx.ignore_index = ignore_index

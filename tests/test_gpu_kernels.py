@@ -8,6 +8,9 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from mipipe import ops
+from mipipe.ops.linear import ActFold
+
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
@@ -623,6 +626,98 @@ def test_deferred_wgrad_op(k):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("act,p,T", [(2, 0.0, 512), (2, 0.1, 512), (1, 0.2, 512), (2, 0.1, 8192), (1, 0.0, 384)])
+def test_linear_dgrad_activation_backward_epilogue(k, act, p, T):
+    """dgrad with the activation backward in the epilogue == (dy W) * mask * act'(saved):
+    the mask regenerated from the forward GEMM's Philox layout (big and 128x128 kernels)."""
+    torch.manual_seed(30)
+    E, F = 256, 1024
+    x = torch.randn(T, E, device=DEV).to(torch.bfloat16)
+    w1 = (torch.randn(F, E, device=DEV) * 0.05).to(torch.bfloat16)
+    b1 = (torch.randn(F, device=DEV) * 0.1).to(torch.bfloat16)
+    w2 = (torch.randn(E, F, device=DEV) * 0.05).to(torch.bfloat16)
+    y, pre, seed, offset = k.linear_fwd(x, w1, b1, act, p, act == 2)
+    saved = pre if act == 2 else y
+    dy = torch.randn(T, E, device=DEV).to(torch.bfloat16)
+    got = k.linear_dgrad(dy, w2, None, None, act, saved, p, seed, offset)
+    dh = dy.float() @ w2.float()
+    keep = (y != 0).float()  # GELU output is 0 only where dropped
+    scale = 1.0 / (1.0 - p) if p > 0 else 1.0
+    if act == 2:
+        s = pre.float()
+        grad = 0.5 * (1 + torch.erf(s / math.sqrt(2))) + s * torch.exp(-0.5 * s * s) / math.sqrt(2 * math.pi)
+        ref = dh * keep * scale * grad
+    else:
+        ref = dh * keep * scale
+    err = ((got.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("activation,norm_first", [("relu", False), ("gelu", True), ("gelu", False)])
+def test_feedforward_act_fold_matches_unfolded(k, activation, norm_first):
+    """FeedForwardBlock with the activation backward folded into fc_out's dgrad
+    == the same block without the fold (same dropout masks: reseeded)."""
+    from mipipe.models.transformer import FeedForwardBlock
+
+    torch.manual_seed(31)
+    blk = FeedForwardBlock(256, 1024, 0.1, activation, norm_first=norm_first, device=DEV, dtype=torch.bfloat16)
+    x0 = torch.randn(4, 128, 256, device=DEV).to(torch.bfloat16)
+    grads = []
+    for fold in (True, False):
+        for prm in blk.parameters():
+            prm.grad = None
+        x = x0.clone().requires_grad_()
+        torch.cuda.manual_seed(5)
+        f = ActFold() if fold else None
+        h, xr = blk.fc_in.forward_fanout(x, True, f)
+        out = blk.fc_out(xr, h, f)
+        out.float().square().sum().backward()
+        grads.append([x.grad.float().clone()] + [prm.grad.float().clone() for prm in blk.parameters()])
+    for a, b in zip(*grads):
+        assert ((a - b).abs().max() / (b.abs().max() + 1e-12)).item() < 2e-2
+
+
+def test_act_fold_rejects_second_consumer(k):
+    """The fold is only valid when h has one consumer: a second use is caught."""
+    torch.manual_seed(32)
+    x = torch.randn(256, 128, device=DEV).to(torch.bfloat16).requires_grad_()
+    w1 = (torch.randn(512, 128, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_()
+    w2 = (torch.randn(128, 512, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_()
+    f = ActFold()
+    h = ops.linear(x, w1, None, "gelu", 0.0, True, act_fold_out=f)
+    y = ops.linear(h, w2, None, act_fold_in=f)
+    with pytest.raises(RuntimeError, match="another consumer"):
+        (y.float().sum() + h.float().sum()).backward()
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_learned_positions_fused_embedding(k, p):
+    """GPT-2 learned positions through the fused embedding kernels: forward adds
+    the table, backward accumulates its gradient by position (dropout mask
+    shared with the token-table gradient)."""
+    from mipipe.models.lm import Encoder
+
+    torch.manual_seed(33)
+    enc = Encoder(1000, 256, p, max_len=128, learned_positions=True, scale_embedding=False, device=DEV,
+                  dtype=torch.bfloat16)
+    tok = torch.randint(0, 1000, (4, 64), device=DEV)
+    y = enc(tok)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    keep = (y != 0).float() if p > 0 else torch.ones_like(y, dtype=torch.float32)
+    scale = 1.0 / (1.0 - p) if p > 0 else 1.0
+    g = dy.float() * keep * scale  # [B, S, E]
+    ref_pos = torch.zeros(128, 256, device=DEV)
+    ref_pos[:64] = g.sum(0)
+    ref_tok = torch.zeros(1000, 256, device=DEV).index_add_(0, tok.reshape(-1), g.reshape(-1, 256))
+    assert enc.pos_weight.grad is not None
+    assert ((enc.pos_weight.grad.float() - ref_pos).abs().max() / ref_pos.abs().max()).item() < 1e-2
+    assert ((enc.weight.grad.float() - ref_tok).abs().max() / ref_tok.abs().max()).item() < 2e-2
+    # forward: table rows + position rows (where kept)
+    ref_y = (enc.weight.float()[tok] + enc.pos_weight.float()[:64]) * scale * keep
+    assert ((y.float() - ref_y).abs().max() / ref_y.abs().max()).item() < 1e-2
+
+
 def test_linear_dropout_mask_and_main_grad(k):
     from mipipe.ops import linear
 
@@ -955,6 +1050,102 @@ def test_vocab_split_decoder_gpu(k):
     assert rel(head.weight.grad, dec.weight.grad[:512]) < 2e-2
     assert rel(tail.weight.grad[:488], dec.weight.grad[512:1000]) < 2e-2
     assert rel(tail.bias.grad[:488], dec.bias.grad[512:1000]) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_vocab_split_ignore_index_and_dtypes(k, dtype):
+    """Ignored targets (and targets in both halves) through the fused pack /
+    merge / mean kernels, bf16 and fp32, against the fp32 PyTorch loss."""
+    from mipipe.models import Decoder, split_decoder
+
+    torch.manual_seed(18)
+    dec = Decoder(1000, 256, device=DEV, dtype=dtype)
+    head, tail = split_decoder(dec)
+    x = torch.randn(2, 64, 256, device=DEV).to(dtype).requires_grad_()
+    t = torch.randint(0, 1000, (2, 64), device=DEV)
+    t[0, :7] = -100
+    xr = x.detach().float().requires_grad_()
+    wr = dec.weight.detach().float().requires_grad_()
+    logits = (xr @ wr.t() + dec.bias.float()).reshape(-1, 1000)
+    ref = torch.nn.functional.cross_entropy(logits, t.reshape(-1), ignore_index=-100)
+    ref.backward()
+    loss = tail(head(x, t), t)
+    loss.backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert abs(loss.item() - ref.item()) < tol * abs(ref.item())
+
+    def rel(a, b):
+        return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+    assert rel(x.grad, xr.grad) < 3 * tol
+    assert rel(head.weight.grad, wr.grad[:512]) < 3 * tol
+    assert rel(tail.weight.grad[:488], wr.grad[512:1000]) < 3 * tol
+    assert tail.weight.grad[488:].abs().max().item() == 0.0  # padded vocabulary rows
+    # the fixed-order mean: bitwise reproducible
+    again = tail(head(x.detach(), t), t)
+    assert again.item() == loss.item()
+
+
+def test_vocab_split_launches_no_aten_kernels(k):
+    """Head + tail forward and backward run only mipipe kernels (plus copies of
+    nothing): no elementwise / reduction / cat kernels from ATen."""
+    from mipipe.models import Decoder, split_decoder
+
+    torch.manual_seed(19)
+    dec = Decoder(1000, 256, device=DEV, dtype=torch.bfloat16)
+    head, tail = split_decoder(dec)
+    x = torch.randn(2, 64, 256, device=DEV).to(torch.bfloat16).requires_grad_()
+    t = torch.randint(0, 1000, (2, 64), device=DEV)
+    tail(head(x, t), t).backward()  # warm (allocations, lazy init)
+    torch.cuda.synchronize()
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with torch.profiler.profile(activities=acts) as prof:
+        tail(head(x, t), t).backward()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    if not names:
+        pytest.skip("the profiler recorded no device kernels on this build")
+    aten = [n for n in names if "at::native" in n or "elementwise" in n.lower() or "reduce_kernel" in n]
+    assert not aten, aten
+
+
+def test_strided_gemm_operands(k):
+    """linear_fwd / linear_dgrad / linear_wgrad on column slices of packed rows
+    (row stride != width) and dgrad into a strided destination with a strided addend."""
+    torch.manual_seed(20)
+    M, E, N, S = 512, 256, 768, 8
+    packed = torch.randn(M, E + S, device=DEV).to(torch.bfloat16)
+    x = packed[:, :E]
+    w = torch.randn(N, E, device=DEV).to(torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    y = k.linear_fwd(x, w, b, 0, 0.0, False)[0]
+    ref = x.float() @ w.float().t() + b.float()
+    assert ((y.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    dmsg = torch.randn(M, E + S, device=DEV).to(torch.bfloat16)
+    out = torch.zeros(M, E + S, device=DEV, dtype=torch.bfloat16)
+    k.linear_dgrad(dy, w, dmsg[:, :E], out[:, :E])
+    ref = dy.float() @ w.float() + dmsg[:, :E].float()
+    assert ((out[:, :E].float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    assert out[:, E:].abs().max().item() == 0.0  # the slots are untouched
+    g = torch.zeros(N, E, device=DEV)
+    k.linear_wgrad(dy, x, g, False)
+    ref = dy.float().t() @ x.float()
+    assert ((g - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+def test_cross_entropy_target_offset(k):
+    """t_offset: the logits are a vocabulary slice; targets outside it get loss 0."""
+    torch.manual_seed(21)
+    logits = torch.randn(64, 300, device=DEV)
+    t = torch.randint(0, 900, (64,), device=DEV)
+    loss, lse = k.cross_entropy_fwd(logits, t, -100, t_offset=300)
+    inside = (t >= 300) & (t < 600)
+    expect_lse = torch.logsumexp(logits, -1)
+    expect = torch.where(inside, expect_lse - logits.gather(1, (t - 300).clamp(0, 299)[:, None])[:, 0],
+                         torch.zeros_like(expect_lse))
+    assert torch.allclose(lse, expect_lse, atol=1e-5)
+    assert torch.allclose(loss, expect, atol=1e-5)
 
 
 @pytest.mark.parametrize("cols", [264, 4096])
