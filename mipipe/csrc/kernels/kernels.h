@@ -237,8 +237,8 @@ struct AdamHyper {
 };
 int sumsq_parts(int64_t n);
 void sumsq(const float* g, int64_t n, float* partial, int nparts, float* out, hipStream_t s);
-// 0: grid-stride kernel, 2 vectors of loads in flight per thread (default);
-// 1: one-shot tiles of 4 vectors per thread (A/B).
+// 0: grid-stride kernel, 2 vectors of loads in flight per thread;
+// 1: one-shot tiles of 4 vectors per thread (default, ~10 % faster).
 void adam_set_variant(int v);
 template <typename M>
 void adam_step(float* master, M* model, const float* grad, float* m, float* v, int64_t n, const AdamHyper& h,

@@ -69,6 +69,8 @@ def _bias_grad(k, d: Tensor, b: Tensor) -> Optional[Tensor]:
         else:
             main.add_(d.float().sum(0))
         return None
+    if k is not None:
+        return k.column_sum(d).to(b.dtype)
     return d.sum(0).to(b.dtype)
 
 

@@ -117,11 +117,30 @@ class ActFold:
     producer checks it receives exactly the tensor the consumer produced.
     """
 
-    __slots__ = ("act", "saved", "p", "seed", "offset", "done_ptr")
+    __slots__ = ("act", "saved", "p", "seed", "offset", "grad", "version")
 
     def __init__(self) -> None:
         self.act, self.saved, self.p, self.seed, self.offset = 0, None, 0.0, 0, 0
-        self.done_ptr: Optional[int] = None
+        # the folded gradient the consumer produced, and its version: the
+        # producer accepts only this tensor, unmodified (autograd accumulates a
+        # second consumer's gradient in place or into a new tensor)
+        self.grad: Optional[Tensor] = None
+        self.version = 0
+
+    def done(self, grad: Tensor) -> None:
+        self.grad, self.version = grad, grad._version
+
+    def take(self, d2: Tensor) -> bool:
+        """True if ``d2`` is the folded gradient (then consumed); raises if a
+        fold happened but the gradient reaching the producer is another tensor."""
+        g, self.grad = self.grad, None
+        if g is None:
+            return False
+        if d2.data_ptr() != g.data_ptr() or g._version != self.version:
+            raise RuntimeError("mipipe: an activation's backward was folded into its consumer's dgrad, but the "
+                               "gradient reaching the activation is a different tensor (the activation output "
+                               "has another consumer): do not pass one ActFold to such a graph")
+        return True
 
     def offer(self, act: int, saved: Tensor, p: float, seed: int, offset: int) -> None:
         self.act, self.saved, self.p, self.seed, self.offset = act, saved, p, seed, offset
@@ -170,7 +189,7 @@ class _Linear(torch.autograd.Function):
         if fold_out is not None and fused_tile and act != 0 and x2.dtype == torch.bfloat16 and saved is not None:
             fold_out.offer(act, saved, p, seed, offset)
             ctx.fold_out = fold_out
-        if fold_in is not None and fused_tile and fold_in.ready_for(x2) and torch.is_grad_enabled():
+        if fold_in is not None and fused_tile and fold_in.ready_for(x2) and ctx.needs_input_grad[0]:
             ctx.fold_in = fold_in
         ctx.in_shape = shape
         y = y.view(*shape[:-1], w.shape[0])
@@ -197,14 +216,7 @@ class _Linear(torch.autograd.Function):
         # inside deferred_wgrad(): the bias gradient joins the step's batch too
         defer_b = main_b is not None and _DEFERRED is not None and d2.shape[-1] % 8 == 0
         act, p = ctx.act, ctx.p
-        fold = ctx.fold_out
-        folded = fold is not None and fold.done_ptr is not None
-        if folded:
-            if fold.done_ptr != d2.data_ptr():
-                raise RuntimeError("mipipe: an activation's backward was folded into its consumer's dgrad, but the "
-                                   "gradient reaching the activation is a different tensor (the activation output "
-                                   "has another consumer): do not pass one ActFold to such a graph")
-            fold.done_ptr = None
+        if ctx.fold_out is not None and ctx.fold_out.take(d2):
             act, p = 0, 0.0  # d2 is already the pre-activation gradient
         if act != 0 or p > 0.0:
             # GEMM-saved GELU pre-activation already includes the bias.
@@ -233,7 +245,7 @@ class _Linear(torch.autograd.Function):
             fin = ctx.fold_in
             if ctx.fused_tile and fin is not None and r2 is None and dres is None:
                 dx = k.linear_dgrad(dpre, w, None, None, fin.act, fin.saved, fin.p, fin.seed, fin.offset)
-                fin.done_ptr = dx.data_ptr()
+                fin.done(dx)
             elif ctx.fused_tile:
                 dx = k.linear_dgrad(dpre, w, r2)
             else:
