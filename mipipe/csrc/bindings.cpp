@@ -812,7 +812,7 @@ void fill_qkv(AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
   a.B = (int)q.size(0); a.S = (int)q.size(1); a.H = (int)q.size(2); a.D = (int)q.size(3);
   a.sb_qkv = q.stride(0); a.ld_qkv = q.stride(1); a.sh_qkv = q.stride(2);
   MP_CHECK(attn_ok(q.scalar_type(), a.S, a.D), "attention: unsupported S=", a.S, " D=", a.D, " for ",
-           q.scalar_type(), " (bf16: S % 64 == 0, D in {64,128,256}; fp32: S % 32 == 0, D == 64)");
+           q.scalar_type(), " (bf16: S % 64 == 0, D in {64,128,256}; fp32: S % 32 == 0, D in {64,128})");
 }
 
 // bf16 D = 64, S >= 256 run the long-sequence kernels (attention_long.hip);

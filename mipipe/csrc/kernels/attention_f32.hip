@@ -34,7 +34,7 @@
 // weight (score -inf in the forward, P = 0 in the backward) and the key loops
 // stop at the last block holding a valid key.
 //
-// Supported: fp32, S % 32 == 0, D = 64, causal or not.
+// Supported: fp32, S % 32 == 0, D = 64 or 128, causal or not.
 #include "common.h"
 #include "kernels.h"
 
@@ -133,6 +133,9 @@ __device__ __forceinline__ void colsT_times_acc(const char* blk, int li, int h, 
       const float a = *reinterpret_cast<const float*>(blk + boff<D>(arow(s, h), d >> 2) + (d & 3) * 4);
       out[t] = mfma(a, p[s], out[t]);
     }
+    // D = 128: keep the scheduler from hoisting all D/32 x 16 LDS loads ahead
+    // of the MFMAs (64 live values pushed the dK/dV kernel into scratch)
+    if constexpr (D > 64) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -340,8 +343,13 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dq_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------ dK, dV
-template <int D, bool CAUSAL>
+// PART 0: dK and dV in one kernel (D = 64).  D = 128 runs PART 1 (dV) and
+// PART 2 (dK) as two kernels: resident K and V fragments plus both
+// accumulator sets exceed a lane's 512 registers (the one-kernel form spilled
+// 356 B/lane); the split recomputes S = Q K^T once more instead.
+template <int D, bool CAUSAL, int PART>
 __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) {
+  constexpr bool kDV = PART != 2, kDK = PART != 1;
   __shared__ __attribute__((aligned(16))) char lds[2 * 32 * D * 4 + 2 * 32 * 4];
   char* ldsQ = lds;
   char* ldsO = lds + 32 * D * 4;  // dO block
@@ -358,15 +366,15 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) 
   const float* dOb = reinterpret_cast<const float*>(a.dout) + ooff;
   const float sl = a.scale * kLog2e;
 
-  float kf[D / 2], vf[D / 2];
+  float kf[D / 2], vf[kDK ? D / 2 : 1];
   load_row_frags<D>(reinterpret_cast<const float*>(a.k) + hoff, a.ld_qkv, key, h, sl, kf);
-  load_row_frags<D>(reinterpret_cast<const float*>(a.v) + hoff, a.ld_qkv, key, h, 1.f, vf);
+  if constexpr (kDK) load_row_frags<D>(reinterpret_cast<const float*>(a.v) + hoff, a.ld_qkv, key, h, 1.f, vf);
   const float pscale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
-  f32x16 dk[D / 32], dv[D / 32];
+  f32x16 dk[kDK ? D / 32 : 1], dv[kDV ? D / 32 : 1];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) {
-    dk[t] = zero16();
-    dv[t] = zero16();
+    if constexpr (kDK) dk[t] = zero16();
+    if constexpr (kDV) dv[t] = zero16();
   }
 
   const int kl = a.kv_len > 0 ? a.kv_len : a.S;  // valid keys
@@ -395,7 +403,8 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) 
     gload(min(qb + 1, nqb - 1));
     if (active && !(CAUSAL && 32 * qb + 31 < k0)) {
       f32x16 s = rows_times_frags<D>(ldsQ, li, h, kf, zero16());   // S[q][k] (log2 domain)
-      f32x16 dp = rows_times_frags<D>(ldsO, li, h, vf, zero16());  // dP[q][k]
+      f32x16 dp;                                                   // dP[q][k]
+      if constexpr (kDK) dp = rows_times_frags<D>(ldsO, li, h, vf, zero16());
       f32x16 pd;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -413,19 +422,19 @@ __global__ void __launch_bounds__(kThreads, 1) attn_f32_dkdv_kernel(AttnArgs a) 
           const uint32_t word = j == 0 ? wv.x : (j == 1 ? wv.y : (j == 2 ? wv.z : wv.w));
           keep = word >= a.threshold ? pscale : 0.f;
         }
-        pd[r] = pr * keep;
-        s[r] = pr * (dp[r] * keep - ldsL[32 + qr]);  // dS
+        if constexpr (kDV) pd[r] = pr * keep;
+        if constexpr (kDK) s[r] = pr * (dp[r] * keep - ldsL[32 + qr]);  // dS
       }
-      colsT_times_acc<D>(ldsO, li, h, pd, dv);  // dV^T += dO^T P_drop
-      colsT_times_acc<D>(ldsQ, li, h, s, dk);   // dK^T += Q^T dS
+      if constexpr (kDV) colsT_times_acc<D>(ldsO, li, h, pd, dv);  // dV^T += dO^T P_drop
+      if constexpr (kDK) colsT_times_acc<D>(ldsQ, li, h, s, dk);   // dK^T += Q^T dS
     }
     __syncthreads();
     lstore();
     __syncthreads();
   }
   if (active) {
-    store_T<D>(reinterpret_cast<float*>(a.dk) + hoff, a.ld_qkv, k0 + li, h, dk, a.scale);
-    store_T<D>(reinterpret_cast<float*>(a.dv) + hoff, a.ld_qkv, k0 + li, h, dv, 1.f);
+    if constexpr (kDK) store_T<D>(reinterpret_cast<float*>(a.dk) + hoff, a.ld_qkv, k0 + li, h, dk, a.scale);
+    if constexpr (kDV) store_T<D>(reinterpret_cast<float*>(a.dv) + hoff, a.ld_qkv, k0 + li, h, dv, 1.f);
   }
 }
 
@@ -441,25 +450,37 @@ void run_bwd(const AttnArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_f32_delta_kernel<D>), dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, a);
   const dim3 grid((a.S + 127) / 128, a.B * a.H);
   hipLaunchKernelGGL((attn_f32_dq_kernel<D, CAUSAL>), grid, dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL((attn_f32_dkdv_kernel<D, CAUSAL>), grid, dim3(kThreads), 0, s, a);
+  if constexpr (D > 64) {
+    hipLaunchKernelGGL((attn_f32_dkdv_kernel<D, CAUSAL, 1>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((attn_f32_dkdv_kernel<D, CAUSAL, 2>), grid, dim3(kThreads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((attn_f32_dkdv_kernel<D, CAUSAL, 0>), grid, dim3(kThreads), 0, s, a);
+  }
 }
 
 }  // namespace
 
-// D = 64 only (the reference's head dim, and GPT-2's): at D = 128 the dK/dV
-// kernel's register-resident K/V fragments and accumulators exceed 512 registers.
-bool attention_f32_supported(int S, int D) { return S >= 32 && S % 32 == 0 && D == 64; }
+// D = 64 (the reference's head dim, and GPT-2's) and D = 128 (dV and dK as two kernels).
+bool attention_f32_supported(int S, int D) { return S >= 32 && S % 32 == 0 && (D == 64 || D == 128); }
 
 void attention_f32_fwd(const AttnArgs& ai, hipStream_t s) {
   AttnArgs a = ai;
   a.threshold = dropout_threshold(a.p);
-  if (a.causal) run_fwd<64, true>(a, s); else run_fwd<64, false>(a, s);
+  if (a.D == 128) {
+    if (a.causal) run_fwd<128, true>(a, s); else run_fwd<128, false>(a, s);
+  } else {
+    if (a.causal) run_fwd<64, true>(a, s); else run_fwd<64, false>(a, s);
+  }
 }
 
 void attention_f32_bwd(const AttnArgs& ai, hipStream_t s) {
   AttnArgs a = ai;
   a.threshold = dropout_threshold(a.p);
-  if (a.causal) run_bwd<64, true>(a, s); else run_bwd<64, false>(a, s);
+  if (a.D == 128) {
+    if (a.causal) run_bwd<128, true>(a, s); else run_bwd<128, false>(a, s);
+  } else {
+    if (a.causal) run_bwd<64, true>(a, s); else run_bwd<64, false>(a, s);
+  }
 }
 
 }  // namespace mipipe

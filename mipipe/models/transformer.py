@@ -365,7 +365,10 @@ class FeedForwardBlock(nn.Module):
         # h's only consumer is fc_out: its dgrad applies the activation backward
         fold = ActFold() if FOLD_ACT else None
         h, xr = self.fc_in.forward_fanout(x, FANOUT, fold)
-        return self.fc_out(xr, h, fold)
+        out = self.fc_out(xr, h, fold)
+        if fold is not None:
+            fold.release()
+        return out
 
     def flops_per_token(self, seq_len: int) -> float:
         return 2 * 2 * self.d_model * self.dim_feedforward

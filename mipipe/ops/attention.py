@@ -13,7 +13,7 @@ Causal masking and attention dropout are supported; the dropout mask is
 regenerated from Philox (seed, offset) in backward, so checkpoint recompute
 replays it exactly.  Supported on the GPU path: bf16 with ``S % 64 == 0`` and
 ``D in {64, 128, 256}`` (attention.hip), fp32 with ``S % 32 == 0`` and
-``D == 64`` (attention_f32.hip, the reference's own precision); the
+``D in {64, 128}`` (attention_f32.hip, the reference's own precision); the
 CPU path is eager math.  Any smaller head dim (e.g. 32, 80, 96, 160) runs on
 the kernels zero-padded to the next supported one (the scale stays that of the
 real head dim; the padded columns are sliced off), and a non-causal sequence of
@@ -115,7 +115,7 @@ def _note_math_path(S: int, D: int, dtype) -> None:
         import warnings
 
         warnings.warn(f"mipipe attention: S={S} D={D} {dtype} runs the eager math path (HIP kernels: bf16 with "
-                      "S % 64 == 0, D in {64, 128, 256}; fp32 with S % 32 == 0, D == 64)", stacklevel=3)
+                      "S % 64 == 0, D in {64, 128, 256}; fp32 with S % 32 == 0, D in {64, 128})", stacklevel=3)
 
 
 def _gpu_ok(t: Tensor, S: int, D: int) -> bool:
@@ -153,7 +153,7 @@ def _run_shape(t: Tensor, S: int, D: int, causal: bool, scale: float) -> Optiona
       feature D is 1 in every query, 0 in every real key and -32768 in every padded
       key, so a padded key scores -32768 * scale below any real one and gets weight 0
       (its V rows are 0 as well)."""
-    dims = [D] + [d for d in ((64, 128, 256) if t.dtype == torch.bfloat16 else (64,)) if d > D]
+    dims = [D] + [d for d in ((64, 128, 256) if t.dtype == torch.bfloat16 else (64, 128)) if d > D]
     for dp in dims:
         if _gpu_ok(t, S, dp):
             return S, dp, 0

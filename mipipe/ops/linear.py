@@ -145,6 +145,10 @@ class ActFold:
     def offer(self, act: int, saved: Tensor, p: float, seed: int, offset: int) -> None:
         self.act, self.saved, self.p, self.seed, self.offset = act, saved, p, seed, offset
 
+    def release(self) -> None:
+        """Drops the offered tensor (the consumer took its own reference, or none came)."""
+        self.saved = None
+
     def ready_for(self, x2: Tensor) -> bool:
         s = self.saved
         return s is not None and s.shape == x2.shape and s.dtype == x2.dtype == torch.bfloat16
@@ -181,16 +185,24 @@ class _Linear(torch.autograd.Function):
                 if act == 2:
                     preact = pre_bias  # pre-BIAS; backward adds the bias back
         saved = preact if act == 2 else (y if act == 1 else None)
-        ctx.save_for_backward(x2, w, bias, saved)
-        ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
-        ctx.fused_tile = fused_tile
-        # activation backward folded into the consumer's dgrad (ActFold)
+        # activation backward folded into the consumer's dgrad (ActFold): the
+        # producer's saved tensor is ALSO saved here, through save_for_backward
+        # (released after this backward, seen by saved-tensor hooks), never
+        # held by the hand-off object itself
         ctx.fold_out = ctx.fold_in = None
+        fold_saved = None
         if fold_out is not None and fused_tile and act != 0 and x2.dtype == torch.bfloat16 and saved is not None:
             fold_out.offer(act, saved, p, seed, offset)
             ctx.fold_out = fold_out
         if fold_in is not None and fused_tile and fold_in.ready_for(x2) and ctx.needs_input_grad[0]:
             ctx.fold_in = fold_in
+            ctx.fold_args = (fold_in.act, fold_in.p, fold_in.seed, fold_in.offset)
+            fold_saved = fold_in.saved
+        if fold_in is not None:
+            fold_in.saved = None
+        ctx.save_for_backward(x2, w, bias, saved, fold_saved)
+        ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
+        ctx.fused_tile = fused_tile
         ctx.in_shape = shape
         y = y.view(*shape[:-1], w.shape[0])
         if res is not None:
@@ -203,7 +215,7 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, dres=None):  # type: ignore[override]
-        x2, w, bias, saved = ctx.saved_tensors
+        x2, w, bias, saved, fold_saved = ctx.saved_tensors
         dres_in = dy if ctx.has_res else None  # y = res + f(x): the residual input's gradient is dy
         if dy is None:  # only the fan-out branch carries a gradient
             return dres, None, None, None, None, None, None
@@ -244,7 +256,8 @@ class _Linear(torch.autograd.Function):
                     r2 = None
             fin = ctx.fold_in
             if ctx.fused_tile and fin is not None and r2 is None and dres is None:
-                dx = k.linear_dgrad(dpre, w, None, None, fin.act, fin.saved, fin.p, fin.seed, fin.offset)
+                f_act, f_p, f_seed, f_offset = ctx.fold_args
+                dx = k.linear_dgrad(dpre, w, None, None, f_act, fold_saved, f_p, f_seed, f_offset)
                 fin.done(dx)
             elif ctx.fused_tile:
                 dx = k.linear_dgrad(dpre, w, r2)

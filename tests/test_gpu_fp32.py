@@ -145,12 +145,16 @@ def _keyquad_keep(B, H, S, p, seed, offset):
 
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("p", [0.0, 0.25])
-@pytest.mark.parametrize("S", [32, 128, 160, 256])
-def test_attention_f32(k, causal, p, S):
+@pytest.mark.parametrize("S,D", [(32, 64), (128, 64), (160, 64), (256, 64), (128, 128), (160, 128), (64, 96)])
+def test_attention_f32(k, causal, p, S, D):
+    """fp32 kernels: D = 64 (dK/dV in one kernel), D = 128 (dV and dK kernels),
+    D = 96 (zero-padded to 128)."""
     from mipipe.ops import attention_packed
 
+    if p > 0 and D not in (64, 128):
+        pytest.skip("the mask replay below calls the kernel at the real head dim")
     torch.manual_seed(4)
-    B, H, D = 2, 3, 64
+    B, H = 2, 3
     scale = 1.0 / math.sqrt(D)
     qkv = torch.randn(B, S, 3, H, D, device=DEV, requires_grad=True)
     torch.manual_seed(11)

@@ -678,7 +678,7 @@ def test_feedforward_act_fold_matches_unfolded(k, activation, norm_first):
         out = blk.fc_out(xr, h, f)
         out.float().square().sum().backward()
         if fold:
-            assert f.saved is not None and f.grad is None  # offered, folded and consumed
+            assert f.act != 0 and f.saved is None and f.grad is None  # offered, taken over, folded, consumed
         grads.append([x.grad.float().clone()] + [prm.grad.float().clone() for prm in blk.parameters()])
     for a, b in zip(*grads):
         assert ((a - b).abs().max() / (b.abs().max() + 1e-12)).item() < 2e-2
