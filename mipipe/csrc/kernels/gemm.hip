@@ -336,6 +336,12 @@ __device__ __forceinline__ void glds16_saddr(const char* base, uint32_t off, con
       : "memory", "m0");
 }
 
+// s_waitcnt vmcnt(N): all but the N most recently issued vector-memory ops done.
+template <int N>
+__device__ __forceinline__ void vmcnt_keep() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 template <bool KC, int W>
 __device__ __forceinline__ void stage_fast(const bf16_t* base, int64_t ld, int k0, const uint32_t (&off)[W / 64],
                                            char* tile, int wave) {
@@ -520,19 +526,32 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
 //     in its phase-3 load interval -- so every wave's reads of tile u+1 start
 //     after a barrier all DMAs of the tile have landed behind.
 //
-// 0: one barrier per K-tile everywhere, 1: ping-pong everywhere, 2 (default):
+// 3 (default) / 4: as 2 / 1 with the B operand staged two K-tiles ahead (PP = 2).
+// 0: one barrier per K-tile everywhere, 1: ping-pong everywhere, 2:
 // ping-pong except the weight-gradient layout (both operands I-contiguous),
 // where the per-tile loop measured 1-4 % faster (profiles/gemm_saddr_ab.txt).
 // (A piece-staged variant -- each half-tile re-staged as soon as its own last
 // reader was 2 phases behind, 6 phases of DMA lead, counted vmcnt -- measured
 // 1-8 % slower than ping-pong: profiles/gemm_schedules_ab.txt.)
-int g_gemm_sched = 2;
+// Default 3: the B lead measured +3-7 % on the KC-layout forward / dgrad GEMMs
+// (enc12 qkv fwd 1313 -> 1365 TF/s, dec dgrad 1297 -> 1388, GPT-2-XL dgrads
+// +3-4 %), neutral elsewhere (profiles/gemm_sched_ab.txt).
+int g_gemm_sched = -1;  // -1: MIPIPE_GEMM_SCHED (default 3) not read yet
+int gemm_sched() {
+  if (g_gemm_sched < 0) {
+    const char* e = getenv("MIPIPE_GEMM_SCHED");
+    g_gemm_sched = e ? atoi(e) : 3;
+  }
+  return g_gemm_sched;
+}
 
 // W: block tile width along N -- 256, or 128 for grids where 256x256 tiles
 // would leave CUs idle (256x128 block, 128x32 per wave).
 // EXTRA: the bf16 epilogue also applies dropout and/or stores the
 // pre-activation (otherwise it is branch-free bias + activation).
-template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP, int W, bool EXTRA>
+// PP: 0 = one barrier per K-tile, 1 = ping-pong, 2 = ping-pong with the B
+// operand staged two K-tiles ahead (below).
+template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA>
 __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   constexpr int NJ = W / 64;          // 16-wide MFMA column tiles per wave
   constexpr int JJ = NJ / 2;          // ... per ping-pong quadrant
@@ -562,16 +581,29 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   uint32_t offA[4], offB[NJ];
   stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave, lane, offA);
   stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave, lane, offB);
+  // PP == 2 (LEADB): the B tile of K-tile u+2 is staged in phase 3 of tile u,
+  // into the buffer tile u is being computed from -- its B region is dead by
+  // then (B fragments are read in phases 0/1 and kept in registers; group 1's
+  // last B read of tile u, phase 1, retired two barriers earlier).  B thus has
+  // ~1.5 K-tiles to land instead of ~2 phases; the tile-end waits become
+  // vmcnt(NB): all but the B DMAs just issued (loads retire in order).
+  constexpr bool LEADB = PP == 2;
+  constexpr int NB = W / 64;  // B DMAs per wave per K-tile
   {
     int kl;
     const bf16_t* A = seg_base(g, true, kt0 * BK, kl);
     stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem, wave);
     const bf16_t* B = seg_base(g, false, kt0 * BK, kl);
     stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
+    if (LEADB && nk > 1) {
+      B = seg_base(g, false, (kt0 + 1) * BK, kl);
+      stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, wave);
+    }
   }
 
   if constexpr (PP) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (LEADB && nk > 1) vmcnt_keep<NB>();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
     bf16x8 af[4][2], bf[2][JJ][2];
@@ -602,12 +634,21 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
           const bf16_t* A = seg_base(g, true, (kt0 + u + 1) * BK, kl);
           stage_fast<A_KC, 256>(A, g.lda, kl, offA, nxt, wave);
         }
-        if (ph == 1 && more) {
+        if (!LEADB && ph == 1 && more) {
           int kl;
           const bf16_t* B = seg_base(g, false, (kt0 + u + 1) * BK, kl);
           stage_fast<B_KC, W>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
         }
-        if (ph == 3 && wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool lead = LEADB && u + 2 < nk;  // a B DMA two tiles ahead is issued this tile
+        if (ph == 3 && lead) {
+          int kl;
+          const bf16_t* B = seg_base(g, false, (kt0 + u + 2) * BK, kl);
+          stage_fast<B_KC, W>(B, g.ldb, kl, offB, const_cast<char*>(cur) + kTileBytes, wave);
+        }
+        if (ph == 3 && wm == 1) {
+          if (lead) vmcnt_keep<NB>();
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -623,7 +664,10 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
               acc[qm * 4 + ii][qn * JJ + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   af[ii][s], bf[qn][jj][s], acc[qm * 4 + ii][qn * JJ + jj], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        if (ph == 3 && wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ph == 3 && wm == 0) {
+          if (lead) vmcnt_keep<NB>();
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -742,7 +786,7 @@ int big_width(const GemmArgs& g) {
   return 0.75 * r128 < 1.0 * r256 ? 128 : 256;
 }
 
-template <bool A_KC, bool B_KC, int EPI, int ACT, bool PP, int W, bool EXTRA>
+template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA>
 void launch_big(const GemmArgs& g, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
@@ -756,12 +800,16 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
 
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
-  const bool pp = big::g_gemm_sched == 1 || (big::g_gemm_sched == 2 && (A_KC || B_KC));
+  const int sc = big::gemm_sched();
+  const bool pp = sc == 1 || sc == 4 || ((sc == 2 || sc == 3) && (A_KC || B_KC));
+  const bool lead = sc == 3 || sc == 4;
   const bool narrow = big_width(g) == 128;
-  if (pp && narrow) launch_big<A_KC, B_KC, EPI, ACT, true, 128, EXTRA>(g, s);
-  else if (pp) launch_big<A_KC, B_KC, EPI, ACT, true, 256, EXTRA>(g, s);
-  else if (narrow) launch_big<A_KC, B_KC, EPI, ACT, false, 128, EXTRA>(g, s);
-  else launch_big<A_KC, B_KC, EPI, ACT, false, 256, EXTRA>(g, s);
+  if (pp && lead && narrow) launch_big<A_KC, B_KC, EPI, ACT, 2, 128, EXTRA>(g, s);
+  else if (pp && lead) launch_big<A_KC, B_KC, EPI, ACT, 2, 256, EXTRA>(g, s);
+  else if (pp && narrow) launch_big<A_KC, B_KC, EPI, ACT, 1, 128, EXTRA>(g, s);
+  else if (pp) launch_big<A_KC, B_KC, EPI, ACT, 1, 256, EXTRA>(g, s);
+  else if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 0, 128, EXTRA>(g, s);
+  else launch_big<A_KC, B_KC, EPI, ACT, 0, 256, EXTRA>(g, s);
 }
 
 int g_gemm_group = -1;  // MIPIPE_GEMM_G: tile-rows per ordering group (A/B); -1 unread, 0 default
@@ -849,7 +897,7 @@ void launch_act(const GemmArgs& g, hipStream_t s) {
 void gemm_set_schedule(int mode) { big::g_gemm_sched = mode; }
 void gemm_set_width(int w) { g_gemm_width = w; }
 void gemm_set_rounds(int on) { g_gemm_rounds = on; }
-int gemm_get_schedule() { return big::g_gemm_sched; }
+int gemm_get_schedule() { return big::gemm_sched(); }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   // 16-byte operand chunks along M/N (I-contiguous layouts) and whole 64-deep K tiles.

@@ -34,9 +34,14 @@ from ..ops.linear import ActFold, mark_gemm_weight
 # Fan-out fusion of the residual-branch gradient (see AttentionCore.forward_fanout);
 # MIPIPE_FANOUT=0 turns it off (A/B measurements).
 FANOUT = os.environ.get("MIPIPE_FANOUT", "1") != "0"
-# MLP activation backward in fc_out's dgrad epilogue (ops.linear.ActFold);
-# MIPIPE_FOLD_ACT=0 turns it off (A/B measurements).
-FOLD_ACT = os.environ.get("MIPIPE_FOLD_ACT", "1") != "0"
+# MLP activation backward in fc_out's dgrad epilogue (ops.linear.ActFold), for
+# the activations in FOLD_ACTS.  ReLU only by default: its backward is a sign
+# test on the saved output, nearly free in the epilogue (enc12 FFN dgrad + act
+# backward 240 -> 222 us), while GELU's erf/exp per element made the epilogue
+# slower than the separate memory-bound kernel (GPT-2-XL fc2 dgrad 244 -> 251
+# us; tools/gemm_dact_probe.py).  MIPIPE_FOLD_ACT=0: off, =all: GELU too.
+_FOLD_ENV = os.environ.get("MIPIPE_FOLD_ACT", "relu")
+FOLD_ACTS = () if _FOLD_ENV == "0" else (("relu", "gelu") if _FOLD_ENV == "all" else ("relu",))
 
 __all__ = [
     "AttentionCore",
@@ -363,7 +368,7 @@ class FeedForwardBlock(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         # h's only consumer is fc_out: its dgrad applies the activation backward
-        fold = ActFold() if FOLD_ACT else None
+        fold = ActFold() if self.fc_in.activation in FOLD_ACTS else None
         h, xr = self.fc_in.forward_fanout(x, FANOUT, fold)
         out = self.fc_out(xr, h, fold)
         if fold is not None:

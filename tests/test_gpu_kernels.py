@@ -396,10 +396,11 @@ def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
 
 
 @pytest.mark.parametrize("width", [256, 128])
-@pytest.mark.parametrize("sched", [0, 1, 2])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4])
 def test_gemm_main_loop_schedules(k, sched, width):
-    """Every 256x256 main loop (per-tile barrier, ping-pong, the default mix) on every
-    layout, for 1, 2, 3 and many K-tiles, edge tiles, K-segments and the bf16 epilogue."""
+    """Every 256x256 main loop (per-tile barrier, ping-pong, the mixes, ping-pong with
+    the B lead) on every layout, for 1, 2, 3 and many K-tiles, edge tiles, K-segments
+    and the bf16 epilogue."""
     from mipipe.ops import linear
 
     old = k.gemm_get_schedule()
