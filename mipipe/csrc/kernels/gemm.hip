@@ -526,21 +526,23 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
 //     in its phase-3 load interval -- so every wave's reads of tile u+1 start
 //     after a barrier all DMAs of the tile have landed behind.
 //
-// 3 (default) / 4: as 2 / 1 with the B operand staged two K-tiles ahead (PP = 2).
+// 3 / 4 (default): as 2 / 1 with the B operand staged two K-tiles ahead (PP = 2).
 // 0: one barrier per K-tile everywhere, 1: ping-pong everywhere, 2:
 // ping-pong except the weight-gradient layout (both operands I-contiguous),
 // where the per-tile loop measured 1-4 % faster (profiles/gemm_saddr_ab.txt).
 // (A piece-staged variant -- each half-tile re-staged as soon as its own last
 // reader was 2 phases behind, 6 phases of DMA lead, counted vmcnt -- measured
 // 1-8 % slower than ping-pong: profiles/gemm_schedules_ab.txt.)
-// Default 3: the B lead measured +3-7 % on the KC-layout forward / dgrad GEMMs
+// Default 4: the B lead measured +3-7 % on the KC-layout forward / dgrad GEMMs
 // (enc12 qkv fwd 1313 -> 1365 TF/s, dec dgrad 1297 -> 1388, GPT-2-XL dgrads
-// +3-4 %), neutral elsewhere (profiles/gemm_sched_ab.txt).
-int g_gemm_sched = -1;  // -1: MIPIPE_GEMM_SCHED (default 3) not read yet
+// +3-4 %; profiles/gemm_sched_ab.txt), and with it the ping-pong loop beats
+// the per-tile one on the weight-gradient layout as well (+3-5 % at the sizes
+// of a step's flush: profiles/wgrad_flush_sched.txt).
+int g_gemm_sched = -1;  // -1: MIPIPE_GEMM_SCHED (default 4) not read yet
 int gemm_sched() {
   if (g_gemm_sched < 0) {
     const char* e = getenv("MIPIPE_GEMM_SCHED");
-    g_gemm_sched = e ? atoi(e) : 3;
+    g_gemm_sched = e ? atoi(e) : 4;
   }
   return g_gemm_sched;
 }

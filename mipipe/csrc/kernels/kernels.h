@@ -140,7 +140,7 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K);
 // g.ws with k_splits * M * N floats when it is > 1.
 int gemm_splitk_factor(const GemmArgs& g);
 // Main-loop schedule of the 256x256 GEMM: 0 = one barrier per K-tile, 1 = ping-pong wave groups,
-// 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout, 3 (default) / 4 = 2 / 1 with
+// 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout, 3 / 4 (default) = 2 / 1 with
 // the B operand staged two K-tiles ahead.
 void gemm_set_schedule(int mode);
 void gemm_set_width(int w);
