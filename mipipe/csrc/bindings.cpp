@@ -317,6 +317,28 @@ std::tuple<Tensor, Tensor> py_ce_fwd(Tensor logits, Tensor target, int64_t ignor
   return {loss, lse};
 }
 
+// Mean cross-entropy over the valid targets: (loss [] fp32, lse [N], weight [N] = valid / count).
+std::tuple<Tensor, Tensor, Tensor> py_ce_mean_fwd(Tensor logits, Tensor target, int64_t ignore_index) {
+  check_rows(logits, "logits");
+  check_cuda(target, "target");
+  MP_CHECK(target.scalar_type() == at::kLong && target.numel() == logits.size(0),
+           "cross_entropy_mean: expects [N, V] logits and [N] int64 target");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  const int64_t rows = logits.size(0), V = logits.size(1);
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss_row = at::empty({rows}, fopt);
+  auto lse = at::empty({rows}, fopt);
+  auto weight = at::empty({rows}, fopt);
+  auto loss = at::empty({}, fopt);
+  auto s = cur_stream(logits);
+  dispatch_fb(logits, "cross_entropy_mean_fwd", [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    cross_entropy_mean_fwd<T>(cptr<T>(logits), cptr<int64_t>(target), rows, V, logits.stride(0), ignore_index,
+                              ptr<float>(loss_row), ptr<float>(lse), ptr<float>(weight), ptr<float>(loss), s);
+  });
+  return {loss, lse, weight};
+}
+
 // A per-row fp32 vector, possibly strided (a column of a packed message's
 // statistic slots): its stride in floats.
 int64_t row_vector(const Tensor& t, int64_t rows, const char* name) {
@@ -1034,6 +1056,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cross_entropy_bwd", &py_ce_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("scale"),
         py::arg("ignore_index"), py::arg("row_scale") = py::none(), py::arg("out") = py::none(),
         py::arg("zero_pad") = false, py::arg("t_offset") = 0, py::arg("stat_out") = py::none());
+  m.def("cross_entropy_mean_fwd", &py_ce_mean_fwd, py::arg("logits"), py::arg("target"), py::arg("ignore_index"));
   m.def("vsplit_head_fwd", &py_vsplit_head_fwd);
   m.def("vsplit_tail_fwd", &py_vsplit_tail_fwd);
   m.def("embedding_fwd", &py_embed_fwd);

@@ -199,6 +199,12 @@ void attention_f32_bwd(const AttnArgs& a, hipStream_t s);
 template <typename T>
 void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
                        int64_t ignore_index, float* loss, float* lse, hipStream_t s, int64_t t_offset = 0);
+// Mean CE in two launches (row losses, then a one-block masked mean): loss[0] =
+// mean over valid targets; weight[r] = valid / count (the backward's row scale).
+template <typename T>
+void cross_entropy_mean_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
+                            int64_t ignore_index, float* loss_row, float* lse, float* weight, float* loss,
+                            hipStream_t s);
 // lse / row_scale read with strides ld_lse / ld_rs (floats); stat_out: (lse,
 // scale) written to nslot fp32 words per row (split-decoder gradient slots).
 template <typename T>

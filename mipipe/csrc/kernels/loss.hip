@@ -257,7 +257,63 @@ __global__ void __launch_bounds__(kT) ce_bwd_kernel(const T* __restrict__ logits
   for (int64_t c = V + threadIdx.x; c < zero_to; c += kT) Io<T>::store(d + c, 0.f);
 }
 
+// Plain CE mean: loss = sum(loss_row) / max(#valid targets, 1) with valid =
+// (t != ignore_index and 0 <= t < V); weight[r] = valid / count (the rows'
+// dL/dloss_row for dL/dloss = 1, read by the backward as its row scale).  One
+// block, fixed-order reduction (bitwise reproducible).
+__global__ void __launch_bounds__(kMeanT) ce_mean_kernel(const float* __restrict__ loss_row,
+                                                         const int64_t* __restrict__ target, int64_t rows, int64_t V,
+                                                         int64_t ignore_index, float* __restrict__ weight,
+                                                         float* __restrict__ loss) {
+  __shared__ float sl[kMeanT / 64], sc[kMeanT / 64], tot;
+  float a = 0.f, c = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += kMeanT) {
+    const int64_t t = target[r];
+    a += loss_row[r];
+    c += (t != ignore_index && t >= 0 && t < V) ? 1.f : 0.f;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sl[threadIdx.x >> 6] = a;
+    sc[threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float A = 0.f, C = 0.f;
+    for (int w = 0; w < kMeanT / 64; ++w) {
+      A += sl[w];
+      C += sc[w];
+    }
+    C = fmaxf(C, 1.f);
+    loss[0] = A / C;
+    tot = 1.f / C;
+  }
+  __syncthreads();
+  const float inv = tot;
+  for (int64_t r = threadIdx.x; r < rows; r += kMeanT) {
+    const int64_t t = target[r];
+    weight[r] = (t != ignore_index && t >= 0 && t < V) ? inv : 0.f;
+  }
+}
+
 }  // namespace
+
+template <typename T>
+void cross_entropy_mean_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,
+                            int64_t ignore_index, float* loss_row, float* lse, float* weight, float* loss,
+                            hipStream_t s) {
+  if (rows == 0) return;
+  hipLaunchKernelGGL((ce_fwd_kernel<T>), dim3((unsigned)rows), dim3(kT), 0, s, logits, target, V, ld, ignore_index,
+                     loss_row, lse, (int64_t)0);
+  hipLaunchKernelGGL(ce_mean_kernel, dim3(1), dim3(kMeanT), 0, s, loss_row, target, rows, V, ignore_index, weight,
+                     loss);
+}
+template void cross_entropy_mean_fwd<float>(const float*, const int64_t*, int64_t, int64_t, int64_t, int64_t, float*, float*, float*, float*, hipStream_t);
+template void cross_entropy_mean_fwd<bf16_t>(const bf16_t*, const int64_t*, int64_t, int64_t, int64_t, int64_t, float*, float*, float*, float*, hipStream_t);
 
 template <typename T>
 void cross_entropy_fwd(const T* logits, const int64_t* target, int64_t rows, int64_t V, int64_t ld,

@@ -46,17 +46,18 @@ class _CrossEntropy(torch.autograd.Function):
         k = kernels_for(logits)
         lc = logits if (logits.dim() == 2 and logits.stride(1) == 1) else logits.contiguous()
         target = target.contiguous()
-        loss_rows, lse = k.cross_entropy_fwd(lc, target, ignore_index)
-        count = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
-        ctx.save_for_backward(lc, target, lse, count)
+        # row losses, then a one-block masked mean: loss and the per-row weights
+        # valid / count (the backward's row scale) with no ATen reductions
+        loss, lse, weight = k.cross_entropy_mean_fwd(lc, target, ignore_index)
+        ctx.save_for_backward(lc, target, lse, weight)
         ctx.ignore_index = ignore_index
-        return loss_rows.sum() / count
+        return loss
 
     @staticmethod
     def backward(ctx, dloss):  # type: ignore[override]
-        logits, target, lse, count = ctx.saved_tensors
+        logits, target, lse, weight = ctx.saved_tensors
         k = kernels_for(logits)
-        scale = (dloss.to(torch.float32) / count).reshape(1).contiguous()
+        scale = dloss.to(torch.float32).reshape(1)  # x weight[row] in the kernel
         n, v = logits.shape
         ld = logits.stride(0)
         if ld > v:
@@ -65,10 +66,10 @@ class _CrossEntropy(torch.autograd.Function):
             # its rows are 16-byte aligned (vector path) and the Decoder's
             # slice backward can hand the padded buffer on without a copy.
             buf = torch.empty((n, ld), dtype=logits.dtype, device=logits.device)
-            k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index, None, buf, True)
+            k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index, weight, buf, True)
             mark_zero_padded(buf)
             return buf[:, :v], None, None
-        return k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index), None, None
+        return k.cross_entropy_bwd(logits, target, lse, scale, ctx.ignore_index, weight), None, None
 
 
 def _rows_uniform(t: Tensor) -> bool:

@@ -14,6 +14,11 @@ the step the GPU spends in kernels (the rest is launch gaps and host waits).
 host blocks once the queue holds a few thousand packets.)
 
     python tools/pp_rank_emulation.py [--rank R] [--steps N]
+    python tools/pp_rank_emulation.py --config gpt2_xl --ranks all   # every rank in turn, one table
+
+With ``--ranks all`` the table ends with the PP-step estimate these per-rank
+times give: the slowest rank's wall x (1 + the planner's simulated bubble
+share), and the tokens/s that implies for the whole job.
 """
 import argparse
 import statistics
@@ -63,22 +68,59 @@ class Loopback(Channels):
         return _Done()
 
 
+# per-config defaults: BASELINE.json's PP=8 configs (#3 enc12 chunks 32 except_last, #4 GPT-2-XL chunks 8 always)
+DEFAULTS = {"enc12_d4096": (32, 32, "except_last"), "gpt2_xl": (8, 18, "always")}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="enc12_d4096", choices=sorted(DEFAULTS))
     ap.add_argument("--rank", type=int, default=-1, help="pipeline rank to emulate (default: the most loaded)")
+    ap.add_argument("--ranks", default=None, help="'all' or a comma list: emulate these ranks in turn")
     ap.add_argument("--pp", type=int, default=8)
-    ap.add_argument("--chunks", type=int, default=32)
-    ap.add_argument("--micro-batch", type=int, default=32)
+    ap.add_argument("--chunks", type=int, default=None)
+    ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--checkpoint", default="except_last")
+    ap.add_argument("--checkpoint", default=None)
     args = ap.parse_args()
+    d_chunks, d_mb, d_ck = DEFAULTS[args.config]
+    args.chunks = args.chunks or d_chunks
+    args.micro_batch = args.micro_batch or d_mb
+    args.checkpoint = args.checkpoint or d_ck
 
-    dev = torch.device("cuda", 0)
-    cfg = CONFIGS["enc12_d4096"]
+    cfg = CONFIGS[args.config]
     pp, m, mb = args.pp, args.chunks, args.micro_batch
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
     virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb)
-    rank = args.rank if args.rank >= 0 else max(range(pp), key=plan.rank_cost)
+    if args.ranks:
+        ranks = list(range(pp)) if args.ranks == "all" else [int(r) for r in args.ranks.split(",")]
+    else:
+        ranks = [args.rank if args.rank >= 0 else max(range(pp), key=plan.rank_cost)]
+    walls = {}
+    for rank in ranks:
+        walls[rank] = run_rank(args, cfg, plan, virtual, rank)
+        torch.cuda.empty_cache()
+    if len(walls) > 1:
+        from mipipe.parallel.stage import simulate_step
+        from mipipe.pipeline import checkpoint_stop_for
+
+        slow = max(walls, key=walls.get)
+        bwd_ratio = 2.0 + recompute  # as bench.py prices the plan, recompute explicit in the simulation
+        sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
+                                        pp, virtual, m, 2.0, deferred_w=0.5,
+                                        checkpoint_stop=checkpoint_stop_for(args.checkpoint, m))
+        bub = 1.0 - max(sim_busy) / sim_t  # the slowest rank's idle share
+        est = walls[slow] * (1.0 + bub)
+        tokens = m * mb * cfg.seq_len
+        print(f"# slowest rank {slow}: {walls[slow]:.1f} ms/step; planner-simulated bubble {100 * bub:.1f} % -> "
+              f"PP={pp} step ~{est:.1f} ms = {tokens / est * 1e3:,.0f} tokens/s for the job "
+              f"({m} x {mb} x {cfg.seq_len} tokens per step)")
+    return 0
+
+
+def run_rank(args, cfg, plan, virtual, rank) -> float:
+    dev = torch.device("cuda", 0)
+    pp, m, mb = args.pp, args.chunks, args.micro_batch
     torch.manual_seed(0)
     stages = [build_stage(cfg, plan, vs, device=dev, dtype=torch.bfloat16).train() for vs in plan.vstages(rank)]
     shapes = [stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(rank)]
@@ -97,7 +139,7 @@ def main() -> int:
     inputs = [tokens[i, :, :cfg.seq_len].to(dev) for i in range(m)] if rank == 0 else None
     targets = [tokens[i, :, 1:].contiguous().to(dev) for i in range(m)]
     params = sum(p.numel() for p in opt.params)
-    print(f"# PP={pp} rank {rank} of enc12_d4096 (plan v={virtual}, split head {plan.split_decoder}, "
+    print(f"# PP={pp} rank {rank} of {cfg.name} (plan v={virtual}, split head {plan.split_decoder}, "
           f"vstages {plan.vstages(rank)}, units {[len(plan.slice(v)) for v in plan.vstages(rank)]}), "
           f"{params / 1e6:.1f}M params, chunks {m} x micro-batch {mb} x {cfg.seq_len}, {args.checkpoint}")
 
@@ -119,8 +161,9 @@ def main() -> int:
     wall = statistics.median(walls)
     total = 2 + args.steps
     print(f"wall {wall:.2f} ms/step (median of {args.steps}); {total} steps executed in all -- GPU busy per step = "
-          f"rocprofv3 total kernel time / {total}")
-    return 0
+          f"rocprofv3 total kernel time / {total}", flush=True)
+    del engine, opt, stages
+    return wall
 
 
 if __name__ == "__main__":
