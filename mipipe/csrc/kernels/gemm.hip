@@ -589,8 +589,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   // last B read of tile u, phase 1, retired two barriers earlier).  B thus has
   // ~1.5 K-tiles to land instead of ~2 phases; the tile-end waits become
   // vmcnt(NB): all but the B DMAs just issued (loads retire in order).
-  constexpr bool LEADB = PP == 2;
+  constexpr bool LEADB = PP == 2 || PP == 3;
   constexpr int NB = W / 64;  // B DMAs per wave per K-tile
+  constexpr int NA = 4;       // A DMAs per wave per K-tile
   {
     int kl;
     const bf16_t* A = seg_base(g, true, kt0 * BK, kl);
@@ -601,9 +602,99 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       B = seg_base(g, false, (kt0 + 1) * BK, kl);
       stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, wave);
     }
+    if (PP == 3 && wm == 1 && nk > 1) {  // group 1 stages its A share one tile earlier (below)
+      A = seg_base(g, true, (kt0 + 1) * BK, kl);
+      stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem + kBuf, wave);
+    }
   }
 
-  if constexpr (PP) {
+  if constexpr (PP == 3) {
+    // Half-tile ping-pong: as PP = 2, but a K-tile is 2 phases of 32 MFMAs
+    // (one 64-row half of the wave's 128x64 tile each, all NJ column tiles:
+    // A fragments read in both phases, B in phase 0 and kept), so the two
+    // barriers of a phase are paid once per 512 MFMA cycles instead of 256.
+    // Intervals (global count, group 1 one behind): group 0 loads in 4u and
+    // 4u+2, group 1 in 4u+1 and 4u+3.  A read issued before a DMA into the
+    // same bytes returns the old bytes (same wave: program order; another
+    // wave: a barrier between), so a region may be restaged by a DMA issued
+    // after the barrier that follows its last read's ISSUE:
+    //   * the A region of tile u-1's buffer is last read by group 1 in 4u-1
+    //     (its phase-1 load): group 1 restages it with A(u+1) right there,
+    //     after its own reads (tile u+1 = tile u-1's buffer), group 0 in 4u;
+    //   * the B region of tile u's buffer is last read by group 1 in 4u+1:
+    //     both groups stage B(u+2) into it in their phase-1 loads (4u+2/4u+3).
+    // Every wave drains what tile u+1 needs before the barrier ending 4u+3:
+    // group 0 after its phase-1 MFMAs (vmcnt(NB): B(u+2) may be in flight),
+    // group 1 in its phase-1 load (vmcnt(NA + NB): A(u+2) and B(u+2)).
+    // DMA budget: 4-6 intervals (~2-3k cycles) per piece.
+    if (nk > 1) {
+      if (wm == 1) vmcnt_keep<NA + NB>();
+      else vmcnt_keep<NB>();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
+    bf16x8 af[4][2], bq[NJ][2];
+    for (int u = 0; u < nk; ++u) {
+      char* cur = smem + (u & 1) * kBuf;
+      char* nxt = smem + ((u + 1) & 1) * kBuf;
+      const bool more = u + 1 < nk, lead = u + 2 < nk;
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        // ---- load interval ----
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC, 256>(cur, wm * 128 + ph * 64 + 16 * ii, s, lane);
+        if (ph == 0) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) bq[j][s] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * j, s, lane);
+          if (wm == 0 && more) {
+            int kl;
+            const bf16_t* A = seg_base(g, true, (kt0 + u + 1) * BK, kl);
+            stage_fast<A_KC, 256>(A, g.lda, kl, offA, nxt, wave);
+          }
+        } else if (lead) {
+          int kl;
+          if (wm == 1) {
+            const bf16_t* A = seg_base(g, true, (kt0 + u + 2) * BK, kl);
+            stage_fast<A_KC, 256>(A, g.lda, kl, offA, cur, wave);
+          }
+          const bf16_t* B = seg_base(g, false, (kt0 + u + 2) * BK, kl);
+          stage_fast<B_KC, W>(B, g.ldb, kl, offB, cur + kTileBytes, wave);
+        }
+        if (ph == 1 && wm == 1) {
+          if (lead) vmcnt_keep<NA + NB>();
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- MFMA interval ----
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              acc[ph * 4 + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ii][s], bq[j][s], acc[ph * 4 + ii][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (ph == 1 && wm == 0) {
+          if (lead) vmcnt_keep<NB>();
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // equalise the barrier count
+  } else if constexpr (PP) {
     if (LEADB && nk > 1) vmcnt_keep<NB>();
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -806,7 +897,9 @@ void launch_big_w(const GemmArgs& g, hipStream_t s) {
   const bool pp = sc == 1 || sc == 4 || ((sc == 2 || sc == 3) && (A_KC || B_KC));
   const bool lead = sc == 3 || sc == 4;
   const bool narrow = big_width(g) == 128;
-  if (pp && lead && narrow) launch_big<A_KC, B_KC, EPI, ACT, 2, 128, EXTRA>(g, s);
+  if (sc == 5 && narrow) launch_big<A_KC, B_KC, EPI, ACT, 3, 128, EXTRA>(g, s);
+  else if (sc == 5) launch_big<A_KC, B_KC, EPI, ACT, 3, 256, EXTRA>(g, s);
+  else if (pp && lead && narrow) launch_big<A_KC, B_KC, EPI, ACT, 2, 128, EXTRA>(g, s);
   else if (pp && lead) launch_big<A_KC, B_KC, EPI, ACT, 2, 256, EXTRA>(g, s);
   else if (pp && narrow) launch_big<A_KC, B_KC, EPI, ACT, 1, 128, EXTRA>(g, s);
   else if (pp) launch_big<A_KC, B_KC, EPI, ACT, 1, 256, EXTRA>(g, s);

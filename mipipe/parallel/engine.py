@@ -65,11 +65,20 @@ __all__ = ["PipelineEngine", "StepStats", "schedule_actions"]
 
 @dataclass
 class StepStats:
-    loss: Optional[Tensor] = None
+    losses: List[Tensor] = field(default_factory=list)  # per-micro-batch losses (device scalars)
     busy_ms: float = 0.0          # GPU time of this rank's compute (events)
     step_ms: float = 0.0          # wall time of the step on this rank
     forward_ms: List[float] = field(default_factory=list)
     backward_ms: List[float] = field(default_factory=list)
+    _loss: Optional[Tensor] = field(default=None, repr=False)
+
+    @property
+    def loss(self) -> Optional[Tensor]:
+        """Mean loss over the micro-batches (None off the last stage).  Reduced on
+        first access, so a step whose loss nobody reads launches no reduction."""
+        if self._loss is None and self.losses:
+            self._loss = torch.stack(self.losses).float().mean()
+        return self._loss
 
 
 def schedule_actions(kind: str, m: int, n: int, j: int, virtual: int = 1) -> List[Tuple[str, int, int]]:
@@ -202,6 +211,7 @@ class PipelineEngine:
         self.measure = measure
         self.defer_wgrad = defer_wgrad
         self.grad_divisor = float(grad_divisor)
+        self._seeds: Dict[tuple, Tensor] = {}
         if schedule == "1f1b" and self.virtual > 1:
             raise ValueError("1f1b supports one chunk per rank")
         if isinstance(watchdog, (int, float)):
@@ -372,6 +382,18 @@ class PipelineEngine:
             return y
         return self.loss_fn(y, targets[i])
 
+    def _loss_seed(self, loss: Tensor) -> Tensor:
+        """Backward seed of a micro-batch loss: d(mean over the m micro-batches and
+        the ``grad_divisor`` replicas)/d(loss) = 1 / (m * grad_divisor), a device
+        constant made once, so the loss path launches no divide and no fill."""
+        key = (loss.shape, loss.dtype, loss.device, self.chunks, self.grad_divisor)
+        seed = self._seeds.get(key)
+        if seed is None:
+            seed = torch.full(loss.shape, 1.0 / (self.chunks * self.grad_divisor), dtype=loss.dtype,
+                              device=loss.device)
+            self._seeds[key] = seed
+        return seed
+
     def _timer(self):
         if not self.measure or self.device.type != "cuda":
             return None
@@ -502,7 +524,7 @@ class PipelineEngine:
             if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
                 loss = self._loss(mod, y, targets, i)
                 losses.append(loss.detach())
-                y = loss / (m * self.grad_divisor)  # backward seeds from the scaled loss
+                y = loss  # its backward is seeded with 1 / (m * grad_divisor) (_loss_seed)
             if tm:
                 tm[1].record()
                 events.append(("F", tm))
@@ -546,7 +568,7 @@ class PipelineEngine:
                     with torch.enable_grad(), enable_recomputing():
                         y = self._run(mod, x, targets, i, tracker)
                         if last and (self.loss_fn is not None or getattr(mod, "fused_loss", False)):
-                            y = self._loss(mod, y, targets, i) / (m * self.grad_divisor)
+                            y = self._loss(mod, y, targets, i)
                 if tracker is not None:
                     skip_out[c][i] = tracker.outgoing
                 if tr:
@@ -556,7 +578,8 @@ class PipelineEngine:
                 y = stage_out[c][i]
             # Stashed skips are outputs of this chunk too: their gradients
             # (from the popping stage) seed the same backward pass.
-            outs, seeds = [y], [None if last else grad_buf[c][i]]
+            has_loss = last and (self.loss_fn is not None or getattr(mod, "fused_loss", False))
+            outs, seeds = [y], [(self._loss_seed(y) if has_loss else None) if last else grad_buf[c][i]]
             for key in self._stashes[c]:
                 r = routes[key]
                 if not r.has_grad:
@@ -576,10 +599,7 @@ class PipelineEngine:
             tm = self._timer()
             if tm:
                 tm[0].record()
-            if len(outs) == 1 and last:
-                y.backward()
-            else:
-                torch.autograd.backward(outs, seeds)
+            torch.autograd.backward(outs, seeds)
             if tm:
                 tm[1].record()
                 events.append(("B", tm))
@@ -659,8 +679,7 @@ class PipelineEngine:
                 armed.__exit__(None, None, None)
         self._mark("step done")
 
-        if losses:
-            stats.loss = torch.stack(losses).float().mean()
+        stats.losses = losses
         if events:
             torch.cuda.synchronize(self.device)
             for kind, (a, b) in events:

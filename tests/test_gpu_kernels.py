@@ -396,7 +396,7 @@ def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
 
 
 @pytest.mark.parametrize("width", [256, 128])
-@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4, 5])
 def test_gemm_main_loop_schedules(k, sched, width):
     """Every 256x256 main loop (per-tile barrier, ping-pong, the mixes, ping-pong with
     the B lead) on every layout, for 1, 2, 3 and many K-tiles, edge tiles, K-segments

@@ -58,7 +58,7 @@ def main() -> None:
         step()
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-    with torch.profiler.profile(activities=acts, with_stack=True) as prof:
+    with torch.profiler.profile(activities=acts, with_stack=True, record_shapes=True) as prof:
         step()
         torch.cuda.synchronize()
     kern = [e for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
@@ -73,10 +73,11 @@ def main() -> None:
             continue
         frames = [f for f in (e.stack or []) if ("mipipe" in f or "bench" in f or "tools" in f)
                   and "aten_audit" not in f]
-        where = frames[0] if frames else "(no mipipe frame)"
-        groups[(e.name, where)] += 1
-    for (name, where), n in groups.most_common(40):
-        print(f"{n:4d}  {name:32s} {where}")
+        where = frames[0] if frames else "(no Python frame: autograd thread)"
+        shapes = str(getattr(e, "input_shapes", "") or "")[:70]
+        groups[(e.name, where, shapes)] += 1
+    for (name, where, shapes), n in groups.most_common(40):
+        print(f"{n:4d}  {name:24s} {shapes:72s} {where}")
 
 
 if __name__ == "__main__":
