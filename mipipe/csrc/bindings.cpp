@@ -747,7 +747,11 @@ void py_column_sum_segments(std::vector<Tensor> xs, Tensor out, bool accumulate)
 // of once per micro-batch and K is long enough to amortise the tile prologue.
 // accumulate = false: the FIRST launch overwrites main_grad (its first write of
 // the step after a lazy zero_grad), later launches accumulate.
-void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, Tensor main_grad, bool accumulate) {
+// bias_grad (optional, fp32 [N]): the bias gradient colsum(dy) folded into the
+// same GEMMs (GemmArgs::rowsum, accumulated); returns false (nothing added to
+// bias_grad) when the shape cannot take the fold -- the caller then reduces it.
+bool py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, Tensor main_grad, bool accumulate,
+                              std::optional<Tensor> bias_grad) {
   MP_CHECK(!dys.empty() && dys.size() == xs.size(), "linear_wgrad_segments: need matching non-empty lists");
   check_cuda(main_grad, "main_grad");
   const int64_t T = dys[0].size(0), N = dys[0].size(1), K = xs[0].size(1);
@@ -767,7 +771,7 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
              "linear_wgrad_segments: every micro-batch needs the same row strides");
   at::hip::HIPGuardMasqueradingAsCUDA guard(main_grad.device());
   const int total = (int)dys.size();
-  for (int first = 0; first < total; first += GemmArgs::kMaxSegs) {
+  auto args_for = [&](int first) {
     const int n = std::min(GemmArgs::kMaxSegs, total - first);
     GemmArgs g;
     g.C = main_grad.data_ptr();
@@ -779,9 +783,23 @@ void py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
       g.b_seg[i] = xs[first + i].data_ptr();
     }
     g.A = g.a_seg[0]; g.B = g.b_seg[0];
+    return g;
+  };
+  bool fold = false;
+  if (bias_grad && dt == at::kBFloat16) {
+    check_cuda(*bias_grad, "bias_grad");
+    MP_CHECK(bias_grad->scalar_type() == at::kFloat && bias_grad->numel() == N && bias_grad->is_contiguous(),
+             "linear_wgrad_segments: bias_grad must be a contiguous fp32 [N]");
+    fold = true;
+    for (int first = 0; first < total && fold; first += GemmArgs::kMaxSegs) fold = gemm_rowsum_ok(args_for(first));
+  }
+  for (int first = 0; first < total; first += GemmArgs::kMaxSegs) {
+    GemmArgs g = args_for(first);
+    if (fold) g.rowsum = bias_grad->data_ptr<float>();
     Tensor ws = split_k_workspace(g, dt, main_grad);
     gemm_run(dt, g, cur_stream(main_grad));
   }
+  return fold;
 }
 
 // Generic test entry: C[M,N] (fp32) = A . B with A given [M,K] (a_kc) or [K,M],
@@ -1088,7 +1106,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_wgrad", &py_linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("main_grad"),
         py::arg("accumulate") = true);
   m.def("linear_wgrad_segments", &py_linear_wgrad_segments, py::arg("dys"), py::arg("xs"), py::arg("main_grad"),
-        py::arg("accumulate") = true);
+        py::arg("accumulate") = true, py::arg("bias_grad") = py::none());
   m.def("column_sum_segments", &py_column_sum_segments);
   m.def("gemm_f32", &py_gemm_f32);
   m.def("sumsq", &py_sumsq);

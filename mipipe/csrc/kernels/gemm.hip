@@ -538,11 +538,18 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
 // +3-4 %; profiles/gemm_sched_ab.txt), and with it the ping-pong loop beats
 // the per-tile one on the weight-gradient layout as well (+3-5 % at the sizes
 // of a step's flush: profiles/wgrad_flush_sched.txt).
-int g_gemm_sched = -1;  // -1: MIPIPE_GEMM_SCHED (default 4) not read yet
+// 5: half-tile ping-pong (PP = 3: 2 phases of 32 MFMAs per K-tile), 6: 5 on the
+// KC layouts and 4 on the weight-gradient layout, 7 (DEFAULT, round 3): whole-
+// tile ping-pong (PP = 4: one 64-MFMA interval per K-tile and wave, 236-242
+// VGPRs, no scratch).  Fewer, longer intervals pay the two barriers of a phase
+// less often: enc12 qkv fwd 1369 -> 1438 TF/s, dec dgrad 1387 -> 1500, the
+// enc12 PP=1 bench 139.0k -> 143.8k tok/s (same box, arms alternated;
+// profiles/gemm_sched_ab.txt).
+int g_gemm_sched = -1;  // -1: MIPIPE_GEMM_SCHED (default 7) not read yet
 int gemm_sched() {
   if (g_gemm_sched < 0) {
     const char* e = getenv("MIPIPE_GEMM_SCHED");
-    g_gemm_sched = e ? atoi(e) : 4;
+    g_gemm_sched = e ? atoi(e) : 7;
   }
   return g_gemm_sched;
 }
@@ -574,6 +581,18 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fused bias gradient (GemmArgs::rowsum): group-0 thread t sums the 4 rows
+  // [16 tn + 4 (t & 3), +4) of K-row t >> 2 of every A tile (I-contiguous image)
+  const bool rsum = g.rowsum != nullptr && tn < 16 && !A_KC;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto rowsum_step = [&](const char* tile) {
+    if (rsum && wm == 0) {
+      const int r = tid >> 2, c8 = 4 * tn + (tid & 3);
+      const s16x4 v = *reinterpret_cast<const s16x4*>(tile + ic_off_w<256>(r, c8));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+    }
+  };
   int kt0 = 0, nk = g.K / BK;
   if (g.k_splits > 1) {  // this block's share of the K-tiles
     const int total = nk;
@@ -589,7 +608,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   // last B read of tile u, phase 1, retired two barriers earlier).  B thus has
   // ~1.5 K-tiles to land instead of ~2 phases; the tile-end waits become
   // vmcnt(NB): all but the B DMAs just issued (loads retire in order).
-  constexpr bool LEADB = PP == 2 || PP == 3;
+  constexpr bool LEADB = PP == 2 || PP == 3 || PP == 4;
   constexpr int NB = W / 64;  // B DMAs per wave per K-tile
   constexpr int NA = 4;       // A DMAs per wave per K-tile
   {
@@ -598,7 +617,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem, wave);
     const bf16_t* B = seg_base(g, false, kt0 * BK, kl);
     stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
-    if (LEADB && nk > 1) {
+    if ((PP == 2 || PP == 3) && nk > 1) {
       B = seg_base(g, false, (kt0 + 1) * BK, kl);
       stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, wave);
     }
@@ -606,7 +625,74 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       A = seg_base(g, true, (kt0 + 1) * BK, kl);
       stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem + kBuf, wave);
     }
+    if (PP == 4 && wm == 1 && nk > 1) {  // group 1 stages whole tiles one tile earlier (below)
+      A = seg_base(g, true, (kt0 + 1) * BK, kl);
+      stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem + kBuf, wave);
+      B = seg_base(g, false, (kt0 + 1) * BK, kl);
+      stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, wave);
+    }
   }
+
+  if constexpr (PP == 4) {
+    // Whole-tile ping-pong: one load and one MFMA interval per K-tile and wave
+    // (64 MFMAs: the wave's whole 128x64 tile), barriers paid once per 1024
+    // MFMA cycles.  Group 0 loads tile u in interval 2u, group 1 in 2u+1
+    // (global count).  Tile u+1 goes into tile u-1's buffer, last read by
+    // group 1 in 2u-1: group 1 stages its share right after those reads
+    // (program order), group 0 in its load interval 2u.  Tile u+1 must have
+    // landed by the barrier ending 2u+1: group 0 drains after its MFMAs
+    // (vmcnt(0)), group 1 in its load interval 2u+1 after staging tile u+2
+    // (vmcnt(NA + NB)).
+    if (wm == 1 && nk > 1) vmcnt_keep<NA + NB>();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
+    bf16x8 af[8][2], bq[NJ][2];
+    for (int u = 0; u < nk; ++u) {
+      char* cur = smem + (u & 1) * kBuf;
+      char* nxt = smem + ((u + 1) & 1) * kBuf;
+#pragma unroll
+      for (int ii = 0; ii < 8; ++ii)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC, 256>(cur, wm * 128 + 16 * ii, s, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) bq[j][s] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * j, s, lane);
+      rowsum_step(cur);
+      const int ahead = wm == 0 ? 1 : 2;  // the tile this group stages now
+      if (u + ahead < nk) {
+        int kl;
+        char* dst = wm == 0 ? nxt : cur;
+        const bf16_t* A = seg_base(g, true, (kt0 + u + ahead) * BK, kl);
+        stage_fast<A_KC, 256>(A, g.lda, kl, offA, dst, wave);
+        const bf16_t* B = seg_base(g, false, (kt0 + u + ahead) * BK, kl);
+        stage_fast<B_KC, W>(B, g.ldb, kl, offB, dst + kTileBytes, wave);
+      }
+      if (wm == 1) {
+        if (u + 2 < nk) vmcnt_keep<NA + NB>();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int ii = 0; ii < 8; ++ii)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ii][s], bq[j][s], acc[ii][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // equalise the barrier count
+  } else
 
   if constexpr (PP == 3) {
     // Half-tile ping-pong: as PP = 2, but a K-tile is 2 phases of 32 MFMAs
@@ -647,6 +733,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
           for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC, 256>(cur, wm * 128 + ph * 64 + 16 * ii, s, lane);
+        if (ph == 0) rowsum_step(cur);
         if (ph == 0) {
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
@@ -715,6 +802,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC, 256>(cur, wm * 128 + qm * 64 + 16 * ii, s, lane);
         }
+        if (ph == 0) rowsum_step(cur);
         if (ph == 0 || ph == 1) {
 #pragma unroll
           for (int jj = 0; jj < JJ; ++jj)
@@ -782,6 +870,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       stage_fast<B_KC, W>(B, g.ldb, kl, offB, nxt + kTileBytes, wave);
     }
     const char* cur = smem + (kt & 1) * kBuf;
+    rowsum_step(cur);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 bfr[NJ];
@@ -797,6 +886,25 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   }
   }
 
+  if (rsum) {  // K-rows -> one sum per row: lanes (xor over the K-row bits), then the 4 group-0 waves through LDS
+    __syncthreads();  // every wave is done reading the operand buffers
+    float* red = reinterpret_cast<float*>(smem);
+    if (wm == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = 4; o < 64; o <<= 1) rs[e] += __shfl_xor(rs[e], o, 64);
+      if (lane < 4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[wave * 16 + 4 * lane + e] = rs[e];
+    }
+    __syncthreads();
+    if (tid < 16) {
+      const float v = red[tid] + red[16 + tid] + red[32 + tid] + red[48 + tid];
+      const int row = m0 + 16 * tn + tid;
+      if (row < g.M) g.rowsum[row] += v;
+    }
+  }
   // ---- epilogue ----
   // 1) element-wise epilogue in registers (accumulator layout): bias,
   //    activation, dropout (the mask is tied to this layout); with an aux
@@ -894,11 +1002,14 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
   const int sc = big::gemm_sched();
-  const bool pp = sc == 1 || sc == 4 || ((sc == 2 || sc == 3) && (A_KC || B_KC));
-  const bool lead = sc == 3 || sc == 4;
+  const bool pp = sc == 1 || sc == 4 || sc == 6 || ((sc == 2 || sc == 3) && (A_KC || B_KC));
+  const bool lead = sc == 3 || sc == 4 || sc == 6;
   const bool narrow = big_width(g) == 128;
-  if (sc == 5 && narrow) launch_big<A_KC, B_KC, EPI, ACT, 3, 128, EXTRA>(g, s);
-  else if (sc == 5) launch_big<A_KC, B_KC, EPI, ACT, 3, 256, EXTRA>(g, s);
+  const bool half = sc == 5 || (sc == 6 && (A_KC || B_KC));
+  if (sc == 7 && narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA>(g, s);
+  else if (sc == 7) launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA>(g, s);
+  else if (half && narrow) launch_big<A_KC, B_KC, EPI, ACT, 3, 128, EXTRA>(g, s);
+  else if (half) launch_big<A_KC, B_KC, EPI, ACT, 3, 256, EXTRA>(g, s);
   else if (pp && lead && narrow) launch_big<A_KC, B_KC, EPI, ACT, 2, 128, EXTRA>(g, s);
   else if (pp && lead) launch_big<A_KC, B_KC, EPI, ACT, 2, 256, EXTRA>(g, s);
   else if (pp && narrow) launch_big<A_KC, B_KC, EPI, ACT, 1, 128, EXTRA>(g, s);
@@ -994,6 +1105,11 @@ void gemm_set_width(int w) { g_gemm_width = w; }
 void gemm_set_rounds(int on) { g_gemm_rounds = on; }
 int gemm_get_schedule() { return big::gemm_sched(); }
 
+bool gemm_rowsum_ok(const GemmArgs& g) {
+  return !g.a_kc && (g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32) && use_big(g) && gemm_splitk_factor(g) <= 1 &&
+         (g.N + big_width(g) - 1) / big_width(g) >= 16;
+}
+
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   // 16-byte operand chunks along M/N (I-contiguous layouts) and whole 64-deep K tiles.
   // ... and 32-bit per-lane staging offsets: a K-contiguous operand spans < 4 GiB.
@@ -1061,6 +1177,7 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
   // only when the last round is at most half full (see above)
   if (tm * tn <= 256 || (tm * tn) % 256 == 0 || (tm * tn) % 256 > 128) return false;
   const bool along_n = tn >= tm;
+  if (along_n && g.rowsum != nullptr) return false;  // the row slices need every tile column of a tile row
   const int other = along_n ? tm : tn, along = along_n ? tn : tm;
   const int per = 256 / other;  // tiles of the split dimension per launch
   if (per < 1 || (along + per - 1) / per > 16) return false;
@@ -1083,6 +1200,7 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
     } else {
       c.M = hi - lo;
       c.mask_row0 = g.mask_row0 + lo;
+      if (g.rowsum != nullptr) c.rowsum = g.rowsum + lo;
       const int64_t aoff = (g.a_kc ? (int64_t)lo * g.lda : (int64_t)lo) * 2;
       c.A = byte_off(g.A, aoff);
       for (int i = 0; i < GemmArgs::kMaxSegs; ++i) c.a_seg[i] = byte_off(g.a_seg[i], aoff);

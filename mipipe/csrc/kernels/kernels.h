@@ -132,10 +132,18 @@ struct GemmArgs {
   // dimensions lda / ldb); seg_k must be a multiple of 64.
   static constexpr int kMaxSegs = 16;
   int seg_k = 0;
+  // Fused bias gradient of a weight-gradient GEMM (A = dY read as [K=T, M]):
+  // rowsum[m] += sum_k A[k][m], fp32.  The 256 rows of a tile row are split
+  // into 16-row slices summed by the blocks tn = 0..15 of that tile row, each
+  // over the whole K (one writer per row: deterministic).  Needs
+  // ceil(N / block width) >= 16 and k_splits == 1 (gemm_rowsum_ok).
+  float* rowsum = nullptr;
   const void* a_seg[kMaxSegs] = {};
   const void* b_seg[kMaxSegs] = {};
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
+// True if gemm_bf16 can fold g.rowsum into g (the wgrad layout, no split-K, >= 16 tile columns).
+bool gemm_rowsum_ok(const GemmArgs& g);
 // Split-K factor gemm_bf16 would use for g (1 = none); the caller provides
 // g.ws with k_splits * M * N floats when it is > 1.
 int gemm_splitk_factor(const GemmArgs& g);

@@ -19,6 +19,7 @@ torch.matmul with the same fused elementwise kernels.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Optional
 
 import torch
@@ -292,6 +293,9 @@ class _Linear(torch.autograd.Function):
 # micro-batch.  Module-level (not thread-local): autograd runs backward on its
 # own device threads.
 _DEFERRED: Optional[dict] = None
+# Bias gradients folded into the weight-gradient GEMMs of the flush
+# (MIPIPE_FUSE_BIAS=0: separate column-sum kernels, for A/B runs).
+_FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 
 
 def _defer(w: Tensor, dy: Tensor, x: Tensor) -> None:
@@ -352,24 +356,45 @@ def flush_wgrad() -> None:
     listeners = list(_WGRAD_LISTENERS)
     for li in listeners:
         li.flush_begin([w for w, _, _ in queue.values()])
+    # A bias queued with the very dY tensors of a weight (one Linear) has its
+    # column sums folded into that weight's GEMMs (GemmArgs::rowsum) when the
+    # shape allows; it is reduced when its weight is processed.
+    weight_dys = {tuple(id(d) for d in dys) for _, dys, xs in queue.values() if xs is not None}
+    bias_of = {}
+    for b, dys, xs in queue.values():
+        key = tuple(id(d) for d in dys)
+        if xs is None and key in weight_dys:
+            bias_of[key] = b
     for w, dys, xs in queue.values():
+        key = tuple(id(d) for d in dys)
+        if xs is None and bias_of.get(key) is w:
+            continue  # with its weight
         k = kernels_for(dys[0])
         # a single-process Pipe queues weights of several devices: launch each on its own
         dev = dys[0].device
+        done = [w]
         with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
             if xs is None:  # a bias
                 k.column_sum_segments(dys, w.main_grad, True)
             else:
+                b = bias_of.get(key)
+                fused = False
                 T = dys[0].shape[0]
                 uniform = (all(d.shape == dys[0].shape and d.stride() == dys[0].stride() for d in dys)
                            and all(x.shape == xs[0].shape and x.stride() == xs[0].stride() for x in xs))
                 if uniform and T % 64 == 0:
-                    k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w))
+                    fused = k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w),
+                                                    b.main_grad if (b is not None and _FUSE_BIAS) else None)
                 else:
                     for d, x in zip(dys, xs):
                         k.linear_wgrad(d, x, w.main_grad, _claim(w))
+                if b is not None:
+                    if not fused:
+                        k.column_sum_segments(dys, b.main_grad, True)
+                    done.append(b)
         for li in listeners:
-            li.wgrad_done(w)
+            for p in done:
+                li.wgrad_done(p)
 
 
 def begin_deferred_wgrad() -> bool:

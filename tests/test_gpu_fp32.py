@@ -193,15 +193,18 @@ def test_attention_f32_recompute_replays_mask(k):
     assert (s1, off1) == (s2, off2) and torch.equal(o1, o2) and torch.equal(lse1, lse2)
 
 
-def test_transformer_layer_fp32_on_kernels(k):
+@pytest.mark.parametrize("S", [128, 37, 40, 100])
+def test_transformer_layer_fp32_on_kernels(k, S):
     """fp32 post-norm TransformerEncoderLayer (the reference's layer and precision) on the
-    fp32 GEMM / attention / LN kernels vs nn.TransformerEncoderLayer: no eager fallback."""
+    fp32 GEMM / attention / LN kernels vs nn.TransformerEncoderLayer: no eager fallback,
+    also on the short tail windows of the reference's get_batch (S = 37 / 40 / 100: padded
+    keys masked by the kernels' key bound; /root/reference/main.py:108-113)."""
     from torch import nn
 
     from mipipe.models import TransformerEncoderLayer
 
     torch.manual_seed(0)
-    E, H, F_, B, S = 256, 4, 512, 3, 128
+    E, H, F_, B = 256, 4, 512, 8
     ref = nn.TransformerEncoderLayer(E, H, F_, dropout=0.0, batch_first=True).to(DEV)
     ours = TransformerEncoderLayer(E, H, F_, dropout=0.0, device=DEV).load_from_torch(ref)
     x = torch.randn(B, S, E, device=DEV, requires_grad=True)

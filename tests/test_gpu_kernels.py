@@ -396,7 +396,7 @@ def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
 
 
 @pytest.mark.parametrize("width", [256, 128])
-@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_gemm_main_loop_schedules(k, sched, width):
     """Every 256x256 main loop (per-tile barrier, ping-pong, the mixes, ping-pong with
     the B lead) on every layout, for 1, 2, 3 and many K-tiles, edge tiles, K-segments
@@ -436,6 +436,36 @@ def test_gemm_main_loop_schedules(k, sched, width):
     finally:
         k.gemm_set_schedule(old)
         k.gemm_set_width(0)
+
+
+@pytest.mark.parametrize("sched", [0, 4, 5, 6, 7])
+def test_wgrad_segments_fused_bias(k, sched):
+    """The bias gradient folded into the K-segmented weight-gradient GEMM
+    (GemmArgs::rowsum): equal to the column sums of every dY, accumulated; a
+    shape that cannot take the fold (< 16 tile columns, or split-K) returns
+    False and leaves the bias gradient alone."""
+    old = k.gemm_get_schedule()
+    k.gemm_set_schedule(sched)
+    try:
+        torch.manual_seed(11)
+        for N, Kin, T, nseg in [(520, 4096, 256, 3), (1000, 4104, 128, 18), (256, 512, 128, 2), (1024, 4096, 1024, 16)]:
+            dys = [torch.randn(T, N, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+            xs = [torch.randn(T, Kin, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+            main = torch.zeros(N, Kin, device=DEV)
+            bias = torch.full((N,), 0.5, device=DEV)
+            fused = k.linear_wgrad_segments(dys, xs, main, True, bias)
+            expect = sum(d.float().t() @ x.float() for d, x in zip(dys, xs))
+            assert ((main - expect).abs().max() / expect.abs().max()).item() < 1e-3, (N, Kin, sched)
+            if Kin < 4096:
+                assert not fused
+            if fused:
+                ref = 0.5 + sum(d.float().sum(0) for d in dys)
+                assert torch.allclose(bias, ref, atol=1e-2, rtol=1e-4), (N, Kin, sched, (bias - ref).abs().max())
+            else:
+                assert torch.all(bias == 0.5)
+    finally:
+        k.gemm_set_schedule(old)
+
 
 
 @pytest.mark.parametrize("M,K,N", [(2048, 4096, 9216), (1000, 4096, 8192), (2048, 1600, 28928), (776, 1024, 16384)])

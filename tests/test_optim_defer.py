@@ -22,9 +22,15 @@ class _FakeK:
         else:
             main.copy_(g)
 
-    def linear_wgrad_segments(self, dys, xs, main, accumulate):
+    fold_bias = True  # what the native binding answers for a bias_grad (shape-dependent there)
+
+    def linear_wgrad_segments(self, dys, xs, main, accumulate, bias_grad=None):
         for i, (d, x) in enumerate(zip(dys, xs)):
             self.linear_wgrad(d, x, main, accumulate or i > 0)
+        if bias_grad is None or not self.fold_bias:
+            return False
+        bias_grad.add_(sum(d.float().sum(0) for d in dys))
+        return True
 
     def column_sum_segments(self, dys, main, accumulate):
         s = sum(d.float().sum(0) for d in dys)
@@ -104,3 +110,45 @@ def test_zero_grad_keeps_other_optimizers_queue(fake_kernels):
     assert lin.deferred_param_ids() == {id(w1)}
     o1.fold_grads()
     assert torch.allclose(w1.main_grad, dy.t() @ x, atol=1e-5)
+
+
+@pytest.mark.parametrize("fold", [True, False])
+def test_flush_folds_bias_into_its_weight_gemm(fake_kernels, monkeypatch, fold):
+    """A bias queued with its weight's dY tensors is reduced with that weight (folded into
+    the GEMM, or by a column sum when the binding declines); listeners hear of both."""
+    monkeypatch.setattr(_FakeK, "fold_bias", fold)
+    w = torch.zeros(3, 4)
+    b = torch.zeros(3)
+    w.main_grad = torch.zeros(3, 4)
+    b.main_grad = torch.full((3,), 1.0)
+    lone = torch.zeros(3)
+    lone.main_grad = torch.zeros(3)
+    dys = [torch.randn(8, 3) for _ in range(2)]
+    xs = [torch.randn(8, 4) for _ in range(2)]
+    other = [torch.randn(8, 3)]
+    seen = []
+
+    class L:
+        def flush_begin(self, pending):
+            seen.append(("begin", len(pending)))
+
+        def wgrad_done(self, p):
+            seen.append(p)
+
+    li = L()
+    lin.add_wgrad_listener(li)
+    try:
+        assert lin.begin_deferred_wgrad()
+        for d, x in zip(dys, xs):
+            lin._defer_bias(b, d)
+            lin._defer(w, d, x)
+        lin._defer_bias(lone, other[0])
+        lin.end_deferred_wgrad()
+    finally:
+        lin.remove_wgrad_listener(li)
+    assert torch.allclose(w.main_grad, sum(d.t() @ x for d, x in zip(dys, xs)), atol=1e-5)
+    assert torch.allclose(b.main_grad, 1.0 + sum(d.sum(0) for d in dys), atol=1e-5)
+    assert torch.allclose(lone.main_grad, other[0].sum(0), atol=1e-5)
+    assert seen[0] == ("begin", 3)
+    done = seen[1:]
+    assert len(done) == 3 and any(p is w for p in done) and any(p is b for p in done) and any(p is lone for p in done)
