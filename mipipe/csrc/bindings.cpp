@@ -468,8 +468,9 @@ std::tuple<Tensor, int64_t, int64_t> py_embed_fwd(Tensor tokens, Tensor weight, 
   const int64_t S = tokens.size(1), E = weight.size(1), V = weight.size(0);
   if (pe) {
     check_cuda(*pe, "pe");
-    MP_CHECK(pe->scalar_type() == at::kFloat && pe->dim() == 2 && pe->size(1) == E && pe->size(0) >= S,
-             "embedding: pe must be fp32 [max_len >= S, E]");
+    MP_CHECK((pe->scalar_type() == at::kFloat || pe->scalar_type() == weight.scalar_type()) && pe->dim() == 2 &&
+                 pe->size(1) == E && pe->size(0) >= S && pe->is_contiguous(),
+             "embedding: pe must be a contiguous fp32 or weight-dtype [max_len >= S, E]");
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(weight.device());
   auto out = at::empty({tokens.size(0), S, E}, weight.options());
@@ -478,8 +479,9 @@ std::tuple<Tensor, int64_t, int64_t> py_embed_fwd(Tensor tokens, Tensor weight, 
   auto s = cur_stream(weight);
   dispatch_fb(weight, "embedding_fwd", [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    embedding_fwd<T>(cptr<int64_t>(tokens), cptr<T>(weight), pe ? cptr<float>(*pe) : nullptr, ptr<T>(out),
-                     tokens.numel(), (int)S, (int)E, V, (float)scale, (float)p, seed, offset, s);
+    embedding_fwd<T>(cptr<int64_t>(tokens), cptr<T>(weight), pe ? pe->data_ptr() : nullptr,
+                     pe ? pe->scalar_type() == at::kFloat : true, ptr<T>(out), tokens.numel(), (int)S, (int)E, V,
+                     (float)scale, (float)p, seed, offset, s);
   });
   return {out, (int64_t)seed, (int64_t)offset};
 }

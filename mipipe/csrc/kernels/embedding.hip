@@ -90,11 +90,15 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restric
 }  // namespace
 
 template <typename T>
-void embedding_fwd(const int64_t* tokens, const T* weight, const float* pe, T* out, int64_t rows, int seq_len, int E,
-                   int64_t V, float scale, float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+void embedding_fwd(const int64_t* tokens, const T* weight, const void* pe, bool pe_f32, T* out, int64_t rows,
+                   int seq_len, int E, int64_t V, float scale, float p, uint64_t seed, uint64_t offset, hipStream_t s) {
   if (rows == 0) return;
-  hipLaunchKernelGGL((embed_fwd_kernel<T, float>), dim3((unsigned)rows), dim3(256), 0, s, tokens, weight, pe, out,
-                     seq_len, E, V, scale, p, dropout_threshold(p), seed, offset);
+  if (pe_f32 || pe == nullptr)
+    hipLaunchKernelGGL((embed_fwd_kernel<T, float>), dim3((unsigned)rows), dim3(256), 0, s, tokens, weight,
+                       static_cast<const float*>(pe), out, seq_len, E, V, scale, p, dropout_threshold(p), seed, offset);
+  else  // a table in the model dtype (GPT-2's learned positions in a bf16 model): read as stored
+    hipLaunchKernelGGL((embed_fwd_kernel<T, T>), dim3((unsigned)rows), dim3(256), 0, s, tokens, weight,
+                       static_cast<const T*>(pe), out, seq_len, E, V, scale, p, dropout_threshold(p), seed, offset);
 }
 
 template <typename T>
@@ -105,8 +109,8 @@ void embedding_bwd(const int64_t* tokens, const T* dout, float* dweight, int64_t
                      seq_len > 0 ? seq_len : 1, E, V, scale, p, dropout_threshold(p), seed, offset);
 }
 
-template void embedding_fwd<float>(const int64_t*, const float*, const float*, float*, int64_t, int, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
-template void embedding_fwd<bf16_t>(const int64_t*, const bf16_t*, const float*, bf16_t*, int64_t, int, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
+template void embedding_fwd<float>(const int64_t*, const float*, const void*, bool, float*, int64_t, int, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
+template void embedding_fwd<bf16_t>(const int64_t*, const bf16_t*, const void*, bool, bf16_t*, int64_t, int, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t);
 template void embedding_bwd<float>(const int64_t*, const float*, float*, int64_t, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t, float*, int);
 template void embedding_bwd<bf16_t>(const int64_t*, const bf16_t*, float*, int64_t, int, int64_t, float, float, uint64_t, uint64_t, hipStream_t, float*, int);
 

@@ -235,9 +235,10 @@ void vsplit_tail_fwd(const T* logits, int64_t ld, int64_t rows, int64_t V, const
                      float* weight_row, float* loss, hipStream_t s);
 
 // ------------------------------------------------------------------ embedding
+// pe (optional): position table [>= seq_len, E], fp32 (pe_f32) or T.
 template <typename T>
-void embedding_fwd(const int64_t* tokens, const T* weight, const float* pe, T* out, int64_t rows, int seq_len, int E,
-                   int64_t V, float scale, float p, uint64_t seed, uint64_t offset, hipStream_t s);
+void embedding_fwd(const int64_t* tokens, const T* weight, const void* pe, bool pe_f32, T* out, int64_t rows,
+                   int seq_len, int E, int64_t V, float scale, float p, uint64_t seed, uint64_t offset, hipStream_t s);
 // dpe (optional): fp32 [>= seq_len, E] learned-position gradient, += the masked rows by position.
 template <typename T>
 void embedding_bwd(const int64_t* tokens, const T* dout, float* dweight, int64_t rows, int E, int64_t V, float scale,

@@ -255,6 +255,222 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
   }
 }
 
+// ---- wave-per-row variants for rows up to 2048 wide (GPT-2-XL's 1600,
+// ref_main's 2048) --------------------------------------------------------------
+// One wave per row, kRowWaves rows per block, reductions by wave shuffles only
+// (no LDS, no barriers in the row loop): at 1600 columns the one-row-per-
+// 256-thread kernels above leave 56 threads idle and pay two block barriers
+// per row with only 2 KB of row data in flight (latency-bound: ~3 TB/s).
+// Lane l holds 16-byte vectors l, l + 64, l + 128, l + 192 of its row.
+constexpr int kRowWaves = 8;
+constexpr int kRowNV = 4;
+
+// 8 elements kept as loaded (bf16: 4 registers instead of 8), converted on use.
+template <typename T> struct Raw8;
+template <> struct Raw8<float> {
+  float v[8];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void load(const float* p) { Io<float>::load8(p, v); }
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+};
+template <> struct Raw8<bf16_t> {
+  u16x8 v;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0;
+  }
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const u16x8*>(p); }
+  __device__ __forceinline__ float get(int i) const { return bf2f(v[i]); }
+};
+
+template <typename T>
+__global__ void __launch_bounds__(64 * kRowWaves) ln_fwd_rows_kernel(
+    const T* __restrict__ x, const T* __restrict__ res, const T* __restrict__ gamma, const T* __restrict__ beta,
+    T* __restrict__ y, T* __restrict__ z, float* __restrict__ mean_out, float* __restrict__ rstd_out, int rows,
+    int cols, float eps, float p, uint32_t threshold, uint64_t seed, uint64_t offset) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;  // whole waves: no barriers below
+  const size_t base = (size_t)row * cols;
+  const int nvec = cols >> 3;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  float v[kRowNV][8];
+  float s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRowNV; ++k) {
+    const int vi = lane + 64 * k;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[k][i] = 0.f;
+    if (vi < nvec) {
+      const size_t e = base + (size_t)vi * 8;
+      Io<T>::load8(x + e, v[k]);
+      if (p > 0.f) {
+        const uint32_t keep = dropout_keep8(seed, offset, e, threshold);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[k][i] = ((keep >> i) & 1) ? v[k][i] * scale : 0.f;
+      }
+      if (res != nullptr) {
+        float r[8];
+        Io<T>::load8(res + e, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[k][i] += r[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s1 += v[k][i];
+    }
+  }
+  const float mean = wave_sum(s1) / (float)cols;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRowNV; ++k)
+    if (lane + 64 * k < nvec)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[k][i] - mean;
+        s2 += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(s2) / (float)cols + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int k = 0; k < kRowNV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+      const size_t e = base + (size_t)vi * 8;
+      if (z != nullptr) Io<T>::store8(z + e, v[k]);
+      float g[8], b[8], o[8];
+      Io<T>::load8(gamma + vi * 8, g);
+      Io<T>::load8(beta + vi * 8, b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mean) * rstd * g[i] + b[i];
+      Io<T>::store8(y + e, o);
+    }
+  }
+}
+
+// Backward: gridDim.x = nparts blocks, waves stride over the rows; each lane
+// keeps its columns' dgamma / dbeta sums, folded over the block's waves through
+// LDS in wave order (deterministic) into the block's partial row.
+template <typename T>
+__global__ void __launch_bounds__(64 * kRowWaves) ln_bwd_rows_kernel(
+    const T* __restrict__ dy, const T* __restrict__ z, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const T* __restrict__ gamma, T* __restrict__ dz, T* __restrict__ dx,
+    float* __restrict__ dgamma_part, float* __restrict__ dbeta_part, int rows, int cols, float p,
+    uint32_t threshold, uint64_t seed, uint64_t offset, const T* __restrict__ addend) {
+  __shared__ float fold[2 * kRowNV * 8 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nvec = cols >> 3;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const float inv_n = 1.f / (float)cols;
+  // gamma is re-read per row (an L1/L2 hit): held in registers next to the
+  // row data and the dgamma / dbeta sums, it spilled
+  float dg[kRowNV][8], db[kRowNV][8];
+#pragma unroll
+  for (int k = 0; k < kRowNV; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dg[k][i] = db[k][i] = 0.f;
+  const int stride = gridDim.x * kRowWaves;
+  for (int row = blockIdx.x * kRowWaves + wave; row < rows; row += stride) {
+    const size_t base = (size_t)row * cols;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[kRowNV][8], gy[kRowNV][8];
+    Raw8<T> ad[kRowNV];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < kRowNV; ++k) {
+      const int vi = lane + 64 * k;
+      float zz[8], d[8], g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zz[i] = d[i] = g[i] = 0.f;
+      ad[k].zero();
+      if (vi < nvec) {
+        const size_t e = base + (size_t)vi * 8;
+        Io<T>::load8(z + e, zz);
+        Io<T>::load8(dy + e, d);
+        Io<T>::load8(gamma + vi * 8, g);
+        if (addend != nullptr) ad[k].load(addend + e);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xh[k][i] = (zz[i] - mean) * rstd;
+        gy[k][i] = d[i] * g[i];
+        dg[k][i] += d[i] * xh[k][i];
+        db[k][i] += d[i];
+        a += gy[k][i];
+        b += gy[k][i] * xh[k][i];
+      }
+    }
+    a = wave_sum(a) * inv_n;
+    b = wave_sum(b) * inv_n;
+#pragma unroll
+    for (int k = 0; k < kRowNV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        const size_t e = base + (size_t)vi * 8;
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = rstd * (gy[k][i] - a - xh[k][i] * b) + ad[k].get(i);
+        Io<T>::store8(dz + e, o);
+        if (dx != nullptr) {
+          const uint32_t keep = dropout_keep8(seed, offset, e, threshold);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = ((keep >> i) & 1) ? o[i] * scale : 0.f;
+          Io<T>::store8(dx + e, o);
+        }
+      }
+    }
+  }
+  // fold the waves' partials into wave 0, one wave at a time (fixed order)
+  for (int src = 1; src < kRowWaves; ++src) {
+    if (wave == src) {
+#pragma unroll
+      for (int k = 0; k < kRowNV; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          fold[((0 * kRowNV + k) * 8 + i) * 64 + lane] = dg[k][i];
+          fold[((1 * kRowNV + k) * 8 + i) * 64 + lane] = db[k][i];
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int k = 0; k < kRowNV; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          dg[k][i] += fold[((0 * kRowNV + k) * 8 + i) * 64 + lane];
+          db[k][i] += fold[((1 * kRowNV + k) * 8 + i) * 64 + lane];
+        }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < kRowNV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        const size_t o = (size_t)blockIdx.x * cols + vi * 8;
+        Io<float>::store8(dgamma_part + o, dg[k]);
+        Io<float>::store8(dbeta_part + o, db[k]);
+      }
+    }
+  }
+}
+
+// MIPIPE_LN_ROWS=0: the one-row-per-block kernels at every width (A/B runs).
+int g_ln_rows = -1;
+bool ln_rows_variant(int cols) {
+  if (g_ln_rows < 0) {
+    const char* e = getenv("MIPIPE_LN_ROWS");
+    g_ln_rows = e ? atoi(e) : 1;
+  }
+  return g_ln_rows != 0 && cols <= 64 * kRowNV * 8;
+}
+
 template <typename T, int MAXV>
 void launch_fwd(const LnArgs<T>& a, hipStream_t s) {
   hipLaunchKernelGGL((ln_fwd_kernel<T, MAXV>), dim3(a.rows), dim3(kThreads), 0, s, a.x, a.res, a.gamma, a.beta,
@@ -291,6 +507,12 @@ int ln_bwd_parts(int rows, int cols) {
 
 template <typename T>
 void layernorm_fwd(const LnArgs<T>& a, hipStream_t s) {
+  if (ln_rows_variant(a.cols)) {
+    hipLaunchKernelGGL((ln_fwd_rows_kernel<T>), dim3((a.rows + kRowWaves - 1) / kRowWaves), dim3(64 * kRowWaves), 0, s,
+                       a.x, a.res, a.gamma, a.beta, a.y, a.z, a.mean, a.rstd, a.rows, a.cols, a.eps, a.p,
+                       dropout_threshold(a.p), a.seed, a.offset);
+    return;
+  }
   switch (ln_max_vec(a.cols)) {
     case 1: launch_fwd<T, 1>(a, s); break;
     case 2: launch_fwd<T, 2>(a, s); break;
@@ -302,6 +524,13 @@ void layernorm_fwd(const LnArgs<T>& a, hipStream_t s) {
 
 template <typename T>
 void layernorm_bwd(const LnBwdArgs<T>& a, hipStream_t s) {
+  if (ln_rows_variant(a.cols)) {
+    hipLaunchKernelGGL((ln_bwd_rows_kernel<T>), dim3(a.nparts), dim3(64 * kRowWaves), 0, s, a.dy, a.z, a.mean, a.rstd,
+                       a.gamma, a.dz, a.dx, a.dgamma_part, a.dbeta_part, a.rows, a.cols, a.p, dropout_threshold(a.p),
+                       a.seed, a.offset, a.addend);
+    reduce_parts(a.dgamma_part, a.dbeta_part, a.nparts, a.cols, a.dgamma, a.dbeta, a.out_f32, a.accumulate, s);
+    return;
+  }
   switch (ln_max_vec(a.cols)) {
     case 1: launch_bwd<T, 1>(a, s); break;
     case 2: launch_bwd<T, 2>(a, s); break;

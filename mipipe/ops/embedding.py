@@ -61,6 +61,10 @@ def embed_scale_posenc_dropout(
         if pe is not None:
             x = x + pe[: tokens.shape[1]].to(x.dtype)
         return F.dropout(x, p, True) if p > 0 else x
-    if pe is not None and pe.dtype != torch.float32:
+    if pe is not None and pe.dtype not in (torch.float32, weight.dtype):
         pe = pe.float()
+    if pe is not None and not pe.is_contiguous():
+        pe = pe.contiguous()
+    # a table in the model dtype is read as stored: its gradient goes straight to
+    # its fp32 main_grad (no cast node, no dense gradient)
     return _Embed.apply(tokens, weight, pe, float(scale), p)

@@ -29,12 +29,18 @@ def layer_norm_reference(
 
 class _AddDropoutLayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, p, fanout=False):  # type: ignore[override]
+    def forward(ctx, x, residual, weight, bias, eps, p, fanout=False, save=True):  # type: ignore[override]
         ctx.set_materialize_grads(False)
         k = kernels_for(x)
         xc = x.contiguous()
         rc = residual.contiguous() if residual is not None else None
-        y, z, mean, rstd, seed, offset = k.layernorm_fwd(xc, rc, weight, bias, eps, p, True)
+        # z (the normalised sum) is written only for a backward, and only when it
+        # is not the input itself: a pre-norm LayerNorm (no residual, no dropout)
+        # saves x, and a forward under no_grad (a checkpointed stage) saves nothing
+        z_is_x = residual is None and p == 0.0
+        y, z, mean, rstd, seed, offset = k.layernorm_fwd(xc, rc, weight, bias, eps, p, save and not z_is_x)
+        if save and z_is_x:
+            z = xc
         ctx.save_for_backward(z, mean, rstd, weight)
         ctx.p = p
         ctx.seed = seed
@@ -51,7 +57,7 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
     def backward(ctx, dy, dfan=None):  # type: ignore[override]
         z, mean, rstd, weight = ctx.saved_tensors
         if dy is None:  # only the fan-out branch carries a gradient
-            return dfan, None, None, None, None, None, None
+            return dfan, None, None, None, None, None, None, None
         k = kernels_for(dy)
         mg = accumulable(weight)
         mb = accumulable(ctx.bias) if ctx.bias is not None else None
@@ -68,7 +74,7 @@ class _AddDropoutLayerNorm(torch.autograd.Function):
         if dfan is not None and add is None:
             dx = dx + dfan
         dres = dz if ctx.has_residual else None
-        return dx, dres, dgamma, dbeta, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None
 
 
 def add_dropout_layer_norm(
@@ -84,7 +90,7 @@ def add_dropout_layer_norm(
     p = float(p) if training else 0.0
     if not x.is_cuda:
         return layer_norm_reference(x, residual, weight, bias, eps, p, True)
-    return _AddDropoutLayerNorm.apply(x, residual, weight, bias, float(eps), p)
+    return _AddDropoutLayerNorm.apply(x, residual, weight, bias, float(eps), p, False, torch.is_grad_enabled())
 
 
 def layer_norm_fanout(x: Tensor, weight: Tensor, bias: Tensor, eps: float = 1e-5):

@@ -158,7 +158,7 @@ class ActFold:
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act, p, fanout=False, res=None, fold_out=None,
-                fold_in=None):  # type: ignore[override]
+                fold_in=None, save=True):  # type: ignore[override]
         ctx.set_materialize_grads(False)
         k = kernels_for(x)
         shape = x.shape
@@ -176,7 +176,8 @@ class _Linear(torch.autograd.Function):
                     r2 = r2.to(x2.dtype).contiguous()
                     if not _aligned(r2):
                         r2 = r2.clone()
-            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2, r2)
+            # GELU's pre-activation is written only for a backward (not under no_grad)
+            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2)
             res = None  # added in the epilogue
         else:
             y = torch.matmul(x2, w.t())
@@ -219,7 +220,7 @@ class _Linear(torch.autograd.Function):
         x2, w, bias, saved, fold_saved = ctx.saved_tensors
         dres_in = dy if ctx.has_res else None  # y = res + f(x): the residual input's gradient is dy
         if dy is None:  # only the fan-out branch carries a gradient
-            return dres, None, None, None, None, None, None
+            return dres, None, None, None, None, None, None, None, None, None
         k = kernels_for(dy)
         d2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         if ctx.fused_tile and not _aligned(d2):
@@ -279,7 +280,7 @@ class _Linear(torch.autograd.Function):
                 _add_or_copy(main, torch.matmul(dpre.t(), x2), w)
             else:
                 dw = torch.matmul(dpre.t(), x2)
-        return dx, dw, db, None, None, None, dres_in, None, None
+        return dx, dw, db, None, None, None, dres_in, None, None, None
 
 
 # ---------------------------------------------------------------- deferred wgrad
@@ -472,7 +473,8 @@ def linear(
     if not x.is_cuda:
         y = F.linear(x, weight)
         return bias_act_reference(y, bias, activation, p, True)
-    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p, False, None, act_fold_out, act_fold_in)
+    return _Linear.apply(x, weight, bias, ACTIVATIONS[activation], p, False, None, act_fold_out, act_fold_in,
+                         torch.is_grad_enabled())
 
 
 def linear_residual(

@@ -67,7 +67,7 @@ for name, M, N, K, kind in cases:
         for m in modes + modes[::-1]:
             k.gemm_set_schedule(m)
             res[m].append(timeit(fn))
-    k.gemm_set_schedule(4)
+    k.gemm_set_schedule(7)
     fl = 2.0 * M * N * K
     print(f"{name:22s} {M:6d} {N:6d} {K:6d} | " +
           " | ".join(f"{min(res[m]):8.1f} {fl / min(res[m]) / 1e6:5.0f}" for m in modes), flush=True)

@@ -48,7 +48,7 @@ for tag, T, shapes in (("gpt2xl", 4 * 18432, ((4800, 1600), (1600, 1600), (6400,
             for m in modes + modes[::-1]:
                 k.gemm_set_schedule(m)
                 res[m].append(timeit(lambda: k.linear_wgrad(dy, x, g, True)))
-        k.gemm_set_schedule(4)
+        k.gemm_set_schedule(7)
         fl = 2.0 * T * N * K
         print(f"{tag} [{N} x {K}], T={T} | " + " | ".join(f"{min(res[m]):9.1f} {fl / min(res[m]) / 1e6:5.0f}"
                                                           for m in modes), flush=True)
