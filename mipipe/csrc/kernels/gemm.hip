@@ -963,8 +963,11 @@ int big_tiles(const GemmArgs& g, int w) { return ((g.M + big::BM - 1) / big::BM)
 // The 256-row kernel handles every shape (edge tiles masked); the 128x128 one
 // only exact multiples of 128, where it is kept for grids too small to fill
 // the 256 CUs with 256x256 tiles.
+// Chunks of a per-round launch stay on it too: the last chunk of e.g.
+// GPT-2-XL's fc1 forward (18432 x 6400, 7 rounds + 2 tile rows) ran on the
+// 128x128 kernel at ~250 TF/s.
 bool use_big(const GemmArgs& g) {
-  return g.seg_k > 0 || g.M % BM != 0 || g.N % BN != 0 || big_tiles(g, 256) >= 128;
+  return g.round_chunk || g.seg_k > 0 || g.M % BM != 0 || g.N % BN != 0 || big_tiles(g, 256) >= 128;
 }
 
 // Block width of the 256-row kernel: 256, or 128 when the grid of 256x256
@@ -1184,6 +1187,7 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
   const int cbytes = g.epi == kEpiStoreBf16 ? 2 : 4;
   for (int t0 = 0; t0 < along; t0 += per) {
     GemmArgs c = g;
+    c.round_chunk = true;
     const int lo = t0 * 256, hi = std::min((t0 + per) * 256, along_n ? g.N : g.M);
     c.mask_ld = g.mask_ld > 0 ? g.mask_ld : g.N;
     if (along_n) {

@@ -126,6 +126,7 @@ struct GemmArgs {
   // position in the full output, so the dropout mask (Philox counter
   // (row >> 2) * mask_ld + col) is the full matrix's.  mask_ld = 0: N.
   int mask_row0 = 0, mask_col0 = 0, mask_ld = 0;
+  bool round_chunk = false;  // a launch_by_rounds chunk: stays on the 256-row kernel even when small
   // K-segmented operands (deferred weight gradients: one GEMM over the
   // micro-batches of a step without concatenating them).  seg_k > 0: K-rows
   // [s*seg_k, (s+1)*seg_k) of A / B live at a_seg[s] / b_seg[s] (leading

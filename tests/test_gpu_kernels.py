@@ -518,6 +518,10 @@ def test_gemm_round_launches_identical(k):
     r = torch.randn(4096, 4608, device=DEV).to(torch.bfloat16)
     dys = [torch.randn(256, 8200, device=DEV).to(torch.bfloat16) for _ in range(2)]  # wgrad 8200 x 2048: 33 x 8
     xs = [torch.randn(256, 2048, device=DEV).to(torch.bfloat16) for _ in range(2)]
+    # 11 x 25 tiles: a 23-column chunk and a 2-column one that is an exact multiple of the
+    # 128x128 kernel's tile (it stays on the 256-row kernel: GemmArgs::round_chunk)
+    x3 = torch.randn(2816, 512, device=DEV).to(torch.bfloat16)
+    w3 = (torch.randn(6400, 512, device=DEV) / math.sqrt(512)).to(torch.bfloat16)
 
     def run():
         torch.manual_seed(77)
@@ -527,7 +531,8 @@ def test_gemm_round_launches_identical(k):
         dx = k.linear_dgrad(dy, w2, r)
         mg = torch.zeros(8200, 2048, device=DEV)
         k.linear_wgrad_segments(dys, xs, mg, False)
-        return [y1, y2, pre, dx, mg]
+        y3 = k.linear_fwd(x3, w3, None, 0, 0.0, False)[0]
+        return [y1, y2, pre, dx, mg, y3]
 
     try:
         k.gemm_set_rounds(0)
@@ -544,6 +549,7 @@ def test_gemm_round_launches_identical(k):
     assert abs(kept.float().sum().item() / pos.float().sum().item() - 0.7) < 0.02
     assert torch.allclose(ref[0].float()[kept], (want / 0.7)[kept], atol=5e-2, rtol=3e-2)
     assert torch.allclose(ref[3].float(), dy.float() @ w2.float() + r.float(), atol=0.5, rtol=3e-2)
+    assert torch.allclose(ref[5].float(), x3.float() @ w3.float().t(), atol=5e-2, rtol=3e-2)
 
 
 def test_linear_op_matches_reference(k):
