@@ -1096,8 +1096,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_supported", &py_gemm_supported);
   m.def("gemm_f32_supported", &py_gemm_f32_supported);
   m.def("attention_set_fused_bwd", &attention_set_fused_bwd);
-  m.def("gemm_set_schedule", &gemm_set_schedule, "256x256 GEMM main loop: 0 per-tile barrier, 1 ping-pong, 2 ping-pong except wgrad (default)");
+  m.def("gemm_set_schedule", &gemm_set_schedule,
+        "256x256 GEMM main loop: 7 whole-tile ping-pong (default, the only one in the product build); a "
+        "--gemm-ab build also has the A/B schedules 0-6 (kernels.h).  Returns false for a schedule not built in.");
   m.def("gemm_get_schedule", &gemm_get_schedule);
+  m.def("gemm_ab_build", &gemm_ab_build, "true if the A/B GEMM schedules 0-6 are compiled in (-DMIPIPE_GEMM_AB)");
   m.def("gemm_set_rounds", &gemm_set_rounds, "1: launch multi-round GEMM grids one round of tiles at a time (default)");
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),

@@ -545,11 +545,17 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
 // less often: enc12 qkv fwd 1369 -> 1438 TF/s, dec dgrad 1387 -> 1500, the
 // enc12 PP=1 bench 139.0k -> 143.8k tok/s (same box, arms alternated;
 // profiles/gemm_sched_ab.txt).
+// Only schedule 7 is compiled into the product build (launch_big_w); the
+// others need -DMIPIPE_GEMM_AB.
 int g_gemm_sched = -1;  // -1: MIPIPE_GEMM_SCHED (default 7) not read yet
 int gemm_sched() {
   if (g_gemm_sched < 0) {
+#ifdef MIPIPE_GEMM_AB
     const char* e = getenv("MIPIPE_GEMM_SCHED");
     g_gemm_sched = e ? atoi(e) : 7;
+#else
+    g_gemm_sched = 7;
+#endif
   }
   return g_gemm_sched;
 }
@@ -985,6 +991,7 @@ int big_width(const GemmArgs& g) {
     g_gemm_width = e ? atoi(e) : 0;
   }
   if (g_gemm_width == 128 || g_gemm_width == 256) return g_gemm_width;
+  if (g.width == 128 || g.width == 256) return g.width;
   if (g.k_splits > 1) return 256;
   const int r256 = (big_tiles(g, 256) + 255) / 256, r128 = (big_tiles(g, 128) + 255) / 256;
   return 0.75 * r128 < 1.0 * r256 ? 128 : 256;
@@ -1002,12 +1009,20 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
                      dim3(big::kThreads), big::kSmemBytes, s, g);
 }
 
+// The product build instantiates the default main loop only (schedule 7, the
+// whole-tile ping-pong).  The A/B schedules 0-6 are compiled in only with
+// -DMIPIPE_GEMM_AB (python -m mipipe.build --gemm-ab), for tools/gemm_sched_ab.py
+// and the like; without it gemm_set_schedule() accepts 7 alone.
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
+  const bool narrow = big_width(g) == 128;
+#ifndef MIPIPE_GEMM_AB
+  if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA>(g, s);
+  else launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA>(g, s);
+#else
   const int sc = big::gemm_sched();
   const bool pp = sc == 1 || sc == 4 || sc == 6 || ((sc == 2 || sc == 3) && (A_KC || B_KC));
   const bool lead = sc == 3 || sc == 4 || sc == 6;
-  const bool narrow = big_width(g) == 128;
   const bool half = sc == 5 || (sc == 6 && (A_KC || B_KC));
   if (sc == 7 && narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA>(g, s);
   else if (sc == 7) launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA>(g, s);
@@ -1019,6 +1034,7 @@ void launch_big_w(const GemmArgs& g, hipStream_t s) {
   else if (pp) launch_big<A_KC, B_KC, EPI, ACT, 1, 256, EXTRA>(g, s);
   else if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 0, 128, EXTRA>(g, s);
   else launch_big<A_KC, B_KC, EPI, ACT, 0, 256, EXTRA>(g, s);
+#endif
 }
 
 int g_gemm_group = -1;  // MIPIPE_GEMM_G: tile-rows per ordering group (A/B); -1 unread, 0 default
@@ -1103,7 +1119,22 @@ void launch_act(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
-void gemm_set_schedule(int mode) { big::g_gemm_sched = mode; }
+bool gemm_set_schedule(int mode) {
+#ifndef MIPIPE_GEMM_AB
+  if (mode != 7) return false;
+#else
+  if (mode < 0 || mode > 7) return false;
+#endif
+  big::g_gemm_sched = mode;
+  return true;
+}
+bool gemm_ab_build() {
+#ifdef MIPIPE_GEMM_AB
+  return true;
+#else
+  return false;
+#endif
+}
 void gemm_set_width(int w) { g_gemm_width = w; }
 void gemm_set_rounds(int on) { g_gemm_rounds = on; }
 int gemm_get_schedule() { return big::gemm_sched(); }
@@ -1188,6 +1219,7 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
   for (int t0 = 0; t0 < along; t0 += per) {
     GemmArgs c = g;
     c.round_chunk = true;
+    c.width = 256;  // the full grid's width: the rowsum fold's slices assume its tile-column count
     const int lo = t0 * 256, hi = std::min((t0 + per) * 256, along_n ? g.N : g.M);
     c.mask_ld = g.mask_ld > 0 ? g.mask_ld : g.N;
     if (along_n) {

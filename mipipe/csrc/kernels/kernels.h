@@ -127,6 +127,7 @@ struct GemmArgs {
   // (row >> 2) * mask_ld + col) is the full matrix's.  mask_ld = 0: N.
   int mask_row0 = 0, mask_col0 = 0, mask_ld = 0;
   bool round_chunk = false;  // a launch_by_rounds chunk: stays on the 256-row kernel even when small
+  int width = 0;             // 256-row kernel block width forced by the caller (0: big_width's rule)
   // K-segmented operands (deferred weight gradients: one GEMM over the
   // micro-batches of a step without concatenating them).  seg_k > 0: K-rows
   // [s*seg_k, (s+1)*seg_k) of A / B live at a_seg[s] / b_seg[s] (leading
@@ -148,12 +149,14 @@ bool gemm_rowsum_ok(const GemmArgs& g);
 // Split-K factor gemm_bf16 would use for g (1 = none); the caller provides
 // g.ws with k_splits * M * N floats when it is > 1.
 int gemm_splitk_factor(const GemmArgs& g);
-// Main-loop schedule of the 256x256 GEMM: 0 = one barrier per K-tile, 1 = ping-pong wave groups,
-// 2 = ping-pong except the wgrad (I-contiguous x I-contiguous) layout, 3 / 4 (default) = 2 / 1 with
-// the B operand staged two K-tiles ahead.
-void gemm_set_schedule(int mode);
-void gemm_set_width(int w);
-void gemm_set_rounds(int on);  // 1: multi-round grids launched one round at a time (default), 0: one launch  // 256-row GEMM block width: 0 auto, 128, 256
+// Main-loop schedule of the 256x256 GEMM: 7 (default, the only one in the product build) = whole-tile
+// ping-pong.  A -DMIPIPE_GEMM_AB build also has 0 = one barrier per K-tile, 1 = 4-phase ping-pong,
+// 2 = 1 except the wgrad layout, 3 / 4 = 2 / 1 with the B operand staged two K-tiles ahead, 5 / 6 =
+// half-tile ping-pong (everywhere / on the K-contiguous layouts).  Returns false for a schedule not built.
+bool gemm_set_schedule(int mode);
+bool gemm_ab_build();
+void gemm_set_width(int w);    // 256-row GEMM block width: 0 auto, 128, 256
+void gemm_set_rounds(int on);  // 1: multi-round grids launched one round at a time (default), 0: one launch
 int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
 // Same interface with fp32 operands (and fp32 bias / res / aux / C): v_mfma_f32_32x32x2_f32.

@@ -260,26 +260,31 @@ __global__ void __launch_bounds__(kT) ce_bwd_kernel(const T* __restrict__ logits
 // Plain CE mean: loss = sum(loss_row) / max(#valid targets, 1) with valid =
 // (t != ignore_index and 0 <= t < V); weight[r] = valid / count (the rows'
 // dL/dloss_row for dL/dloss = 1, read by the backward as its row scale).  One
-// block, fixed-order reduction (bitwise reproducible).
+// block, fixed-order reduction (bitwise reproducible).  A target outside
+// [0, V) that is not ignore_index (nn.CrossEntropyLoss raises on it) makes
+// the loss and the row weights NaN: loud, without a host sync, where
+// leaving the row out would silently re-weight the mean.
 __global__ void __launch_bounds__(kMeanT) ce_mean_kernel(const float* __restrict__ loss_row,
                                                          const int64_t* __restrict__ target, int64_t rows, int64_t V,
                                                          int64_t ignore_index, float* __restrict__ weight,
                                                          float* __restrict__ loss) {
   __shared__ float sl[kMeanT / 64], sc[kMeanT / 64], tot;
-  float a = 0.f, c = 0.f;
+  float a = 0.f, c = 0.f, bad = 0.f;
   for (int64_t r = threadIdx.x; r < rows; r += kMeanT) {
     const int64_t t = target[r];
     a += loss_row[r];
     c += (t != ignore_index && t >= 0 && t < V) ? 1.f : 0.f;
+    bad += (t != ignore_index && (t < 0 || t >= V)) ? 1.f : 0.f;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o, 64);
     c += __shfl_xor(c, o, 64);
+    bad += __shfl_xor(bad, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
     sl[threadIdx.x >> 6] = a;
-    sc[threadIdx.x >> 6] = c;
+    sc[threadIdx.x >> 6] = c + (bad > 0.f ? 1e30f : 0.f);  // any bad target poisons the count
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -288,9 +293,10 @@ __global__ void __launch_bounds__(kMeanT) ce_mean_kernel(const float* __restrict
       A += sl[w];
       C += sc[w];
     }
+    const bool poisoned = C >= 1e30f;
     C = fmaxf(C, 1.f);
-    loss[0] = A / C;
-    tot = 1.f / C;
+    loss[0] = poisoned ? __builtin_nanf("") : A / C;
+    tot = poisoned ? __builtin_nanf("") : 1.f / C;
   }
   __syncthreads();
   const float inv = tot;

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import json
 import os
+import warnings
 from typing import Dict, Iterable, Optional, Tuple
 
 import torch
@@ -147,7 +148,22 @@ def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
 
     params = _named(named_params)
     tensors, meta = _read(path)
-    load_weights(path, params.items())
+    # Every check that can refuse the file runs BEFORE anything is overwritten,
+    # so a refused load leaves the model, optimizer and RNG untouched.
+    cuda_rng = []  # (device, key) pairs to restore
+    if rng and "rng.cpu" in tensors and torch.cuda.is_available():
+        local = sorted((int(k.rsplit(".", 1)[1]), k) for k in tensors if k.startswith("rng.cuda.local."))
+        if not local:  # files written before the device-independent keys: by saved index order
+            local = sorted((int(k.rsplit(".", 1)[1]), k) for k in tensors if k.startswith("rng.cuda."))
+        mine = _cuda_devices(params.values())
+        if local and not mine:
+            warnings.warn(f"{path}: the file holds GPU RNG states but this rank's parameters are on no GPU; "
+                          f"the GPU generators are left as they are")
+        elif len(local) != len(mine):
+            raise ValueError(f"{path}: RNG states for {len(local)} GPU(s), this rank's parameters are on "
+                             f"{len(mine)}")
+        else:
+            cuda_rng = [(d, key) for d, (_, key) in zip(mine, local)]
     opt_meta = meta.get("optimizer")
     if isinstance(optimizer, FlatAdam):
         if not opt_meta or opt_meta.get("kind") != "FlatAdam":
@@ -157,6 +173,15 @@ def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
         if layout != opt_meta["layout"]:
             raise ValueError(f"{path}: the optimizer's parameter layout differs from the saved one "
                              f"(a different partition or model)")
+    for n, p in params.items():
+        key = f"param.{n}"
+        if key not in tensors:
+            raise KeyError(f"{path}: no weights for {n!r}")
+        if tuple(tensors[key].shape) != tuple(p.shape):
+            raise ValueError(f"{path}: {n!r} is {tuple(tensors[key].shape)}, the model has {tuple(p.shape)}")
+    for n, p in params.items():
+        p.copy_(tensors[f"param.{n}"])
+    if isinstance(optimizer, FlatAdam):
         for gi, g in enumerate(optimizer.groups):
             g.master.copy_(tensors[f"flat.{gi}.master"])
             g.exp_avg.copy_(tensors[f"flat.{gi}.exp_avg"])
@@ -177,14 +202,6 @@ def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
             grp["lr"] = lr
     if rng and "rng.cpu" in tensors:
         torch.set_rng_state(tensors["rng.cpu"])
-        if torch.cuda.is_available():
-            local = sorted((int(k.rsplit(".", 1)[1]), k) for k in tensors if k.startswith("rng.cuda.local."))
-            if not local:  # files written before the device-independent keys: by saved index order
-                local = sorted((int(k.rsplit(".", 1)[1]), k) for k in tensors if k.startswith("rng.cuda."))
-            mine = _cuda_devices(params.values())
-            if len(local) != len(mine):
-                raise ValueError(f"{path}: RNG states for {len(local)} GPU(s), this rank's parameters are on "
-                                 f"{len(mine)}")
-            for d, (_, key) in zip(mine, local):
-                torch.cuda.set_rng_state(tensors[key], d)
+        for d, key in cuda_rng:
+            torch.cuda.set_rng_state(tensors[key], d)
     return {"step": meta.get("step", 0), "extra": meta.get("extra", {})}

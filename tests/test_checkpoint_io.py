@@ -124,3 +124,33 @@ def test_rng_restores_onto_loaders_own_gpu(tmp_path, monkeypatch):
     monkeypatch.setattr(cio, "_cuda_devices", lambda params: [4, 5])
     with pytest.raises(ValueError, match="RNG states for 1 GPU"):
         load_training_state(path, lin.named_parameters(), None)
+
+
+def test_refused_load_leaves_state_untouched(tmp_path, monkeypatch):
+    """every check that can refuse a file (RNG device count, optimizer
+    layout, weight shapes) runs before anything is overwritten; parameters on no
+    GPU skip the GPU generators with a warning instead of raising."""
+    import mipipe.utils.checkpoint_io as cio
+
+    lin = torch.nn.Linear(4, 4)
+    states = {0: torch.arange(16, dtype=torch.uint8)}
+    restored = {}
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "get_rng_state", lambda d: states[d].clone())
+    monkeypatch.setattr(torch.cuda, "set_rng_state", lambda st, d: restored.__setitem__(d, st.clone()))
+    monkeypatch.setattr(cio, "_cuda_devices", lambda params: [0])
+    path = rank_path(str(tmp_path), 0)
+    save_training_state(path, lin.named_parameters(), None)
+    other = torch.nn.Linear(4, 4)
+    before = [p.detach().clone() for p in other.parameters()]
+    cpu_before = torch.get_rng_state()
+    monkeypatch.setattr(cio, "_cuda_devices", lambda params: [0, 1])
+    with pytest.raises(ValueError, match="RNG states for 1 GPU"):
+        load_training_state(path, other.named_parameters(), None)
+    assert all(torch.equal(a, b) for a, b in zip(before, other.parameters()))
+    assert torch.equal(torch.get_rng_state(), cpu_before) and not restored
+    monkeypatch.setattr(cio, "_cuda_devices", lambda params: [])
+    with pytest.warns(UserWarning, match="no GPU"):
+        load_training_state(path, other.named_parameters(), None)
+    assert all(torch.equal(a, b) for a, b in zip(lin.parameters(), other.parameters()))
+    assert not restored

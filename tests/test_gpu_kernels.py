@@ -149,6 +149,19 @@ def test_cross_entropy(k, dtype, V, padded):
         assert base.grad[:, V:].abs().max().item() == 0.0
 
 
+def test_cross_entropy_out_of_range_target_is_loud(k):
+    """nn.CrossEntropyLoss raises on a target outside [0, V); the kernel mean
+    poisons the loss (NaN) instead of silently leaving the row out of the mean."""
+    from mipipe.ops import cross_entropy
+
+    logits = torch.randn(64, 1000, device=DEV)
+    t = torch.randint(0, 1000, (64,), device=DEV)
+    t[0] = -100  # ignored: fine
+    assert torch.isfinite(cross_entropy(logits, t)).item()
+    t[7] = 1000
+    assert torch.isnan(cross_entropy(logits, t)).item()
+
+
 # ------------------------------------------------------------------ embedding
 def test_embedding(k):
     from mipipe.models.lm import sinusoidal_positions
@@ -398,13 +411,17 @@ def test_gemm_layouts(k, a_kc, b_kc, M, N, K):
 @pytest.mark.parametrize("width", [256, 128])
 @pytest.mark.parametrize("sched", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_gemm_main_loop_schedules(k, sched, width):
-    """Every 256x256 main loop (per-tile barrier, ping-pong, the mixes, ping-pong with
-    the B lead) on every layout, for 1, 2, 3 and many K-tiles, edge tiles, K-segments
-    and the bf16 epilogue."""
+    """Every 256x256 main loop built in (the product build: the default whole-tile
+    ping-pong; a --gemm-ab build also the per-tile barrier, ping-pong, the mixes,
+    ping-pong with the B lead) on every layout, for 1, 2, 3 and many K-tiles, edge
+    tiles, K-segments and the bf16 epilogue."""
     from mipipe.ops import linear
 
+    if sched != 7 and not k.gemm_ab_build():
+        assert not k.gemm_set_schedule(sched)  # refused, not silently ignored
+        pytest.skip("A/B GEMM schedule not in the product build (python -m mipipe.build --gemm-ab)")
     old = k.gemm_get_schedule()
-    k.gemm_set_schedule(sched)
+    assert k.gemm_set_schedule(sched)
     k.gemm_set_width(width)
     try:
         torch.manual_seed(7)
@@ -444,8 +461,10 @@ def test_wgrad_segments_fused_bias(k, sched):
     (GemmArgs::rowsum): equal to the column sums of every dY, accumulated; a
     shape that cannot take the fold (< 16 tile columns, or split-K) returns
     False and leaves the bias gradient alone."""
+    if sched != 7 and not k.gemm_ab_build():
+        pytest.skip("A/B GEMM schedule not in the product build (python -m mipipe.build --gemm-ab)")
     old = k.gemm_get_schedule()
-    k.gemm_set_schedule(sched)
+    assert k.gemm_set_schedule(sched)
     try:
         torch.manual_seed(11)
         for N, Kin, T, nseg in [(520, 4096, 256, 3), (1000, 4104, 128, 18), (256, 512, 128, 2), (1024, 4096, 1024, 16)]:
