@@ -300,6 +300,7 @@ def main() -> int:
         dist.broadcast(lt, src=world - 1)
         loss_val = float(lt.item())
 
+    comm = _comm_report(engine, device, world, local, on_gpu)
     armed.__exit__(None, None, None)
     if wd is not None:
         wd.close()
@@ -358,12 +359,55 @@ def main() -> int:
             "loss": loss_val,
             "peak_hbm_gib_per_gpu": [round(x, 2) for x in peaks] if on_gpu else None,
             "baseline_note": _baseline_note(ref_match, args.checkpoint),
+            "comm": comm,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _comm_report(engine, device, world, local, on_gpu):
+    """What the job's communicators actually are, for a multi-GPU run to be
+    checked against its own JSON: the default group's backend and size, the
+    RCCL version, and per rank its device (index, PCI bus, UUID) and every
+    pipeline channel it owns as its communicator reports it (backend,
+    ``get_world_size``, whether the warm-up exchanged over it).  Collective."""
+    me = {"rank": dist.get_rank() if world > 1 else 0, "local_rank": local, "device": str(device)}
+    if on_gpu:
+        props = torch.cuda.get_device_properties(device)
+        me.update(device_index=device.index, pci_bus_id=int(getattr(props, "pci_bus_id", -1)),
+                  uuid=str(getattr(props, "uuid", "")))
+    chan = getattr(engine, "chan", None)
+    if chan is not None and hasattr(chan, "comm_info"):
+        me["channels"] = chan.comm_info()
+        me["warmup_s"] = None if getattr(chan, "warmup_s", None) is None else round(chan.warmup_s, 3)
+    else:
+        me["channels"] = []
+    ranks = [me]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    rccl = None
+    try:
+        import torch.cuda.nccl as _nccl
+
+        rccl = ".".join(str(x) for x in _nccl.version())
+    except Exception:
+        pass
+    links = {c["dir"] for r in ranks for c in r["channels"]}
+    warmed = {c["dir"] for r in ranks for c in r["channels"] if c["warmed"]}
+    return {
+        "backend": str(dist.get_backend()) if world > 1 else None,
+        "world_size": dist.get_world_size() if world > 1 else 1,
+        "rccl_version": rccl,
+        "hip_version": torch.version.hip,
+        "pipeline_links": len(links),
+        "pipeline_links_warmed": len(warmed),
+        "distinct_devices": len({(r.get("pci_bus_id"), r.get("uuid")) for r in ranks}) if on_gpu else None,
+        "per_rank": ranks,
+    }
 
 
 def run_pipe(args) -> int:

@@ -550,10 +550,14 @@ bool py_gemm_supported(int64_t M, int64_t N, int64_t K) { return gemm_supported(
 bool py_gemm_f32_supported(int64_t M, int64_t N, int64_t K) { return gemm_f32_supported(M, N, K); }
 
 // y[M,N] = act(x[M,K] . w[N,K]^T + bias) with dropout; optional pre-activation.
+// xt (optional, bf16 [K, M]): also written with x^T by the same GEMM (its
+// blocks transpose the x tiles they stage anyway), the K-contiguous operand of
+// the layer's transposed weight-gradient GEMM (linear_wgrad_xt_segments).
 std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor x, Tensor w,
                                                                            std::optional<Tensor> bias, int64_t act,
                                                                            double p, bool save_preact,
-                                                                           std::optional<Tensor> res) {
+                                                                           std::optional<Tensor> res,
+                                                                           std::optional<Tensor> xt) {
   check_gemm_2d(x, "x");
   check_gemm_2d(w, "w");
   check_same_dtype(x, w, "linear_fwd");
@@ -587,6 +591,13 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   g.lda = row_stride(x, "x"); g.ldb = row_stride(w, "w"); g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreAct; g.act = (int)act; g.p = (float)p;
   g.seed = seed; g.offset = offset;
+  if (xt) {
+    check_gemm_2d(*xt, "xt");
+    MP_CHECK(dt == at::kBFloat16 && xt->scalar_type() == dt && xt->size(0) == K && xt->size(1) == M,
+             "linear_fwd: xt must be bf16 [K, M]");
+    g.at = xt->data_ptr();
+    g.ldat = row_stride(*xt, "xt");
+  }
   gemm_run(dt, g, cur_stream(x));
   return {y, pre, (int64_t)seed, (int64_t)offset};
 }
@@ -800,6 +811,68 @@ bool py_linear_wgrad_segments(std::vector<Tensor> dys, std::vector<Tensor> xs, T
     if (fold) g.rowsum = bias_grad->data_ptr<float>();
     Tensor ws = split_k_workspace(g, dt, main_grad);
     gemm_run(dt, g, cur_stream(main_grad));
+  }
+  return fold;
+}
+
+// The same deferred weight gradient from the transposed inputs x_i^T [K, T]
+// (written by the forward GEMMs, linear_fwd(xt=...)):
+//   main_grad[N, K] += sum_i (x_i^T . dy_i)^T
+// computed as C^T[K, N] with A = x^T read K-contiguous and B = dy read [T, N]
+// -- the dgrad layout, one transposing LDS read per operand instead of two
+// (profiles/wgrad_layout_probe.txt) -- and stored transposed into main_grad.
+// bias_grad: colsum(dy) folded into the same GEMMs (GemmArgs::colsum) when
+// the shape allows (returns whether it was).
+bool py_linear_wgrad_xt_segments(std::vector<Tensor> dys, std::vector<Tensor> xts, Tensor main_grad,
+                                 bool accumulate, std::optional<Tensor> bias_grad) {
+  MP_CHECK(!dys.empty() && dys.size() == xts.size(), "linear_wgrad_xt_segments: need matching non-empty lists");
+  check_cuda(main_grad, "main_grad");
+  const int64_t T = dys[0].size(0), N = dys[0].size(1), K = xts[0].size(0);
+  MP_CHECK(main_grad.scalar_type() == at::kFloat && main_grad.numel() == N * K && main_grad.is_contiguous(),
+           "linear_wgrad_xt_segments: bad main_grad");
+  for (size_t i = 0; i < dys.size(); ++i) {
+    check_gemm_2d(dys[i], "dy");
+    check_gemm_2d(xts[i], "xt");
+    MP_CHECK(dys[i].scalar_type() == at::kBFloat16 && xts[i].scalar_type() == at::kBFloat16,
+             "linear_wgrad_xt_segments: bf16 operands only");
+    MP_CHECK(dys[i].size(0) == T && dys[i].size(1) == N && xts[i].size(0) == K && xts[i].size(1) == T,
+             "linear_wgrad_xt_segments: every micro-batch needs dy [T, N] and xt [K, T]");
+  }
+  MP_CHECK(T % 64 == 0 && K % 8 == 0 && gemm_supported(K, N, T), "linear_wgrad_xt_segments: unsupported shape");
+  const int64_t lda = row_stride(xts[0], "xt"), ldb = row_stride(dys[0], "dy");
+  for (size_t i = 1; i < dys.size(); ++i)
+    MP_CHECK(row_stride(dys[i], "dy") == ldb && row_stride(xts[i], "xt") == lda,
+             "linear_wgrad_xt_segments: every micro-batch needs the same row strides");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(main_grad.device());
+  const int total = (int)dys.size();
+  auto args_for = [&](int first) {
+    const int n = std::min(GemmArgs::kMaxSegs, total - first);
+    GemmArgs g;
+    g.C = main_grad.data_ptr();
+    g.lda = lda; g.ldb = ldb; g.ldc = K; g.M = (int)K; g.N = (int)N; g.K = (int)(T * n);
+    g.a_kc = true; g.b_kc = false; g.trans_c = true;
+    g.epi = (accumulate || first > 0) ? kEpiAccumF32 : kEpiStoreF32;
+    g.seg_k = (int)T;
+    for (int i = 0; i < n; ++i) {
+      g.a_seg[i] = xts[first + i].data_ptr();
+      g.b_seg[i] = dys[first + i].data_ptr();
+    }
+    g.A = g.a_seg[0]; g.B = g.b_seg[0];
+    return g;
+  };
+  bool fold = false;
+  if (bias_grad) {
+    check_cuda(*bias_grad, "bias_grad");
+    MP_CHECK(bias_grad->scalar_type() == at::kFloat && bias_grad->numel() == N && bias_grad->is_contiguous(),
+             "linear_wgrad_xt_segments: bias_grad must be a contiguous fp32 [N]");
+    fold = true;
+    for (int first = 0; first < total && fold; first += GemmArgs::kMaxSegs) fold = gemm_colsum_ok(args_for(first));
+  }
+  for (int first = 0; first < total; first += GemmArgs::kMaxSegs) {
+    GemmArgs g = args_for(first);
+    if (fold) g.colsum = bias_grad->data_ptr<float>();
+    Tensor ws = split_k_workspace(g, at::kBFloat16, main_grad);
+    gemm_bf16(g, cur_stream(main_grad));
   }
   return fold;
 }
@@ -1104,7 +1177,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_rounds", &gemm_set_rounds, "1: launch multi-round GEMM grids one round of tiles at a time (default)");
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
-        py::arg("save_preact"), py::arg("res") = py::none());
+        py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none());
+  m.def("linear_wgrad_xt_segments", &py_linear_wgrad_xt_segments, py::arg("dys"), py::arg("xts"),
+        py::arg("main_grad"), py::arg("accumulate") = true, py::arg("bias_grad") = py::none());
   m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none(),
         py::arg("out") = py::none(), py::arg("act") = 0, py::arg("saved") = py::none(), py::arg("p") = 0.0,
         py::arg("seed") = 0, py::arg("offset") = 0);

@@ -441,7 +441,8 @@ template <int EPI, int W>
 __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W / 64], int wm, int wn, int lane,
                                              int tid, int m0, int n0, int M, int N, int64_t ldc, void* out,
                                              const bf16_t* res, int64_t ldr = 0, const bf16_t* dact_in = nullptr,
-                                             int64_t ldd = 0, int dact = 0, float dact_scale = 1.f) {
+                                             int64_t ldd = 0, int dact = 0, float dact_scale = 1.f,
+                                             bool trans = false) {
   constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512;
   const int quad = lane >> 4, col_in = lane & 15;
   float* stg = reinterpret_cast<float*>(smem);
@@ -484,6 +485,26 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
         *reinterpret_cast<bf16x8*>(C + at) = o;
+      }
+    } else if (trans) {
+      // C^T: element (row m, col n) to C[n * ldc + m].  Item (mq, n): rows
+      // 4 mq .. 4 mq + 3 of column n, one 16-byte store; 8 consecutive items
+      // are 8 row quads of one column (128 contiguous output bytes).
+      float* C = reinterpret_cast<float*>(out);
+#pragma unroll 4
+      for (int u = 0; u < 32 * W / kT; ++u) {
+        const int idx = tid + u * kT;
+        const int mq = (idx & 7) + 8 * (idx / (8 * W)), n = (idx >> 3) % W;
+        if (rbase + 4 * mq >= M || n0 + n >= N) continue;
+        const float* sp = stg + 4 * mq * kStride + n;
+        const float4 v = make_float4(sp[0], sp[kStride], sp[2 * kStride], sp[3 * kStride]);
+        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(n0 + n) * ldc + rbase + 4 * mq);
+        if (EPI == kEpiAccumF32) {
+          const float4 o = *dst;
+          *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        } else {
+          *dst = v;
+        }
       }
     } else {
       float* C = reinterpret_cast<float*>(out);
@@ -566,7 +587,12 @@ int gemm_sched() {
 // pre-activation (otherwise it is branch-free bias + activation).
 // PP: 0 = one barrier per K-tile, 1 = ping-pong, 2 = ping-pong with the B
 // operand staged two K-tiles ahead (below).
-template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA>
+// X: main-loop extras, 0 none, kXEmit the A^T emission (GemmArgs::at), kXColsum
+// the B-side bias fold (GemmArgs::colsum) -- separate instantiations, so the
+// plain kernels keep their register allocation.
+constexpr int kXEmit = 1, kXColsum = 2;
+
+template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA, int X = 0>
 __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   constexpr int NJ = W / 64;          // 16-wide MFMA column tiles per wave
   constexpr int JJ = NJ / 2;          // ... per ping-pong quadrant
@@ -597,6 +623,46 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       const s16x4 v = *reinterpret_cast<const s16x4*>(tile + ic_off_w<256>(r, c8));
 #pragma unroll
       for (int e = 0; e < 4; ++e) rs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+    }
+  };
+  // fused bias gradient on the B side (GemmArgs::colsum): group-0 thread t
+  // sums the 4 columns [16 tm + 4 (t & 3), +4) of K-row t >> 2 of every B tile
+  const bool csum = X == kXColsum && !B_KC && g.colsum != nullptr && tm < W / 16;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto colsum_step = [&](const char* btile) {
+    if (csum && wm == 0) {
+      const int r = tid >> 2, c8 = 4 * tm + (tid & 3);
+      const s16x4 v = *reinterpret_cast<const s16x4*>(btile + ic_off_w<W>(r, c8));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+    }
+  };
+  // A^T emission (GemmArgs::at, K-contiguous A): piece j of this wave covers
+  // tile rows [8 (4 wave + j), +8) x K columns [16 g, +16) (g = lane >> 4); a
+  // 16-lane group's two transposing reads give lane i the 8 rows of column
+  // 16 g + i, stored as one 16-byte chunk of at[k][m].
+  // Addresses are recomputed per emitting tile (1 in tiles_n of them) rather
+  // than held in registers across the main loop.
+  const int ntn = (g.N + W - 1) / W;
+  s16x4 ev[8];
+  auto emit_reads = [&](const char* atile) {
+    const int q = (lane & 15) >> 2, p = lane & 3, gq = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 8 * (4 * wave + j) + q, c16 = 2 * gq + (p >> 1);
+      const int lo = r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4) + 8 * (p & 1);
+      const int hi = (r + 4) * 128 + ((c16 ^ (((r + 4) >> 1) & 7)) << 4) + 8 * (p & 1);
+      ev[2 * j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(atile + lo));
+      ev[2 * j + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(atile + hi));
+    }
+  };
+  auto emit_stores = [&](int kt) {
+    bf16_t* at = reinterpret_cast<bf16_t*>(g.at) + (int64_t)(kt * BK + 16 * (lane >> 4) + (lane & 15)) * g.ldat + m0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rb = 4 * wave + j;
+      if (m0 + 8 * rb < g.M)
+        *reinterpret_cast<s16x8*>(at + 8 * rb) = __builtin_shufflevector(ev[2 * j], ev[2 * j + 1], 0, 1, 2, 3, 4, 5, 6, 7);
     }
   };
   int kt0 = 0, nk = g.K / BK;
@@ -654,9 +720,17 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     __builtin_amdgcn_s_barrier();
     if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
     bf16x8 af[8][2], bq[NJ][2];
+    int ekt = kt0 % ntn;  // (kt0 + u) mod tiles_n: this block emits A^T of K-tile kt0 + u when it equals tn
     for (int u = 0; u < nk; ++u) {
       char* cur = smem + (u & 1) * kBuf;
       char* nxt = smem + ((u + 1) & 1) * kBuf;
+      // emission first: its reads precede this wave's DMA that may restage
+      // `cur`, and its stores (waiting for those reads) precede the fragment
+      // reads, so its 16 data registers are dead before the fragments load
+      if (X == kXEmit && A_KC && ekt == tn) {
+        emit_reads(cur);
+        emit_stores(kt0 + u);
+      }
 #pragma unroll
       for (int ii = 0; ii < 8; ++ii)
 #pragma unroll
@@ -666,6 +740,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) bq[j][s] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * j, s, lane);
       rowsum_step(cur);
+      colsum_step(cur + kTileBytes);
+      ekt = ekt + 1 == ntn ? 0 : ekt + 1;
       const int ahead = wm == 0 ? 1 : 2;  // the tile this group stages now
       if (u + ahead < nk) {
         int kl;
@@ -911,6 +987,25 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       if (row < g.M) g.rowsum[row] += v;
     }
   }
+  if (csum) {  // the same reduction for the B-side column sums
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem) + 64;
+    if (wm == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = 4; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
+      if (lane < 4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[wave * 16 + 4 * lane + e] = cs[e];
+    }
+    __syncthreads();
+    if (tid < 16) {
+      const float v = red[tid] + red[16 + tid] + red[32 + tid] + red[48 + tid];
+      const int col = n0 + 16 * tm + tid;
+      if (col < g.N) g.colsum[col] += v;
+    }
+  }
   // ---- epilogue ----
   // 1) element-wise epilogue in registers (accumulator layout): bias,
   //    activation, dropout (the mask is tied to this layout); with an aux
@@ -957,6 +1052,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
                          reinterpret_cast<const bf16_t*>(g.res), g.ldr, reinterpret_cast<const bf16_t*>(g.dact_in),
                          g.ldd, g.dact, g.dact_scale);
+  else if (EPI != kEpiStoreBf16 && g.trans_c && g.k_splits <= 1)
+    staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out, nullptr, 0, nullptr, 0, 0, 1.f,
+                         true);
   else
     staged_store<EPI, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
                          EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
@@ -973,7 +1071,8 @@ int big_tiles(const GemmArgs& g, int w) { return ((g.M + big::BM - 1) / big::BM)
 // GPT-2-XL's fc1 forward (18432 x 6400, 7 rounds + 2 tile rows) ran on the
 // 128x128 kernel at ~250 TF/s.
 bool use_big(const GemmArgs& g) {
-  return g.round_chunk || g.seg_k > 0 || g.M % BM != 0 || g.N % BN != 0 || big_tiles(g, 256) >= 128;
+  return g.round_chunk || g.seg_k > 0 || g.at != nullptr || g.trans_c || g.colsum != nullptr || g.rowsum != nullptr ||
+         g.M % BM != 0 || g.N % BN != 0 || big_tiles(g, 256) >= 128;
 }
 
 // Block width of the 256-row kernel: 256, or 128 when the grid of 256x256
@@ -997,15 +1096,16 @@ int big_width(const GemmArgs& g) {
   return 0.75 * r128 < 1.0 * r256 ? 128 : 256;
 }
 
-template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA>
+template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA, int X = 0>
 void launch_big(const GemmArgs& g, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA, X>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
     attr_set = true;
   }
-  hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA>), dim3(big_tiles(g, W), g.k_splits),
+  hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA, X>), dim3(big_tiles(g, W), g.k_splits),
                      dim3(big::kThreads), big::kSmemBytes, s, g);
 }
 
@@ -1016,6 +1116,20 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
   const bool narrow = big_width(g) == 128;
+  if constexpr (A_KC && B_KC && EPI == kEpiStoreBf16) {
+    if (g.at != nullptr) {  // forward GEMM that also writes A^T
+      if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA, big::kXEmit>(g, s);
+      else launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA, big::kXEmit>(g, s);
+      return;
+    }
+  }
+  if constexpr (A_KC && !B_KC && EPI != kEpiStoreBf16 && !EXTRA) {
+    if (g.colsum != nullptr) {  // transposed weight gradient with the bias fold
+      if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA, big::kXColsum>(g, s);
+      else launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA, big::kXColsum>(g, s);
+      return;
+    }
+  }
 #ifndef MIPIPE_GEMM_AB
   if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA>(g, s);
   else launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA>(g, s);
@@ -1092,10 +1206,27 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 
 // C[M, N] (fp32, row stride ldc) (+)= sum of the k_splits fp32 partials: the
 // split-K reduction of a weight gradient (accumulate: into main_grad).
+// trans: C[n * ldc + m] (+)= the partials' (m, n) -- a thread reduces rows
+// 4 m' .. 4 m' + 3 of one column n (consecutive threads: consecutive n, so the
+// partials are read in coalesced rows) and writes them as one 16-byte chunk.
 __global__ void __launch_bounds__(256) splitk_reduce_f32_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                                                int64_t ldc, bool accumulate, float* __restrict__ C) {
-  const int64_t chunks = (int64_t)M * (N / 4);
+                                                                int64_t ldc, bool accumulate, bool trans,
+                                                                float* __restrict__ C) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (trans) {
+    if (c >= (int64_t)(M / 4) * N) return;
+    const int m = (int)(c / N) * 4, n = (int)(c % N);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < splits; ++s) {
+      const float* p = ws + (int64_t)s * M * N + (int64_t)m * N + n;
+      v += f32x4{p[0], p[N], p[2 * (int64_t)N], p[3 * (int64_t)N]};
+    }
+    f32x4* dst = reinterpret_cast<f32x4*>(C + (int64_t)n * ldc + m);
+    if (accumulate) v += *dst;
+    *dst = v;
+    return;
+  }
+  const int64_t chunks = (int64_t)M * (N / 4);
   if (c >= chunks) return;
   const int row = (int)(c / (N / 4)), col = (int)(c % (N / 4)) * 4;
   const int64_t at = (int64_t)row * N + col;
@@ -1142,6 +1273,14 @@ int gemm_get_schedule() { return big::gemm_sched(); }
 bool gemm_rowsum_ok(const GemmArgs& g) {
   return !g.a_kc && (g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32) && use_big(g) && gemm_splitk_factor(g) <= 1 &&
          (g.N + big_width(g) - 1) / big_width(g) >= 16;
+}
+
+bool gemm_colsum_ok(const GemmArgs& g) {
+  if (g.b_kc || !(g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32) || gemm_splitk_factor(g) > 1) return false;
+  GemmArgs b = g;
+  b.colsum = reinterpret_cast<float*>(1);  // as launched: on the 256-row kernel
+  const int w = big_width(b);
+  return (g.M + big::BM - 1) / big::BM >= w / 16;
 }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
@@ -1212,6 +1351,7 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
   if (tm * tn <= 256 || (tm * tn) % 256 == 0 || (tm * tn) % 256 > 128) return false;
   const bool along_n = tn >= tm;
   if (along_n && g.rowsum != nullptr) return false;  // the row slices need every tile column of a tile row
+  if (!along_n && g.colsum != nullptr) return false;  // the column slices need every tile row of a tile column
   const int other = along_n ? tm : tn, along = along_n ? tn : tm;
   const int per = 256 / other;  // tiles of the split dimension per launch
   if (per < 1 || (along + per - 1) / per > 16) return false;
@@ -1228,7 +1368,9 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
       const int64_t boff = (g.b_kc ? (int64_t)lo * g.ldb : (int64_t)lo) * 2;
       c.B = byte_off(g.B, boff);
       for (int i = 0; i < GemmArgs::kMaxSegs; ++i) c.b_seg[i] = byte_off(g.b_seg[i], boff);
-      c.C = const_cast<char*>(byte_off(g.C, (int64_t)lo * cbytes));
+      c.C = const_cast<char*>(byte_off(g.C, (g.trans_c ? (int64_t)lo * g.ldc : (int64_t)lo) * cbytes));
+      if (g.colsum != nullptr) c.colsum = g.colsum + lo;
+      if (t0 > 0) c.at = nullptr;  // every chunk holds the whole A: the first one emits A^T
       c.bias = byte_off(g.bias, (int64_t)lo * 2);
       c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * 2));
       c.res = byte_off(g.res, (int64_t)lo * 2);
@@ -1240,7 +1382,8 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
       const int64_t aoff = (g.a_kc ? (int64_t)lo * g.lda : (int64_t)lo) * 2;
       c.A = byte_off(g.A, aoff);
       for (int i = 0; i < GemmArgs::kMaxSegs; ++i) c.a_seg[i] = byte_off(g.a_seg[i], aoff);
-      c.C = const_cast<char*>(byte_off(g.C, (int64_t)lo * g.ldc * cbytes));
+      c.C = const_cast<char*>(byte_off(g.C, (g.trans_c ? (int64_t)lo : (int64_t)lo * g.ldc) * cbytes));
+      c.at = const_cast<char*>(byte_off(g.at, (int64_t)lo * 2));  // A^T columns of this chunk's rows
       c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * g.ldc * 2));
       c.res = byte_off(g.res, (int64_t)lo * g.ldr * 2);
       c.dact_in = byte_off(g.dact_in, (int64_t)lo * g.ldd * 2);
@@ -1262,6 +1405,8 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
     p.C = g.ws;
     p.ldc = g.N;
     p.res = nullptr;
+    p.trans_c = false;  // partials row-major; the reduction transposes
+    p.rowsum = p.colsum = nullptr;
     if (p.a_kc && p.b_kc) launch<true, true, kEpiStoreF32, kActNone>(p, s);
     else if (p.a_kc && !p.b_kc) launch<true, false, kEpiStoreF32, kActNone>(p, s);
     else if (!p.a_kc && !p.b_kc) launch<false, false, kEpiStoreF32, kActNone>(p, s);
@@ -1272,9 +1417,10 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
                          g.k_splits, g.M, g.N, g.ldc, reinterpret_cast<const bf16_t*>(g.res), g.ldr,
                          reinterpret_cast<bf16_t*>(g.C));
     } else {
-      const int64_t chunks = (int64_t)g.M * (g.N / 4);
+      const int64_t chunks = (int64_t)g.M * (g.N / 4);  // = (M / 4) * N items when transposed
       hipLaunchKernelGGL(splitk_reduce_f32_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws,
-                         g.k_splits, g.M, g.N, g.ldc, g.epi == kEpiAccumF32, reinterpret_cast<float*>(g.C));
+                         g.k_splits, g.M, g.N, g.ldc, g.epi == kEpiAccumF32, g.trans_c,
+                         reinterpret_cast<float*>(g.C));
     }
     return;
   }

@@ -140,12 +140,30 @@ struct GemmArgs {
   // over the whole K (one writer per row: deterministic).  Needs
   // ceil(N / block width) >= 16 and k_splits == 1 (gemm_rowsum_ok).
   float* rowsum = nullptr;
+  // The same fold on the B side for the transposed weight-gradient GEMM
+  // (C^T = X^T . dY, B = dY read as [K=T, N]): colsum[n] += sum_k B[k][n];
+  // blocks tm = 0 .. W/16-1 of a tile column sum 16 columns each
+  // (gemm_colsum_ok: >= W/16 tile rows, no split-K).
+  float* colsum = nullptr;
+  // Transposed fp32 output (kEpiAccumF32 / kEpiStoreF32): element (m, n) of
+  // the product goes to C[n * ldc + m] -- the weight gradient dW = (X^T dY)^T
+  // lands in main_grad's [N_out, K_in] layout.
+  bool trans_c = false;
+  // A^T emission (forward GEMMs, A K-contiguous): the block whose tile column
+  // tn equals kt mod (tile columns) also writes K-tile kt of its A tile
+  // transposed, at[k][m] (bf16, row stride ldat, 16-byte aligned, m < M), from
+  // the LDS image it computes from: X^T for the layer's weight-gradient GEMM
+  // without a transposition pass (tools/wgrad_layout_probe.py).
+  void* at = nullptr;
+  int64_t ldat = 0;
   const void* a_seg[kMaxSegs] = {};
   const void* b_seg[kMaxSegs] = {};
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 // True if gemm_bf16 can fold g.rowsum into g (the wgrad layout, no split-K, >= 16 tile columns).
 bool gemm_rowsum_ok(const GemmArgs& g);
+// True if gemm_bf16 can fold g.colsum into g (B I-contiguous, fp32 out, no split-K, >= W/16 tile rows).
+bool gemm_colsum_ok(const GemmArgs& g);
 // Split-K factor gemm_bf16 would use for g (1 = none); the caller provides
 // g.ws with k_splits * M * N floats when it is > 1.
 int gemm_splitk_factor(const GemmArgs& g);

@@ -166,7 +166,7 @@ class _Linear(torch.autograd.Function):
         w = weight.contiguous()
         fused_tile = _tile_ok(k, x2, w)
         seed = offset = 0
-        preact = None
+        preact = xt = None
         ctx.has_res = res is not None
         if fused_tile:
             r2 = None
@@ -176,8 +176,14 @@ class _Linear(torch.autograd.Function):
                     r2 = r2.to(x2.dtype).contiguous()
                     if not _aligned(r2):
                         r2 = r2.clone()
+            # x^T for the transposed weight-gradient GEMM, written by this GEMM
+            # (GemmArgs::at): only when a backward will want this weight's
+            # gradient in a flat-optimizer main_grad
+            if (save and _EMIT_XT and x2.dtype == torch.bfloat16 and ctx.needs_input_grad[1]
+                    and getattr(weight, "main_grad", None) is not None):
+                xt = torch.empty((x2.shape[1], x2.shape[0]), dtype=x2.dtype, device=x2.device)
             # GELU's pre-activation is written only for a backward (not under no_grad)
-            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2)
+            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2, xt)
             res = None  # added in the epilogue
         else:
             y = torch.matmul(x2, w.t())
@@ -202,7 +208,9 @@ class _Linear(torch.autograd.Function):
             fold_saved = fold_in.saved
         if fold_in is not None:
             fold_in.saved = None
-        ctx.save_for_backward(x2, w, bias, saved, fold_saved)
+        # x is kept for the weight gradient only: x^T replaces it when written
+        ctx.x_is_t = xt is not None
+        ctx.save_for_backward(xt if xt is not None else x2, w, bias, saved, fold_saved)
         ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
         ctx.fused_tile = fused_tile
         ctx.in_shape = shape
@@ -270,7 +278,12 @@ class _Linear(torch.autograd.Function):
                 dx = dx + dres
 
         dw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and ctx.x_is_t:  # x2 holds x^T [K, T]
+            if _DEFERRED is not None:
+                _defer(w, dpre, x2, True)
+            else:
+                k.linear_wgrad_xt_segments([dpre], [x2], w.main_grad, _claim(w))
+        elif ctx.needs_input_grad[1]:
             main = getattr(w, "main_grad", None)
             if main is not None and ctx.fused_tile and _DEFERRED is not None:
                 _defer(w, dpre, x2)
@@ -297,17 +310,23 @@ _DEFERRED: Optional[dict] = None
 # Bias gradients folded into the weight-gradient GEMMs of the flush
 # (MIPIPE_FUSE_BIAS=0: separate column-sum kernels, for A/B runs).
 _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
+# Forward GEMMs write x^T for the transposed weight-gradient GEMM
+# (MIPIPE_WGRAD_XT=0: keep x and run the weight gradient with both operands
+# read I-contiguous, for A/B runs).
+_EMIT_XT = os.environ.get("MIPIPE_WGRAD_XT", "1") != "0"
 
 
-def _defer(w: Tensor, dy: Tensor, x: Tensor) -> None:
-    entry = _DEFERRED.setdefault(id(w), (w, [], []))
+def _defer(w: Tensor, dy: Tensor, x: Tensor, transposed: bool = False) -> None:
+    """Queues (dY, X) -- or (dY, X^T) when ``transposed`` -- for ``w``."""
+    entry = _DEFERRED.setdefault(id(w), (w, [], [], []))
     entry[1].append(dy)
     entry[2].append(x)
+    entry[3].append(transposed)
 
 
 def _defer_bias(b: Tensor, dy: Tensor) -> None:
     """Bias gradients: column sums of every queued dY, ONE reduction per bias."""
-    entry = _DEFERRED.setdefault(id(b), (b, [], None))
+    entry = _DEFERRED.setdefault(id(b), (b, [], None, None))
     entry[1].append(dy)
 
 
@@ -356,17 +375,17 @@ def flush_wgrad() -> None:
     queue, _DEFERRED = _DEFERRED, {}
     listeners = list(_WGRAD_LISTENERS)
     for li in listeners:
-        li.flush_begin([w for w, _, _ in queue.values()])
+        li.flush_begin([e[0] for e in queue.values()])
     # A bias queued with the very dY tensors of a weight (one Linear) has its
-    # column sums folded into that weight's GEMMs (GemmArgs::rowsum) when the
-    # shape allows; it is reduced when its weight is processed.
-    weight_dys = {tuple(id(d) for d in dys) for _, dys, xs in queue.values() if xs is not None}
+    # column sums folded into that weight's GEMMs (GemmArgs::rowsum / colsum)
+    # when the shape allows; it is reduced when its weight is processed.
+    weight_dys = {tuple(id(d) for d in e[1]) for e in queue.values() if e[2] is not None}
     bias_of = {}
-    for b, dys, xs in queue.values():
+    for b, dys, xs, _ in queue.values():
         key = tuple(id(d) for d in dys)
         if xs is None and key in weight_dys:
             bias_of[key] = b
-    for w, dys, xs in queue.values():
+    for w, dys, xs, trans in queue.values():
         key = tuple(id(d) for d in dys)
         if xs is None and bias_of.get(key) is w:
             continue  # with its weight
@@ -379,16 +398,7 @@ def flush_wgrad() -> None:
                 k.column_sum_segments(dys, w.main_grad, True)
             else:
                 b = bias_of.get(key)
-                fused = False
-                T = dys[0].shape[0]
-                uniform = (all(d.shape == dys[0].shape and d.stride() == dys[0].stride() for d in dys)
-                           and all(x.shape == xs[0].shape and x.stride() == xs[0].stride() for x in xs))
-                if uniform and T % 64 == 0:
-                    fused = k.linear_wgrad_segments(dys, xs, w.main_grad, _claim(w),
-                                                    b.main_grad if (b is not None and _FUSE_BIAS) else None)
-                else:
-                    for d, x in zip(dys, xs):
-                        k.linear_wgrad(d, x, w.main_grad, _claim(w))
+                fused = _flush_weight(k, w, dys, xs, trans, b.main_grad if (b is not None and _FUSE_BIAS) else None)
                 if b is not None:
                     if not fused:
                         k.column_sum_segments(dys, b.main_grad, True)
@@ -396,6 +406,38 @@ def flush_wgrad() -> None:
         for li in listeners:
             for p in done:
                 li.wgrad_done(p)
+
+
+def _uniform(ts) -> bool:
+    return all(t.shape == ts[0].shape and t.stride() == ts[0].stride() for t in ts)
+
+
+def _flush_weight(k, w: Tensor, dys, xs, trans, bias_main: Optional[Tensor]) -> bool:
+    """One weight's queued gradients: the transposed K-segmented GEMM over the
+    micro-batches that saved x^T, the plain one over those that saved x (a
+    queue may mix them, e.g. a tensor that bypassed the tile path).  Returns
+    whether ``bias_main`` received the bias gradient (folded into a GEMM)."""
+    t_idx = [i for i, t in enumerate(trans) if t]
+    x_idx = [i for i, t in enumerate(trans) if not t]
+    T = dys[0].shape[0]
+    fused = False
+    if t_idx:
+        tdys, txts = [dys[i] for i in t_idx], [xs[i] for i in t_idx]
+        if _uniform(tdys) and _uniform(txts) and T % 64 == 0:
+            fused = k.linear_wgrad_xt_segments(tdys, txts, w.main_grad, _claim(w),
+                                               bias_main if not x_idx else None)
+        else:
+            for d, xt in zip(tdys, txts):
+                k.linear_wgrad_xt_segments([d], [xt], w.main_grad, _claim(w))
+    if x_idx:
+        pdys, pxs = [dys[i] for i in x_idx], [xs[i] for i in x_idx]
+        if _uniform(pdys) and _uniform(pxs) and T % 64 == 0:
+            fused = k.linear_wgrad_segments(pdys, pxs, w.main_grad, _claim(w),
+                                            bias_main if not t_idx else None)
+        else:
+            for d, x in zip(pdys, pxs):
+                k.linear_wgrad(d, x, w.main_grad, _claim(w))
+    return fused
 
 
 def begin_deferred_wgrad() -> bool:

@@ -152,6 +152,7 @@ class Channels:
             a, b = self.ranks[r], self.ranks[(r + 1) % n]
             bwd[r] = (dist.new_group([a, b]) if n > 1 else None, b, a)  # gradients b -> a
         self._fwd, self._bwd = fwd, bwd
+        self.warmed = set()
 
     def warmup(self, device: torch.device) -> None:
         """Creates every channel's communicator up front.
@@ -162,8 +163,11 @@ class Channels:
         wait on a send that can never happen.  Here every link does one tiny
         blocking exchange, links visited in the same global order on every
         rank (a chain of pairwise rendezvous: always deadlock-free)."""
+        import time
+
         dev = torch.device("cpu") if self.host_staged else device
         me = dist.get_rank()
+        t0 = time.perf_counter()
         for table in (self._fwd, self._bwd):
             for r in sorted(table):
                 group, src, dst = table[r]
@@ -171,6 +175,29 @@ class Channels:
                     dist.send(torch.zeros(1, device=dev), dst, group=group)
                 elif me == dst:
                     dist.recv(torch.zeros(1, device=dev), src, group=group)
+                else:
+                    continue
+                self.warmed.add((table is self._fwd, r))
+        self.warmup_s = time.perf_counter() - t0
+
+    warmed: set = frozenset()  # (is_activation_link, link index) this rank exchanged over in warmup()
+    warmup_s = None
+
+    def comm_info(self) -> List[dict]:
+        """This rank's channels as the communicators report them: direction,
+        global (src, dst), the group's backend and ``get_world_size`` (2 for a
+        live pair communicator), whether :meth:`warmup` exchanged over it."""
+        me = dist.get_rank()
+        out = []
+        for kind, table in (("act", self._fwd), ("grad", self._bwd)):
+            for r in sorted(table):
+                group, src, dst = table[r]
+                if me not in (src, dst) or group is None:
+                    continue
+                out.append({"dir": f"{kind} {src}->{dst}", "backend": str(dist.get_backend(group)),
+                            "group_world": dist.get_world_size(group), "group_rank": dist.get_rank(group),
+                            "warmed": (table is self._fwd, r) in self.warmed})
+        return out
 
     def _link(self, table, r):
         return table.get(r % self.world) if self.world > 1 else None

@@ -96,6 +96,17 @@ def test_bench_json_contract(nproc, extra, expect):
     v = cfg["virtual_chunks_per_rank"]
     assert rec["bubble_theory_pct"] == pytest.approx(100.0 * (nproc - 1) / (v * cfg["chunks"] + nproc - 1), abs=0.01)
     assert rec["vs_baseline"] is None  # not the reference's config
+    # the communicators as the job saw them (a multi-GPU JSON checks itself against these)
+    comm = rec["comm"]
+    assert comm["world_size"] == nproc and [r["rank"] for r in comm["per_rank"]] == list(range(nproc))
+    assert comm["rccl_version"] and comm["backend"] == (None if nproc == 1 else "gloo")
+    if extra[:2] != ["--transport", "ipc"] and "ipc" not in extra:
+        v = cfg["virtual_chunks_per_rank"]
+        links = 2 * (nproc if v > 1 else nproc - 1)  # activation + gradient direction per pipeline link
+        assert comm["pipeline_links"] == links and comm["pipeline_links_warmed"] == links
+        for r in comm["per_rank"]:
+            for c in r["channels"]:
+                assert c["group_world"] == 2 and c["backend"] == "gloo" and c["warmed"]
 
 
 def test_bench_pipe_impl_cpu():

@@ -522,6 +522,99 @@ def test_wgrad_split_k(k, N, K, T, nseg):
         assert err < 1e-3, (N, K, T, nseg, accumulate, err)
 
 
+@pytest.mark.parametrize("M,N,K,bias,act", [
+    (8192, 4096, 4096, True, 0),     # enc12 out-proj shape, one round
+    (1000, 1000, 128, True, 1),      # edge rows (clamped), 256x128 blocks
+    (2048, 9000, 512, True, 0),      # multi-round grid launched in chunks along N
+    (4608, 1024, 256, False, 2),     # chunks along M (the emitted columns shift)
+    (1024, 1024, 8192, False, 0),    # long K on a small grid: split-K blocks each emit their K-tiles
+    (520, 264, 64, True, 2),         # one K-tile
+])
+def test_linear_fwd_emits_x_transposed(k, M, N, K, bias, act):
+    """The forward GEMM's A^T emission (GemmArgs::at): x^T bit-exact, and the
+    forward output identical to the launch without it."""
+    torch.manual_seed(21)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16) if bias else None
+    xt = torch.full((K, M), float("nan"), device=DEV).to(torch.bfloat16)
+    y1, pre1, _, _ = k.linear_fwd(x, w, b, act, 0.0, act == 2, None, xt)
+    y0, pre0, _, _ = k.linear_fwd(x, w, b, act, 0.0, act == 2)
+    assert torch.equal(xt, x.t())
+    assert torch.equal(y1, y0)
+    if act == 2:
+        assert torch.equal(pre1, pre0)
+
+
+@pytest.mark.parametrize("N,Kin,T,nseg,bias", [
+    (12288, 4096, 256, 3, True),   # enc12 qkv widths: the bias fold (>= 16 tile rows)
+    (520, 4096, 128, 5, True),     # edge columns of C^T
+    (1600, 1600, 1024, 4, True),   # GPT-2-XL: < 16 tile rows, no fold; split-K
+    (6400, 1600, 512, 2, False),
+    (1000, 4104, 128, 18, True),   # > 16 segments: two launches, the second accumulates
+])
+def test_wgrad_xt_segments(k, N, Kin, T, nseg, bias):
+    """The transposed weight gradient main_grad (+)= sum_i (x_i^T dy_i)^T and the
+    B-side bias fold, against fp32, storing (first write) and accumulating."""
+    torch.manual_seed(22)
+    dys = [torch.randn(T, N, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    xs = [torch.randn(T, Kin, device=DEV).to(torch.bfloat16) for _ in range(nseg)]
+    xts = [x.t().contiguous() for x in xs]
+    expect = sum(d.float().t() @ x.float() for d, x in zip(dys, xs))
+    for accumulate in (False, True):
+        main = torch.randn(N, Kin, device=DEV)
+        base = main.clone() if accumulate else torch.zeros_like(main)
+        bg = torch.full((N,), 0.5, device=DEV) if bias else None
+        fused = k.linear_wgrad_xt_segments(dys, xts, main, accumulate, bg)
+        err = ((main - base - expect).abs().max() / expect.abs().max()).item()
+        assert err < 1e-3, (N, Kin, T, nseg, accumulate, err)
+        if Kin < 4096:
+            assert not fused
+        if bias and fused:
+            ref = 0.5 + sum(d.float().sum(0) for d in dys)
+            assert torch.allclose(bg, ref, atol=1e-2, rtol=1e-4), (bg - ref).abs().max()
+        elif bias:
+            assert torch.all(bg == 0.5)
+
+
+def test_linear_xt_path_matches_plain_wgrad(k):
+    """A FlatAdam-owned Linear trained through the x^T path (the default) gets
+    the same weight / bias gradients, deferred or not, as with MIPIPE_WGRAD_XT
+    off (x kept, both operands read I-contiguous)."""
+    import importlib
+
+    L = importlib.import_module("mipipe.ops.linear")  # the module (mipipe.ops.linear is also a function)
+    torch.manual_seed(23)
+    T, K, N = 512, 4096, 1024
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = torch.nn.Parameter((torch.randn(N, K, device=DEV) / 64).to(torch.bfloat16))
+    b = torch.nn.Parameter(torch.randn(N, device=DEV).to(torch.bfloat16))
+    dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+
+    def grads(emit, deferred):
+        old = L._EMIT_XT
+        L._EMIT_XT = emit
+        try:
+            w.main_grad = torch.zeros(N, K, device=DEV)
+            b.main_grad = torch.zeros(N, device=DEV)
+            ctx = L.deferred_wgrad() if deferred else None
+            if ctx:
+                ctx.__enter__()
+            for _ in range(2):  # two micro-batches
+                L.linear(x, w, b, "relu").backward(dy)
+            if ctx:
+                ctx.__exit__(None, None, None)
+            return w.main_grad.clone(), b.main_grad.clone()
+        finally:
+            L._EMIT_XT = old
+
+    for deferred in (False, True):
+        gw1, gb1 = grads(True, deferred)
+        gw0, gb0 = grads(False, deferred)
+        assert ((gw1 - gw0).abs().max() / gw0.abs().max()).item() < 1e-5, deferred
+        assert torch.allclose(gb1, gb0, atol=1e-3, rtol=1e-5), deferred
+
+
 def test_gemm_round_launches_identical(k):
     """Multi-round grids launched one round of tiles at a time give the same bits as one
     launch -- forward with bias / ReLU / dropout (the mask keeps full-matrix coordinates),
