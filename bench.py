@@ -93,6 +93,11 @@ def parse():
                     help="every rank on cuda:0 (gloo for the small collectives, --transport ipc for the stage "
                          "boundaries): a one-GPU rehearsal of the multi-rank step for timelines "
                          "(tools/profile_ranks.py); NOT a throughput number for n_gpus ranks")
+    ap.add_argument("--pipe-balance", default=None,
+                    help="--impl pipe: transformer LAYERS per partition, e.g. 8,8 (the reference's main.py: "
+                         "embedding + layers 0-7 | layers 8-15 + decoder); with --gpus 1 every partition sits on "
+                         "cuda:0 and each boundary is a native device-to-device copy on the copy streams "
+                         "(Pipe(balance=..., copy_same_device=True)), else partition j on cuda:j")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -441,17 +446,45 @@ def run_pipe(args) -> int:
     mb = args.micro_batch or _default_micro_batch(cfg)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(1234)
-    plan = plan_stages(cfg, n, 1, m, split_decoder=False)
-    stages = [build_stage(cfg, plan, s, device=devices[s], dtype=dtype).train() for s in range(n)]
-    params = [p for st_ in stages for p in st_.parameters()]
-    # weight gradients deferred to one K-segmented GEMM per weight after the backward, as the engine does
-    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
-    pipe = mipipe.Pipe(torch.nn.Sequential(*stages), chunks=m, checkpoint=args.checkpoint)
+    if args.pipe_balance:
+        # the reference's partitioning (main.py:139-171): whole layers per partition, the
+        # embedding with the first, the decoder (and a final norm) with the last
+        from mipipe.models import build_lm_blocks
+
+        layers = [int(v) for v in args.pipe_balance.split(",")]
+        if sum(layers) != cfg.num_layers or min(layers) < 0:
+            raise SystemExit(f"--pipe-balance {args.pipe_balance}: must sum to the {cfg.num_layers} layers")
+        if n > 1 and len(layers) != n:
+            raise SystemExit(f"--pipe-balance has {len(layers)} partitions for --gpus {n}")
+        balance = [2 * L for L in layers]  # an attention and an MLP block per layer
+        balance[0] += 1
+        balance[-1] += 2 if cfg.norm_first else 1
+        blocks = build_lm_blocks(cfg, device=devices[0], dtype=dtype)
+        first = 0
+        for j, size in enumerate(balance):
+            for b in blocks[first:first + size]:
+                b.to(devices[j if n > 1 else 0]).train()
+            first += size
+        params = [p for b in blocks for p in b.parameters()]
+        opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
+        pipe = mipipe.Pipe(torch.nn.Sequential(*blocks), chunks=m, checkpoint=args.checkpoint, balance=balance,
+                           copy_same_device=(n == 1 and len(balance) > 1))
+        plan = None
+    else:
+        plan = plan_stages(cfg, n, 1, m, split_decoder=False)
+        stages = [build_stage(cfg, plan, s, device=devices[s], dtype=dtype).train() for s in range(n)]
+        params = [p for st_ in stages for p in st_.parameters()]
+        # weight gradients deferred to one K-segmented GEMM per weight after the backward, as the engine does
+        opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
+        pipe = mipipe.Pipe(torch.nn.Sequential(*stages), chunks=m, checkpoint=args.checkpoint)
+    devices_used = list(dict.fromkeys(pipe.devices))
 
     g = torch.Generator(device="cpu").manual_seed(0)
     tokens = torch.randint(0, V, (m * mb, S + 1), generator=g)
     x = tokens[:, :S].contiguous().to(devices[0])
     t = tokens[:, 1:].contiguous().to(devices[-1])
+
+    t = t.to(devices_used[-1])
 
     def sync():
         for d in dict.fromkeys(devices):
@@ -476,7 +509,7 @@ def run_pipe(args) -> int:
     ms = (time.perf_counter() - t0) / max(args.steps, 1) * 1e3
     value = m * mb * S / (ms / 1e3)
     ref_match = matches_reference(cfg, args, m, mb)
-    peaks = [torch.cuda.max_memory_allocated(d) / 2**30 for d in dict.fromkeys(devices)] if on_gpu else None
+    peaks = [torch.cuda.max_memory_allocated(d) / 2**30 for d in devices_used] if on_gpu else None
     out = {
         "metric": ("tokens/sec for 12-layer Transformer at PP=N (pipeline-parallel training)"
                    if cfg.name == "enc12_d4096" else f"tokens/sec for {cfg.name} at PP=N (pipeline-parallel training)"),
@@ -489,8 +522,11 @@ def run_pipe(args) -> int:
                      f"dim_feedforward={cfg.dim_feedforward} V={V}",
             "params": sum(p.numel() for p in params), "global_batch": m * mb, "seq_len": S, "micro_batch": mb,
             "chunks": m, "checkpoint": args.checkpoint, "schedule": "gpipe", "parallelism": f"pp{n}",
-            "impl": "pipe (single process, worker thread per GPU, peer copies on copy streams)",
-            "balance": plan.balance,
+            "impl": "pipe (single process, worker thread per GPU, peer copies on copy streams)" + (
+                f"; {len(pipe.partitions)} partitions on one GPU, device-to-device copies on the copy streams"
+                if pipe.copy_same_device else ""),
+            "balance": plan.balance if plan is not None else [len(p_) for p_ in pipe.partitions],
+            "partitions": len(pipe.partitions),
         },
         "bubble_gpipe_v1_pct": round(100.0 * (n - 1) / (m + n - 1), 2),
         "loss": float(loss.item()),

@@ -872,6 +872,11 @@ bool py_linear_wgrad_xt_segments(std::vector<Tensor> dys, std::vector<Tensor> xt
     GemmArgs g = args_for(first);
     if (fold) g.colsum = bias_grad->data_ptr<float>();
     Tensor ws = split_k_workspace(g, at::kBFloat16, main_grad);
+    Tensor cws;
+    if (fold && g.k_splits > 1) {
+      cws = at::empty({(int64_t)g.k_splits, N}, main_grad.options());
+      g.colsum_ws = cws.data_ptr<float>();
+    }
     gemm_bf16(g, cur_stream(main_grad));
   }
   return fold;

@@ -625,16 +625,26 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       for (int e = 0; e < 4; ++e) rs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
     }
   };
-  // fused bias gradient on the B side (GemmArgs::colsum): group-0 thread t
-  // sums the 4 columns [16 tm + 4 (t & 3), +4) of K-row t >> 2 of every B tile
+  // fused bias gradient on the B side (GemmArgs::colsum): the W/16 16-column
+  // slices of the tile column are spread over its tile rows -- block tm, group
+  // wm sums slices tm + tiles_m (wm + 2 j), j = 0, 1 (so >= W/64 tile rows
+  // cover them all, gemm_colsum_ok); group-local thread t sums the 4 columns
+  // [16 s + 4 (t & 3), +4) of K-row t >> 2 of every B tile it reads.
+  const int tiles_m = (g.M + BM - 1) / BM;
   const bool csum = X == kXColsum && !B_KC && g.colsum != nullptr && tm < W / 16;
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  float cs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   auto colsum_step = [&](const char* btile) {
-    if (csum && wm == 0) {
-      const int r = tid >> 2, c8 = 4 * tm + (tid & 3);
-      const s16x4 v = *reinterpret_cast<const s16x4*>(btile + ic_off_w<W>(r, c8));
+    if (csum) {
+      const int t = tid & 255;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+      for (int j = 0; j < 2; ++j) {
+        const int sl = tm + tiles_m * (wm + 2 * j);
+        if (sl < W / 16) {
+          const s16x4 v = *reinterpret_cast<const s16x4*>(btile + ic_off_w<W>(t >> 2, 4 * sl + (t & 3)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[j][e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+        }
+      }
     }
   };
   // A^T emission (GemmArgs::at, K-contiguous A): piece j of this wave covers
@@ -755,9 +765,16 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         if (u + 2 < nk) vmcnt_keep<NA + NB>();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      // Retire this interval's LDS reads BEFORE the barrier: right after it the
+      // other group restages the buffer just read (group 0 DMAs tile u+1 over
+      // tile u-1, group 1 tile u+2 over tile u), and a read still queued in
+      // the LDS when that DMA lands returns the new tile -- an intermittent
+      // wrong accumulator (tools/gemm_round_screen.py caught it: ~1 launch in
+      // 3 of one shape).  Guide rule: restage one phase after a read only when
+      // an lgkmcnt before the reading phase's barrier retired it.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -987,23 +1004,32 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       if (row < g.M) g.rowsum[row] += v;
     }
   }
-  if (csum) {  // the same reduction for the B-side column sums
+  if (csum) {  // the same reduction for the B-side column sums: lanes, then the 4 waves of each group via LDS
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem) + 64;
-    if (wm == 0) {
+    float* red = reinterpret_cast<float*>(smem) + 64;  // [8 waves][2 slices][16 columns]
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int o = 4; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
-      if (lane < 4)
+        for (int o = 4; o < 64; o <<= 1) cs[j][e] += __shfl_xor(cs[j][e], o, 64);
+    if (lane < 4)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) red[wave * 16 + 4 * lane + e] = cs[e];
-    }
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[(wave * 2 + j) * 16 + 4 * lane + e] = cs[j][e];
     __syncthreads();
-    if (tid < 16) {
-      const float v = red[tid] + red[16 + tid] + red[32 + tid] + red[48 + tid];
-      const int col = n0 + 16 * tm + tid;
-      if (col < g.N) g.colsum[col] += v;
+    if (tid < 64) {
+      const int gq = tid >> 5, j = (tid >> 4) & 1, c = tid & 15;
+      const int sl = tm + tiles_m * (gq + 2 * j);
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += red[((4 * gq + w) * 2 + j) * 16 + c];
+      const int col = n0 + 16 * sl + c;
+      if (sl < W / 16 && col < g.N) {
+        if (g.k_splits > 1) g.colsum[(int64_t)blockIdx.y * g.N + col] = v;  // split-K: a partial per split
+        else g.colsum[col] += v;
+      }
     }
   }
   // ---- epilogue ----
@@ -1237,6 +1263,16 @@ __global__ void __launch_bounds__(256) splitk_reduce_f32_kernel(const float* __r
   *dst = v;
 }
 
+// colsum[n] += the k_splits per-split column sums ws[s][n] (fixed order: deterministic).
+__global__ void __launch_bounds__(256) colsum_splits_kernel(const float* __restrict__ ws, int splits, int N,
+                                                            float* __restrict__ colsum) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += ws[(int64_t)s * N + n];
+  colsum[n] += v;
+}
+
 int g_gemm_splitk = -1;  // MIPIPE_GEMM_SPLITK=0 disables (A/B); -1 unread
 
 template <bool A_KC, bool B_KC, int EPI>
@@ -1276,11 +1312,11 @@ bool gemm_rowsum_ok(const GemmArgs& g) {
 }
 
 bool gemm_colsum_ok(const GemmArgs& g) {
-  if (g.b_kc || !(g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32) || gemm_splitk_factor(g) > 1) return false;
+  if (g.b_kc || !g.a_kc || !(g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32)) return false;
   GemmArgs b = g;
-  b.colsum = reinterpret_cast<float*>(1);  // as launched: on the 256-row kernel
+  b.k_splits = gemm_splitk_factor(g);  // as launched (split-K: per-split partials, reduced after)
   const int w = big_width(b);
-  return (g.M + big::BM - 1) / big::BM >= w / 16;
+  return 4 * ((g.M + big::BM - 1) / big::BM) >= w / 16;  // 4 slices per block (2 per wave group)
 }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
@@ -1406,7 +1442,8 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
     p.ldc = g.N;
     p.res = nullptr;
     p.trans_c = false;  // partials row-major; the reduction transposes
-    p.rowsum = p.colsum = nullptr;
+    p.rowsum = nullptr;
+    p.colsum = g.colsum != nullptr ? g.colsum_ws : nullptr;  // per-split column sums [k_splits][N]
     if (p.a_kc && p.b_kc) launch<true, true, kEpiStoreF32, kActNone>(p, s);
     else if (p.a_kc && !p.b_kc) launch<true, false, kEpiStoreF32, kActNone>(p, s);
     else if (!p.a_kc && !p.b_kc) launch<false, false, kEpiStoreF32, kActNone>(p, s);
@@ -1421,6 +1458,9 @@ void gemm_bf16(const GemmArgs& gi, hipStream_t s) {
       hipLaunchKernelGGL(splitk_reduce_f32_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, g.ws,
                          g.k_splits, g.M, g.N, g.ldc, g.epi == kEpiAccumF32, g.trans_c,
                          reinterpret_cast<float*>(g.C));
+      if (g.colsum != nullptr)
+        hipLaunchKernelGGL(colsum_splits_kernel, dim3((unsigned)((g.N + 255) / 256)), dim3(256), 0, s, g.colsum_ws,
+                           g.k_splits, g.N, g.colsum);
     }
     return;
   }

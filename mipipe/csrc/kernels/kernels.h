@@ -142,9 +142,11 @@ struct GemmArgs {
   float* rowsum = nullptr;
   // The same fold on the B side for the transposed weight-gradient GEMM
   // (C^T = X^T . dY, B = dY read as [K=T, N]): colsum[n] += sum_k B[k][n];
-  // blocks tm = 0 .. W/16-1 of a tile column sum 16 columns each
-  // (gemm_colsum_ok: >= W/16 tile rows, no split-K).
+  // the W/16 16-column slices of a tile column are spread over its tile
+  // rows, up to 4 per block (gemm_colsum_ok: >= W/64 tile rows); with split-K
+  // each split writes colsum_ws and one reduction adds them.
   float* colsum = nullptr;
+  float* colsum_ws = nullptr;  // split-K: [k_splits][N] per-split column sums (the caller's workspace)
   // Transposed fp32 output (kEpiAccumF32 / kEpiStoreF32): element (m, n) of
   // the product goes to C[n * ldc + m] -- the weight gradient dW = (X^T dY)^T
   // lands in main_grad's [N_out, K_in] layout.
