@@ -595,6 +595,7 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
     check_gemm_2d(*xt, "xt");
     MP_CHECK(dt == at::kBFloat16 && xt->scalar_type() == dt && xt->size(0) == K && xt->size(1) == M,
              "linear_fwd: xt must be bf16 [K, M]");
+    MP_CHECK(gemm_emit_ok((int)act, (float)p, save_preact), "linear_fwd: this epilogue cannot write xt (gemm_emit_ok)");
     g.at = xt->data_ptr();
     g.ldat = row_stride(*xt, "xt");
   }
@@ -1090,7 +1091,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_set_variant", &mipipe::adam_set_variant);
   py::class_<ipc::Link>(m, "IpcLink")
       .def_static("create", &ipc::Link::create, py::arg("name"), py::arg("device"), py::arg("nslots"),
-                  py::arg("slot_bytes"), py::arg("ipc_events") = true)
+                  py::arg("slot_bytes"))
       .def_static("attach", &ipc::Link::attach, py::arg("name"), py::arg("device"), py::arg("engine") = 0,
                   py::arg("timeout") = 60.0, py::call_guard<py::gil_scoped_release>())
       .def("send",
@@ -1112,6 +1113,27 @@ PYBIND11_MODULE(_C, m) {
              L.wait(seq, p, n, reinterpret_cast<hipStream_t>(consumer), timeout);
            },
            py::arg("seq"), py::arg("dst"), py::arg("consumer_stream"), py::arg("timeout") = 300.0)
+      // Zero-copy receive (device links): the consumer stream waits for message
+      // `seq` on the GPU and the returned tensor IS its slot (no copy), valid
+      // until release(seq).  The tensor does not own the memory: the Link (and
+      // its Python owner) must outlive it.
+      .def("slot_tensor",
+           [](ipc::Link& L, uint64_t seq, std::vector<int64_t> shape, py::object dtype, int64_t device) {
+             MP_CHECK(!L.host_mode() && !L.is_sender(), "ipc slot_tensor: receiving device links only");
+             const auto st = torch::python::detail::py_object_to_dtype(dtype);
+             int64_t n = 1;
+             for (auto d : shape) n *= d;
+             MP_CHECK(n * (int64_t)c10::elementSize(st) <= L.slot_bytes(), "ipc slot_tensor: tensor larger than a slot");
+             return at::from_blob(L.slot_ptr(seq), shape,
+                                  at::TensorOptions().dtype(st).device(at::kCUDA, (c10::DeviceIndex)device));
+           },
+           py::arg("seq"), py::arg("shape"), py::arg("dtype"), py::arg("device"))
+      .def("acquire",
+           [](ipc::Link& L, uint64_t seq, int64_t consumer) { L.acquire(seq, reinterpret_cast<hipStream_t>(consumer)); },
+           py::arg("seq"), py::arg("consumer_stream"))
+      .def("release",
+           [](ipc::Link& L, uint64_t seq, int64_t consumer) { L.release(seq, reinterpret_cast<hipStream_t>(consumer)); },
+           py::arg("seq"), py::arg("consumer_stream"))
       .def("done", &ipc::Link::done)
       .def("abort", &ipc::Link::abort)
       .def("unlink", &ipc::Link::unlink)
@@ -1119,10 +1141,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("copy_stream", [](const ipc::Link& L) { return reinterpret_cast<int64_t>(L.copy_stream()); })
       .def_property_readonly("nslots", &ipc::Link::nslots)
       .def_property_readonly("slot_bytes", &ipc::Link::slot_bytes)
-      .def_property_readonly("ipc_events", &ipc::Link::ipc_events)
       .def_property_readonly("host_mode", &ipc::Link::host_mode)
       .def_property_readonly("is_sender", &ipc::Link::is_sender);
-  m.def("ipc_proxy_shutdown", &ipc::proxy_shutdown, py::call_guard<py::gil_scoped_release>());
   using namespace mipipe;
   m.doc() = "mipipe native runtime + CDNA4 HIP kernels (gfx950)";
   // runtime
@@ -1183,6 +1203,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none());
+  m.def("gemm_emit_ok", &gemm_emit_ok, py::arg("act"), py::arg("p"), py::arg("aux"),
+        "whether linear_fwd can also write x^T for this activation / dropout / pre-activation output");
   m.def("linear_wgrad_xt_segments", &py_linear_wgrad_xt_segments, py::arg("dys"), py::arg("xts"),
         py::arg("main_grad"), py::arg("accumulate") = true, py::arg("bias_grad") = py::none());
   m.def("linear_dgrad", &py_linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("res") = py::none(),

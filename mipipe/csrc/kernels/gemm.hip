@@ -606,6 +606,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 
   int tm, tn;
   tile_coords((g.M + BM - 1) / BM, (g.N + W - 1) / W, tm, tn, g.group_m);
+  tm = __builtin_amdgcn_readfirstlane(tm);  // block-uniform: scalar registers, not two VGPRs
+  tn = __builtin_amdgcn_readfirstlane(tn);
   const int m0 = tm * BM, n0 = tn * W;
   f32x4 acc[8][NJ];
 #pragma unroll
@@ -626,54 +628,42 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     }
   };
   // fused bias gradient on the B side (GemmArgs::colsum): the W/16 16-column
-  // slices of the tile column are spread over its tile rows -- block tm, group
-  // wm sums slices tm + tiles_m (wm + 2 j), j = 0, 1 (so >= W/64 tile rows
-  // cover them all, gemm_colsum_ok); group-local thread t sums the 4 columns
-  // [16 s + 4 (t & 3), +4) of K-row t >> 2 of every B tile it reads.
+  // slices of the tile column are spread over its tile rows -- block tm, wave
+  // group wm sums slice tm + tiles_m wm (so >= W/32 tile rows cover them all,
+  // gemm_colsum_ok); group-local thread t sums the 4 columns [16 s + 4 (t & 3),
+  // +4) of K-row t >> 2 of every B tile it reads.  Four accumulators per lane:
+  // more (two slices per lane) spilled the main loop's DMA offsets.
   const int tiles_m = (g.M + BM - 1) / BM;
-  const bool csum = X == kXColsum && !B_KC && g.colsum != nullptr && tm < W / 16;
-  float cs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const int csl = tm + tiles_m * wm;  // this group's slice
+  const bool csum = X == kXColsum && !B_KC && g.colsum != nullptr && csl < W / 16;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
   auto colsum_step = [&](const char* btile) {
     if (csum) {
       const int t = tid & 255;
+      const s16x4 v = *reinterpret_cast<const s16x4*>(btile + ic_off_w<W>(t >> 2, 4 * csl + (t & 3)));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int sl = tm + tiles_m * (wm + 2 * j);
-        if (sl < W / 16) {
-          const s16x4 v = *reinterpret_cast<const s16x4*>(btile + ic_off_w<W>(t >> 2, 4 * sl + (t & 3)));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) cs[j][e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
-        }
-      }
+      for (int e = 0; e < 4; ++e) cs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
     }
   };
-  // A^T emission (GemmArgs::at, K-contiguous A): piece j of this wave covers
-  // tile rows [8 (4 wave + j), +8) x K columns [16 g, +16) (g = lane >> 4); a
-  // 16-lane group's two transposing reads give lane i the 8 rows of column
-  // 16 g + i, stored as one 16-byte chunk of at[k][m].
-  // Addresses are recomputed per emitting tile (1 in tiles_n of them) rather
-  // than held in registers across the main loop.
+  // A^T emission is spread evenly: K-tile kt's 32 pieces (wave w, j = 0..3:
+  // tile rows [8 (4 w + j), +8)) go to the tile-row's blocks in rotation --
+  // piece (w, j) by block tn = (4 w + j + kt) mod tiles_n -- so a wave emits
+  // at most one piece per K-tile (2 transposing reads, their wait, 1 store)
+  // instead of one block stalling on all 32: few extra registers (the dropout
+  // variant's main loop did not fit them otherwise) and no long stall.
   const int ntn = (g.N + W - 1) / W;
-  s16x4 ev[8];
-  auto emit_reads = [&](const char* atile) {
+  const int ewb = __builtin_amdgcn_readfirstlane((4 * wave) % ntn);  // scalar: no VGPR held across the loop
+  auto emit_piece = [&](const char* atile, int kt, int j) {
     const int q = (lane & 15) >> 2, p = lane & 3, gq = lane >> 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = 8 * (4 * wave + j) + q, c16 = 2 * gq + (p >> 1);
-      const int lo = r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4) + 8 * (p & 1);
-      const int hi = (r + 4) * 128 + ((c16 ^ (((r + 4) >> 1) & 7)) << 4) + 8 * (p & 1);
-      ev[2 * j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(atile + lo));
-      ev[2 * j + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(atile + hi));
-    }
-  };
-  auto emit_stores = [&](int kt) {
-    bf16_t* at = reinterpret_cast<bf16_t*>(g.at) + (int64_t)(kt * BK + 16 * (lane >> 4) + (lane & 15)) * g.ldat + m0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int rb = 4 * wave + j;
-      if (m0 + 8 * rb < g.M)
-        *reinterpret_cast<s16x8*>(at + 8 * rb) = __builtin_shufflevector(ev[2 * j], ev[2 * j + 1], 0, 1, 2, 3, 4, 5, 6, 7);
-    }
+    const int c16 = 2 * gq + (p >> 1);
+    const int rb = 4 * wave + j;
+    const int r = 8 * rb + q;
+    const int lo = r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4) + 8 * (p & 1);
+    const int hi = (r + 4) * 128 + ((c16 ^ (((r + 4) >> 1) & 7)) << 4) + 8 * (p & 1);
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(atile + lo));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(atile + hi));
+    bf16_t* at = reinterpret_cast<bf16_t*>(g.at) + (int64_t)(kt * BK + 16 * gq + (lane & 15)) * g.ldat + m0 + 8 * rb;
+    if (m0 + 8 * rb < g.M) *reinterpret_cast<s16x8*>(at) = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   int kt0 = 0, nk = g.K / BK;
   if (g.k_splits > 1) {  // this block's share of the K-tiles
@@ -730,16 +720,20 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     __builtin_amdgcn_s_barrier();
     if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
     bf16x8 af[8][2], bq[NJ][2];
-    int ekt = kt0 % ntn;  // (kt0 + u) mod tiles_n: this block emits A^T of K-tile kt0 + u when it equals tn
+    int ekt = kt0 % ntn;  // (kt0 + u) mod tiles_n (A^T emission rotation)
     for (int u = 0; u < nk; ++u) {
       char* cur = smem + (u & 1) * kBuf;
       char* nxt = smem + ((u + 1) & 1) * kBuf;
       // emission first: its reads precede this wave's DMA that may restage
       // `cur`, and its stores (waiting for those reads) precede the fragment
       // reads, so its 16 data registers are dead before the fragments load
-      if (X == kXEmit && A_KC && ekt == tn) {
-        emit_reads(cur);
-        emit_stores(kt0 + u);
+      if (X == kXEmit && A_KC) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int e = ewb + j + ekt;  // (4 wave + j + kt) mod tiles_n
+          while (e >= ntn) e -= ntn;
+          if (e == tn) emit_piece(cur, kt0 + u, j);
+        }
       }
 #pragma unroll
       for (int ii = 0; ii < 8; ++ii)
@@ -1004,27 +998,23 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       if (row < g.M) g.rowsum[row] += v;
     }
   }
-  if (csum) {  // the same reduction for the B-side column sums: lanes, then the 4 waves of each group via LDS
+  if (X == kXColsum && g.colsum != nullptr) {  // the same reduction for the B-side column sums, per group
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem) + 64;  // [8 waves][2 slices][16 columns]
+    float* red = reinterpret_cast<float*>(smem) + 64;  // [8 waves][16 columns]
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int o = 4; o < 64; o <<= 1) cs[j][e] += __shfl_xor(cs[j][e], o, 64);
+      for (int o = 4; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
     if (lane < 4)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) red[(wave * 2 + j) * 16 + 4 * lane + e] = cs[j][e];
+      for (int e = 0; e < 4; ++e) red[wave * 16 + 4 * lane + e] = cs[e];
     __syncthreads();
-    if (tid < 64) {
-      const int gq = tid >> 5, j = (tid >> 4) & 1, c = tid & 15;
-      const int sl = tm + tiles_m * (gq + 2 * j);
+    if (tid < 32) {
+      const int gq = tid >> 4, c = tid & 15;
+      const int sl = tm + tiles_m * gq;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) v += red[((4 * gq + w) * 2 + j) * 16 + c];
+      for (int w = 0; w < 4; ++w) v += red[(4 * gq + w) * 16 + c];
       const int col = n0 + 16 * sl + c;
       if (sl < W / 16 && col < g.N) {
         if (g.k_splits > 1) g.colsum[(int64_t)blockIdx.y * g.N + col] = v;  // split-K: a partial per split
@@ -1142,8 +1132,8 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
   const bool narrow = big_width(g) == 128;
-  if constexpr (A_KC && B_KC && EPI == kEpiStoreBf16) {
-    if (g.at != nullptr) {  // forward GEMM that also writes A^T
+  if constexpr (A_KC && B_KC && EPI == kEpiStoreBf16 && !(ACT == kActGelu && EXTRA)) {
+    if (g.at != nullptr) {  // forward GEMM that also writes A^T (gemm_emit_ok)
       if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA, big::kXEmit>(g, s);
       else launch_big<A_KC, B_KC, EPI, ACT, 4, 256, EXTRA, big::kXEmit>(g, s);
       return;
@@ -1311,12 +1301,17 @@ bool gemm_rowsum_ok(const GemmArgs& g) {
          (g.N + big_width(g) - 1) / big_width(g) >= 16;
 }
 
+// The A^T emission is compiled into every forward variant but the GELU one
+// with an extra epilogue (dropout / pre-activation output): that one would
+// spill its main loop's registers (scratch reloads inside the K loop).
+bool gemm_emit_ok(int act, float p, bool aux) { return !(act == kActGelu && (p > 0.f || aux)); }
+
 bool gemm_colsum_ok(const GemmArgs& g) {
   if (g.b_kc || !g.a_kc || !(g.epi == kEpiAccumF32 || g.epi == kEpiStoreF32)) return false;
   GemmArgs b = g;
   b.k_splits = gemm_splitk_factor(g);  // as launched (split-K: per-split partials, reduced after)
   const int w = big_width(b);
-  return 4 * ((g.M + big::BM - 1) / big::BM) >= w / 16;  // 4 slices per block (2 per wave group)
+  return 2 * ((g.M + big::BM - 1) / big::BM) >= w / 16;  // 2 slices per block (1 per wave group)
 }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {

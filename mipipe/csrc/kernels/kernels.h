@@ -143,7 +143,7 @@ struct GemmArgs {
   // The same fold on the B side for the transposed weight-gradient GEMM
   // (C^T = X^T . dY, B = dY read as [K=T, N]): colsum[n] += sum_k B[k][n];
   // the W/16 16-column slices of a tile column are spread over its tile
-  // rows, up to 4 per block (gemm_colsum_ok: >= W/64 tile rows); with split-K
+  // rows, 2 per block (gemm_colsum_ok: >= W/32 tile rows); with split-K
   // each split writes colsum_ws and one reduction adds them.
   float* colsum = nullptr;
   float* colsum_ws = nullptr;  // split-K: [k_splits][N] per-split column sums (the caller's workspace)
@@ -151,11 +151,12 @@ struct GemmArgs {
   // the product goes to C[n * ldc + m] -- the weight gradient dW = (X^T dY)^T
   // lands in main_grad's [N_out, K_in] layout.
   bool trans_c = false;
-  // A^T emission (forward GEMMs, A K-contiguous): the block whose tile column
-  // tn equals kt mod (tile columns) also writes K-tile kt of its A tile
-  // transposed, at[k][m] (bf16, row stride ldat, 16-byte aligned, m < M), from
-  // the LDS image it computes from: X^T for the layer's weight-gradient GEMM
-  // without a transposition pass (tools/wgrad_layout_probe.py).
+  // A^T emission (forward GEMMs, A K-contiguous): the blocks also write
+  // their A tiles transposed, at[k][m] (bf16, row stride ldat, 16-byte
+  // aligned, m < M), from the LDS images they compute from -- each K-tile's
+  // 8-row pieces shared out in rotation over the blocks of the tile row: X^T
+  // for the layer's weight-gradient GEMM without a transposition pass
+  // (tools/wgrad_layout_probe.py).
   void* at = nullptr;
   int64_t ldat = 0;
   const void* a_seg[kMaxSegs] = {};
@@ -164,6 +165,8 @@ struct GemmArgs {
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 // True if gemm_bf16 can fold g.rowsum into g (the wgrad layout, no split-K, >= 16 tile columns).
 bool gemm_rowsum_ok(const GemmArgs& g);
+// True if the forward GEMM with this epilogue can write A^T (GemmArgs::at).
+bool gemm_emit_ok(int act, float p, bool aux);
 // True if gemm_bf16 can fold g.colsum into g (B I-contiguous, fp32 out, no split-K, >= W/16 tile rows).
 bool gemm_colsum_ok(const GemmArgs& g);
 // Split-K factor gemm_bf16 would use for g (1 = none); the caller provides

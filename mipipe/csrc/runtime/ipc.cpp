@@ -1,4 +1,4 @@
-// Device-memory P2P transport between processes: see ipc.h.
+// Device-memory P2P transport between processes, completed on the GPU: see ipc.h.
 #include "ipc.h"
 
 #include <fcntl.h>
@@ -10,10 +10,7 @@
 
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <cstring>
-#include <deque>
-#include <mutex>
 #include <sstream>
 #include <stdexcept>
 #include <thread>
@@ -25,8 +22,9 @@ namespace ipc {
 
 namespace {
 
-constexpr uint64_t kMagic = 0x6d69706970654c4bull;  // "mipipeLK"
+constexpr uint64_t kMagic = 0x6d69706970654c32ull;  // "mipipeL2"
 constexpr int kMaxSlots = 1024;
+constexpr int64_t kFlagStride = 64;  // one flag word per 64-byte line
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
@@ -47,9 +45,11 @@ struct DeviceGuard {
   }
 };
 
+int64_t flag_bytes(int64_t nslots) { return (nslots * kFlagStride + 4095) & ~int64_t(4095); }
+
 }  // namespace
 
-struct alignas(64) SlotCtl {
+struct alignas(64) SlotCtl {  // host mode: the flags themselves; device mode: host-side counts for describe()
   std::atomic<uint64_t> full;
   std::atomic<uint64_t> freed;
   uint64_t bytes;
@@ -61,108 +61,28 @@ struct Shared {
   uint64_t magic;
   int64_t nslots;
   int64_t slot_bytes;
-  int32_t device;        // receiver's device, -1 host mode
-  int32_t use_events;
+  int32_t device;                            // receiver's device, -1 host mode
+  int32_t pad0;
   std::atomic<uint32_t> aborted;
-  std::atomic<uint32_t> sender_ready;
-  std::atomic<uint32_t> sender_detached;     // the sender has closed its mapping of the ring
-  hipIpcMemHandle_t mem;                     // the slot ring
-  hipIpcEventHandle_t freed_ev[kMaxSlots];   // receiver's events, waited by the sender
-  hipIpcEventHandle_t full_ev[kMaxSlots];    // sender's events, waited by the receiver
+  std::atomic<uint32_t> sender_ready;        // the sender has mapped the ring and exported its freed flags
+  std::atomic<uint32_t> sender_detached;     // the sender has unmapped the ring
+  std::atomic<uint32_t> receiver_detached;   // the receiver has unmapped the freed flags
+  std::atomic<uint64_t> sent;                // messages the sender has enqueued
+  std::atomic<uint64_t> released;            // messages the receiver has released (enqueued)
+  hipIpcMemHandle_t ring;                    // receiver's full flags + slots
+  hipIpcMemHandle_t freed;                   // sender's freed flags
   SlotCtl slots[kMaxSlots];
 };
 
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "cross-process atomics need lock-free 64-bit");
 
-// ------------------------------------------------------------------ proxy
-// Publishes a shared counter once a local event completes: the cross-process
-// completion signal for links whose runtime lacks interprocess events.
-namespace {
-
-struct ProxyItem {
-  hipEvent_t event;
-  int device;
-  std::atomic<uint64_t>* target;
-  uint64_t value;
-};
-
-class Proxy {
- public:
-  static Proxy& get() {
-    static Proxy p;
-    return p;
-  }
-  void push(const ProxyItem& it) {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      q_.push_back(it);
-      ++inflight_;
-      if (!thread_.joinable()) thread_ = std::thread([this] { loop(); });
-    }
-    cv_.notify_one();
-  }
-  // Blocks until every pushed item has been published.
-  void drain() {
-    std::unique_lock<std::mutex> l(mu_);
-    done_cv_.wait(l, [this] { return inflight_ == 0; });
-  }
-  void shutdown() {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      stop_ = true;
-    }
-    cv_.notify_one();
-    if (thread_.joinable()) thread_.join();
-    stop_ = false;
-  }
-  ~Proxy() { shutdown(); }
-
- private:
-  void loop() {
-    for (;;) {
-      ProxyItem it;
-      {
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [this] { return stop_ || !q_.empty(); });
-        if (q_.empty()) return;  // stop requested and drained
-        it = q_.front();
-        q_.pop_front();
-      }
-      if (it.device >= 0) {
-        (void)hipSetDevice(it.device);
-        (void)hipEventSynchronize(it.event);
-        (void)hipEventDestroy(it.event);
-      }
-      it.target->store(it.value, std::memory_order_release);
-      {
-        std::lock_guard<std::mutex> l(mu_);
-        --inflight_;
-      }
-      done_cv_.notify_all();
-    }
-  }
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  int64_t inflight_ = 0;
-  std::deque<ProxyItem> q_;
-  std::thread thread_;
-  bool stop_ = false;
-};
-
-}  // namespace
-
-void proxy_shutdown() { Proxy::get().shutdown(); }
-
-// ------------------------------------------------------------------ Link
 static size_t map_size(int64_t nslots, int64_t slot_bytes, bool host) {
-  size_t n = sizeof(Shared);
-  n = (n + 4095) & ~size_t(4095);
+  size_t n = (sizeof(Shared) + 4095) & ~size_t(4095);
   if (host) n += size_t(nslots) * size_t(slot_bytes);
   return n;
 }
 
-std::unique_ptr<Link> Link::create(const std::string& name, int device, int64_t nslots, int64_t slot_bytes,
-                                   bool use_ipc_events) {
+std::unique_ptr<Link> Link::create(const std::string& name, int device, int64_t nslots, int64_t slot_bytes) {
   if (nslots < 1 || nslots > kMaxSlots) throw std::runtime_error("mipipe ipc: nslots must be in [1, 1024]");
   if (slot_bytes < 16) throw std::runtime_error("mipipe ipc: slot_bytes too small");
   slot_bytes = (slot_bytes + 255) & ~int64_t(255);
@@ -188,32 +108,32 @@ std::unique_ptr<Link> Link::create(const std::string& name, int device, int64_t 
   sh->nslots = nslots;
   sh->slot_bytes = slot_bytes;
   sh->device = device;
-  sh->use_events = (!host && use_ipc_events) ? 1 : 0;
   sh->aborted.store(0);
   sh->sender_ready.store(0);
   sh->sender_detached.store(0);
+  sh->receiver_detached.store(0);
+  sh->sent.store(0);
+  sh->released.store(0);
   for (int k = 0; k < nslots; ++k) {
     sh->slots[k].full.store(0);
     sh->slots[k].freed.store(0);
     sh->slots[k].bytes = 0;
   }
   if (host) {
-    L->data_ = reinterpret_cast<char*>(p) + ((sizeof(Shared) + 4095) & ~size_t(4095));
+    L->ring_ = reinterpret_cast<char*>(p) + ((sizeof(Shared) + 4095) & ~size_t(4095));
   } else {
     DeviceGuard g(device);
     void* d = nullptr;
-    check(hipMalloc(&d, size_t(nslots) * size_t(slot_bytes)), "hipMalloc(slots)");
-    L->data_ = static_cast<char*>(d);
-    L->owns_data_ = true;
-    check(hipIpcGetMemHandle(&sh->mem, d), "hipIpcGetMemHandle");
-    if (sh->use_events) {
-      L->local_events_ = new hipEvent_t[nslots];
-      for (int k = 0; k < nslots; ++k) {
-        check(hipEventCreateWithFlags(&L->local_events_[k], hipEventDisableTiming | hipEventInterprocess),
-              "hipEventCreateWithFlags(interprocess)");
-        check(hipIpcGetEventHandle(&sh->freed_ev[k], L->local_events_[k]), "hipIpcGetEventHandle");
-      }
-    }
+    const size_t bytes = size_t(flag_bytes(nslots)) + size_t(nslots) * size_t(slot_bytes);
+    check(hipMalloc(&d, bytes), "hipMalloc(ring)");
+    check(hipMemset(d, 0, size_t(flag_bytes(nslots))), "hipMemset(full flags)");
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize(ring)");
+    L->ring_ = static_cast<char*>(d);
+    L->owns_ring_ = true;
+    check(hipIpcGetMemHandle(&sh->ring, d), "hipIpcGetMemHandle(ring)");
+    L->events_ = new hipEvent_t[nslots];
+    for (int k = 0; k < nslots; ++k)
+      check(hipEventCreateWithFlags(&L->events_[k], hipEventDisableTiming), "hipEventCreate(slot)");
   }
   std::atomic_thread_fence(std::memory_order_seq_cst);
   reinterpret_cast<std::atomic<uint64_t>*>(&sh->magic)->store(kMagic, std::memory_order_release);
@@ -254,25 +174,24 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
   const bool host = sh->device < 0;
   if (host != (device < 0)) throw std::runtime_error("mipipe ipc: host/device mode mismatch on " + name);
   if (host) {
-    L->data_ = reinterpret_cast<char*>(p) + ((sizeof(Shared) + 4095) & ~size_t(4095));
+    L->ring_ = reinterpret_cast<char*>(p) + ((sizeof(Shared) + 4095) & ~size_t(4095));
   } else {
     DeviceGuard g(device);
     void* d = nullptr;
-    check(hipIpcOpenMemHandle(&d, sh->mem, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    L->data_ = static_cast<char*>(d);
+    check(hipIpcOpenMemHandle(&d, sh->ring, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(ring)");
+    L->ring_ = static_cast<char*>(d);
+    void* f = nullptr;
+    check(hipMalloc(&f, size_t(flag_bytes(sh->nslots))), "hipMalloc(freed flags)");
+    check(hipMemset(f, 0, size_t(flag_bytes(sh->nslots))), "hipMemset(freed flags)");
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize(freed flags)");
+    L->freed_ = static_cast<char*>(f);
+    L->owns_freed_ = true;
+    check(hipIpcGetMemHandle(&sh->freed, f), "hipIpcGetMemHandle(freed flags)");
     check(hipStreamCreateWithFlags(&L->copy_stream_, hipStreamNonBlocking), "hipStreamCreate(copy)");
     const int64_t n = sh->nslots;
-    if (sh->use_events) {
-      L->local_events_ = new hipEvent_t[n];
-      L->remote_events_ = new hipEvent_t[n];
-      for (int k = 0; k < n; ++k) {
-        check(hipEventCreateWithFlags(&L->local_events_[k], hipEventDisableTiming | hipEventInterprocess),
-              "hipEventCreateWithFlags(interprocess)");
-        check(hipIpcGetEventHandle(&sh->full_ev[k], L->local_events_[k]), "hipIpcGetEventHandle");
-        check(hipIpcOpenEventHandle(&L->remote_events_[k], sh->freed_ev[k]), "hipIpcOpenEventHandle");
-      }
-      L->remote_open_ = true;
-    }
+    L->events_ = new hipEvent_t[n];
+    for (int k = 0; k < n; ++k)
+      check(hipEventCreateWithFlags(&L->events_[k], hipEventDisableTiming), "hipEventCreate(slot)");
   }
   sh->sender_ready.store(1, std::memory_order_release);
   return L;
@@ -298,38 +217,35 @@ static bool ipc_debug() {
 Link::~Link() {
   IPC_TRACE("destroy %s %s", sender_ ? "sender" : "receiver", name_.c_str());
   try {
-    if (!host_mode() && sh_ != nullptr && !ipc_events()) Proxy::get().drain();  // no publish into a dead map
-    IPC_TRACE("  proxy drained");
-    if (!host_mode() && data_ != nullptr) {
+    if (!host_mode() && sh_ != nullptr) {
       DeviceGuard g(device_);
+      // Everything this side queued on the link has run before a mapping goes:
+      // the sender's copy stream, the receiver's releases (on its streams).
       if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
-      IPC_TRACE("  copy stream synchronized");
+      else (void)hipDeviceSynchronize();
       if (sender_) {
-        (void)hipIpcCloseMemHandle(data_);
+        if (ring_) (void)hipIpcCloseMemHandle(ring_);
         sh_->sender_detached.store(1, std::memory_order_release);
-        IPC_TRACE("  unmapped the peer's ring");
-      } else if (owns_data_) {
-        // Free the ring only once no sender maps it: freeing memory a peer
-        // process still maps can block until that peer lets go, and two
-        // ranks tearing down their receivers first would wait on each other.
-        // A ring still mapped is left to the process teardown.
+        // The receiver maps our freed flags until it detaches; freeing memory a
+        // peer still maps can block until it lets go (two ranks tearing down
+        // in opposite orders would wait on each other), so a still-mapped
+        // allocation is left to the process teardown.
+        if (owns_freed_ && sh_->receiver_detached.load(std::memory_order_acquire)) (void)hipFree(freed_);
+      } else {
+        if (peer_open_ && freed_) (void)hipIpcCloseMemHandle(freed_);
+        sh_->receiver_detached.store(1, std::memory_order_release);
         const bool mapped = sh_->sender_ready.load(std::memory_order_acquire) &&
                             !sh_->sender_detached.load(std::memory_order_acquire);
-        if (!mapped) (void)hipFree(data_);
+        if (owns_ring_ && !mapped) (void)hipFree(ring_);
         IPC_TRACE("  ring %s", mapped ? "left mapped by the peer (not freed)" : "freed");
       }
-      const int64_t n = sh_ ? sh_->nslots : 0;
-      if (local_events_)
-        for (int k = 0; k < n; ++k) (void)hipEventDestroy(local_events_[k]);
-      if (remote_events_ && remote_open_)
-        for (int k = 0; k < n; ++k) (void)hipEventDestroy(remote_events_[k]);
+      if (events_)
+        for (int64_t k = 0; k < sh_->nslots; ++k) (void)hipEventDestroy(events_[k]);
       if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     }
   } catch (...) {
   }
-  IPC_TRACE("  events destroyed");
-  delete[] local_events_;
-  delete[] remote_events_;
+  delete[] events_;
   if (sh_) munmap(sh_, map_bytes_);
   if (fd_ >= 0) close(fd_);
   if (!sender_) shm_unlink(name_.c_str());  // idempotent: ENOENT after unlink() is fine
@@ -337,16 +253,22 @@ Link::~Link() {
 
 int64_t Link::nslots() const { return sh_->nslots; }
 int64_t Link::slot_bytes() const { return sh_->slot_bytes; }
-bool Link::ipc_events() const { return sh_->use_events != 0; }
 
 void Link::abort() { sh_->aborted.store(1, std::memory_order_release); }
 void Link::unlink() { shm_unlink(name_.c_str()); }
 
+char* Link::slot(uint64_t seq) const {
+  const int k = int(seq % uint64_t(sh_->nslots));
+  const int64_t base = host_mode() ? 0 : flag_bytes(sh_->nslots);
+  return ring_ + base + int64_t(k) * sh_->slot_bytes;
+}
+
 std::string Link::describe() const {
   std::ostringstream o;
   o << (sender_ ? "sender" : "receiver") << " of " << name_ << " (" << sh_->nslots << " slots x " << sh_->slot_bytes
-    << " B, " << (host_mode() ? "host" : ("device " + std::to_string(device_)))
-    << (ipc_events() ? ", ipc events" : (host_mode() ? "" : ", proxy-completed")) << ", next seq " << next_seq_ << ")";
+    << " B, " << (host_mode() ? "host" : ("device " + std::to_string(device_) + ", stream-ordered flags"))
+    << ", next seq " << next_seq_ << ", peer-visible sent " << sh_->sent.load() << " / released "
+    << sh_->released.load() << ")";
   return o.str();
 }
 
@@ -381,36 +303,30 @@ uint64_t Link::send(const void* src, size_t bytes, hipStream_t producer, double 
   const int64_t n = sh_->nslots;
   const int k = int(s % uint64_t(n));
   SlotCtl& c = sh_->slots[k];
-  // the slot's previous message (s - n) must have been released
-  if (s >= uint64_t(n)) wait_for("a free slot", s - uint64_t(n) + 1, k, false, timeout_s);
-  char* dst = data_ + size_t(k) * size_t(sh_->slot_bytes);
+  char* dst = slot(s);
   if (host_mode()) {
+    if (s >= uint64_t(n)) wait_for("a free slot", s - uint64_t(n) + 1, k, false, timeout_s);
     std::memcpy(dst, src, bytes);
     c.bytes = bytes;
     c.full.store(s + 1, std::memory_order_release);
+    sh_->sent.store(s + 1, std::memory_order_release);
     ++next_seq_;
     return s;
   }
   DeviceGuard g(device_);
-  if (s >= uint64_t(n) && ipc_events()) check(hipStreamWaitEvent(copy_stream_, remote_events_[k], 0), "wait freed");
   rt::stream_wait(copy_stream_, producer, device_);
+  if (s >= uint64_t(n))  // the slot's previous message released by the receiver's stream
+    check(hipStreamWaitValue64(copy_stream_, freed_ + int64_t(k) * kFlagStride, s - uint64_t(n) + 1,
+                               hipStreamWaitValueGte, ~0ull),
+          "hipStreamWaitValue64(freed)");
   if (bytes) {
-    if (engine_ == 1) {
-      rt::blit_copy(dst, src, bytes, copy_stream_);
-    } else {
-      check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, copy_stream_), "hipMemcpyAsync(send)");
-    }
+    if (engine_ == 1) rt::blit_copy(dst, src, bytes, copy_stream_);
+    else check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, copy_stream_), "hipMemcpyAsync(send)");
   }
+  check(hipStreamWriteValue64(copy_stream_, ring_ + int64_t(k) * kFlagStride, s + 1, 0), "hipStreamWriteValue64(full)");
+  check(hipEventRecord(events_[k], copy_stream_), "hipEventRecord(sent)");
   c.bytes = bytes;
-  if (ipc_events()) {
-    check(hipEventRecord(local_events_[k], copy_stream_), "hipEventRecord(full)");
-    c.full.store(s + 1, std::memory_order_release);
-  } else {
-    hipEvent_t e;
-    check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(proxy)");
-    check(hipEventRecord(e, copy_stream_), "hipEventRecord(proxy)");
-    Proxy::get().push({e, device_, &c.full, s + 1});
-  }
+  sh_->sent.store(s + 1, std::memory_order_release);
   ++next_seq_;
   return s;
 }
@@ -420,64 +336,86 @@ uint64_t Link::post() {
   return next_seq_++;
 }
 
-void Link::open_remote_events() {
-  if (remote_open_ || !ipc_events()) return;
-  // the sender's event handles exist once it has attached
+void Link::open_peer_flags() {
+  if (peer_open_ || host_mode()) return;
+  // the sender exports its freed flags when it attaches
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(300);
   while (!sh_->sender_ready.load(std::memory_order_acquire)) {
     if (sh_->aborted.load()) throw std::runtime_error("mipipe ipc: aborted before the sender attached");
+    if (std::chrono::steady_clock::now() > deadline) throw std::runtime_error("mipipe ipc: the sender never attached");
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
-  const int64_t n = sh_->nslots;
-  remote_events_ = new hipEvent_t[n];
-  for (int k = 0; k < n; ++k) check(hipIpcOpenEventHandle(&remote_events_[k], sh_->full_ev[k]), "hipIpcOpenEventHandle");
-  remote_open_ = true;
+  void* f = nullptr;
+  check(hipIpcOpenMemHandle(&f, sh_->freed, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(freed flags)");
+  freed_ = static_cast<char*>(f);
+  peer_open_ = true;
+}
+
+void* Link::acquire(uint64_t seq, hipStream_t consumer) {
+  if (sender_) throw std::runtime_error("mipipe ipc: acquire on a sending link");
+  if (host_mode()) throw std::runtime_error("mipipe ipc: acquire needs a device link (host mode copies)");
+  const int k = int(seq % uint64_t(sh_->nslots));
+  DeviceGuard g(device_);
+  check(hipStreamWaitValue64(consumer, ring_ + int64_t(k) * kFlagStride, seq + 1, hipStreamWaitValueGte, ~0ull),
+        "hipStreamWaitValue64(full)");
+  return slot(seq);
+}
+
+void Link::release(uint64_t seq, hipStream_t consumer) {
+  if (sender_) throw std::runtime_error("mipipe ipc: release on a sending link");
+  const int k = int(seq % uint64_t(sh_->nslots));
+  if (host_mode()) {
+    sh_->slots[k].freed.store(seq + 1, std::memory_order_release);
+  } else {
+    DeviceGuard g(device_);
+    open_peer_flags();
+    check(hipStreamWriteValue64(consumer, freed_ + int64_t(k) * kFlagStride, seq + 1, 0),
+          "hipStreamWriteValue64(freed)");
+    check(hipEventRecord(events_[k], consumer), "hipEventRecord(released)");
+  }
+  if (seq + 1 > last_done_seq_) last_done_seq_ = seq + 1;
+  sh_->released.store(last_done_seq_, std::memory_order_release);
 }
 
 void Link::wait(uint64_t seq, void* dst, size_t bytes, hipStream_t consumer, double timeout_s) {
   if (sender_) throw std::runtime_error("mipipe ipc: wait on a sending link");
   const int64_t n = sh_->nslots;
   const int k = int(seq % uint64_t(n));
-  SlotCtl& c = sh_->slots[k];
-  wait_for("the message", seq + 1, k, true, timeout_s);
-  if (c.full.load(std::memory_order_acquire) != seq + 1) {
-    std::ostringstream o;
-    o << "mipipe ipc: " << describe() << ": slot " << k << " holds message " << c.full.load() - 1 << ", expected "
-      << seq << " (receives posted out of order, or more than " << n << " in flight)";
-    throw std::runtime_error(o.str());
-  }
-  if (c.bytes != bytes) {
-    std::ostringstream o;
-    o << "mipipe ipc: " << describe() << ": message " << seq << " is " << c.bytes << " B, the receive expects "
-      << bytes;
-    throw std::runtime_error(o.str());
-  }
-  const char* src = data_ + size_t(k) * size_t(sh_->slot_bytes);
+  if ((int64_t)bytes > sh_->slot_bytes) throw std::runtime_error("mipipe ipc: receive larger than a slot");
   if (host_mode()) {
-    std::memcpy(dst, src, bytes);
-    c.freed.store(seq + 1, std::memory_order_release);
+    SlotCtl& c = sh_->slots[k];
+    wait_for("the message", seq + 1, k, true, timeout_s);
+    if (c.full.load(std::memory_order_acquire) != seq + 1) {
+      std::ostringstream o;
+      o << "mipipe ipc: " << describe() << ": slot " << k << " holds message " << c.full.load() - 1 << ", expected "
+        << seq << " (receives posted out of order, or more than " << n << " in flight)";
+      throw std::runtime_error(o.str());
+    }
+    if (c.bytes != bytes) {
+      std::ostringstream o;
+      o << "mipipe ipc: " << describe() << ": message " << seq << " is " << c.bytes << " B, the receive expects "
+        << bytes;
+      throw std::runtime_error(o.str());
+    }
+    std::memcpy(dst, slot(seq), bytes);
+    release(seq, nullptr);
     return;
   }
+  const void* src = acquire(seq, consumer);
   DeviceGuard g(device_);
-  if (ipc_events()) {
-    open_remote_events();
-    check(hipStreamWaitEvent(consumer, remote_events_[k], 0), "wait full");
-  }
   if (bytes) check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, consumer), "hipMemcpyAsync(recv)");
-  if (ipc_events()) {
-    check(hipEventRecord(local_events_[k], consumer), "hipEventRecord(freed)");
-    c.freed.store(seq + 1, std::memory_order_release);
-  } else {
-    hipEvent_t e;
-    check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(proxy)");
-    check(hipEventRecord(e, consumer), "hipEventRecord(proxy)");
-    Proxy::get().push({e, device_, &c.freed, seq + 1});
-  }
+  release(seq, consumer);
 }
 
 bool Link::done(uint64_t seq) const {
   const int k = int(seq % uint64_t(sh_->nslots));
-  const SlotCtl& c = sh_->slots[k];
-  return (sender_ ? c.full : c.freed).load(std::memory_order_acquire) >= seq + 1;
+  if (host_mode()) {
+    const SlotCtl& c = sh_->slots[k];
+    return (sender_ ? c.full : c.freed).load(std::memory_order_acquire) >= seq + 1;
+  }
+  // the slot's event was last recorded for message seq or a later one
+  if (sender_ ? sh_->sent.load() < seq + 1 : last_done_seq_ < seq + 1) return false;
+  return hipEventQuery(events_[k]) == hipSuccess;
 }
 
 }  // namespace ipc

@@ -1,28 +1,35 @@
 // Device-memory point-to-point transport between PROCESSES (SURVEY §5.8 (a),
 // multi-process form): pipeline ranks that share a GPU -- or sit on different
 // GPUs of a node -- move activations and gradients without RCCL and without
-// host staging.
+// host staging, and without a host in the completion path.
 //
 // One Link per directed rank pair.  The RECEIVER owns a ring of `nslots`
-// device buffers (`slot_bytes` each) and exports them once (hipIpcGetMemHandle);
-// the SENDER maps them (hipIpcOpenMemHandle) and copies each message into the
-// next slot on a dedicated copy stream -- the DMA engines (hipMemcpyAsync) or a
-// blit kernel -- so a transfer takes no CUs from the compute stream.  A shared
-// control block (POSIX shm) carries per-slot sequence numbers:
+// device buffers (`slot_bytes` each) behind an array of 64-byte "full" flag
+// words, one device allocation exported once (hipIpcGetMemHandle); the SENDER
+// owns an array of "freed" flag words, exported the same way.  Each side maps
+// the other's allocation once (hipIpcOpenMemHandle).  Message s lands in slot
+// k = s mod nslots:
 //
-//   full[k]  = 1 + sequence number of the last message written into slot k
-//   freed[k] = 1 + sequence number of the last message the receiver released
+//   sender,   on its copy stream:  wait producer; hipStreamWaitValue64(freed[k]
+//             >= s - nslots + 1) (the slot's previous message released);
+//             copy src -> slot k (DMA engines or a blit kernel);
+//             hipStreamWriteValue64(full[k] = s + 1)   -- into the receiver's memory
+//   receiver, on its compute stream: hipStreamWaitValue64(full[k] >= s + 1);
+//             use slot k in place (zero copy) or copy it out; then
+//             hipStreamWriteValue64(freed[k] = s + 1)  -- into the sender's memory
 //
-// Completion crosses the process boundary either through interprocess events
-// (the receiver's stream waits on the event the sender recorded after its
-// copy: no host blocking on either side) or, where interprocess events are
-// unavailable, through a proxy thread that publishes `full`/`freed` once the
-// local copy event has completed.  Messages on a link are matched in order:
-// the receiver posts receives in the order the sender sends (the engine's rule
-// for every transport).
+// Every wait is a stream-ordered command-processor wait: neither host blocks,
+// a transfer overlaps whatever compute precedes the consumer's wait, and the
+// message moves once (sender -> the receiver's slot; the slot is the receive
+// buffer).  tools/micro/ipc_signal_probe.hip checks the primitive across two
+// processes on one MI355X (profiles/ipc_stream_ordered.txt).  Pooled local
+// events (one per slot, re-recorded) give the watchdog a non-blocking
+// completion query.  Messages on a link are matched in order: the receiver
+// posts receives in the order the sender sends (the engine's rule for every
+// transport).
 //
-// Host mode (no GPU): the slots live in the shm segment and copies are
-// memcpy -- the same protocol, exercised by the CPU tests.
+// Host mode (no GPU): the slots live in the shm segment, copies are memcpy
+// and the flags are host atomics -- the same protocol, for the CPU tests.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -40,8 +47,7 @@ class Link {
  public:
   // Receiver side: creates the shm control block `name` and the slot ring.
   // device < 0: host mode (slots in shared memory).
-  static std::unique_ptr<Link> create(const std::string& name, int device, int64_t nslots, int64_t slot_bytes,
-                                      bool use_ipc_events);
+  static std::unique_ptr<Link> create(const std::string& name, int device, int64_t nslots, int64_t slot_bytes);
   // Sender side: attaches to the receiver's block (waits up to `timeout_s`
   // for it to appear).  engine: 0 = hipMemcpyAsync, 1 = blit kernel.
   static std::unique_ptr<Link> attach(const std::string& name, int device, int engine, double timeout_s);
@@ -51,23 +57,31 @@ class Link {
   bool host_mode() const { return device_ < 0; }
   int64_t nslots() const;
   int64_t slot_bytes() const;
-  bool ipc_events() const;
   // Copy stream of a sender (0 in host mode / on the receiver).
   hipStream_t copy_stream() const { return copy_stream_; }
 
   // Sender: enqueue message `bytes` from `src` after the work queued on
-  // `producer` so far.  Returns the message's sequence number.
+  // `producer` so far.  Never blocks the host in device mode (host mode:
+  // blocks while the slot is unreleased).  Returns the sequence number.
   uint64_t send(const void* src, size_t bytes, hipStream_t producer, double timeout_s);
   // Receiver: reserve the next sequence number (posting order = send order).
   uint64_t post();
-  // Receiver: copy message `seq` into `dst` on `consumer` once it has arrived
-  // (host-blocks until the sender has issued it).
+  // Receiver, device mode: make `consumer` wait for message `seq` (no host
+  // block); returns the slot holding it, valid until release(seq).
+  void* acquire(uint64_t seq, hipStream_t consumer);
+  // The slot message `seq` lands in (no wait: pair with acquire()).
+  void* slot_ptr(uint64_t seq) const { return slot(seq); }
+  // Receiver: mark message `seq`'s slot free for the sender, after the work
+  // queued on `consumer` (device) / now (host).
+  void release(uint64_t seq, hipStream_t consumer);
+  // Receiver: acquire + copy into `dst` + release, on `consumer` (host mode:
+  // blocks until the message is there, then memcpy).
   void wait(uint64_t seq, void* dst, size_t bytes, hipStream_t consumer, double timeout_s);
-  // Sender / receiver: true once message `seq` is published (sender: copy
-  // issued and, without ipc events, completed; receiver: slot released).
+  // Sender: message `seq`'s copy has completed; receiver: its slot has been
+  // released (device mode: an event query, never blocks).
   bool done(uint64_t seq) const;
 
-  // Unblocks both sides with an error (a failed peer, a watchdog).
+  // Unblocks host-mode waits with an error (a failed peer, a watchdog).
   void abort();
   // Removes the shm name (after both sides are attached; the mapping stays).
   void unlink();
@@ -76,7 +90,8 @@ class Link {
  private:
   Link() = default;
   void wait_for(const char* what, uint64_t seq, int slot, bool full, double timeout_s) const;
-  void open_remote_events();
+  void open_peer_flags();
+  char* slot(uint64_t seq) const;
 
   std::string name_;
   bool sender_ = false;
@@ -85,17 +100,16 @@ class Link {
   Shared* sh_ = nullptr;
   size_t map_bytes_ = 0;
   int fd_ = -1;
-  char* data_ = nullptr;          // slot ring (device pointer, or inside the shm map)
-  bool owns_data_ = false;
+  char* ring_ = nullptr;          // receiver's allocation: full flags, then the slots (device, or in the shm map)
+  bool owns_ring_ = false;
+  char* freed_ = nullptr;         // sender's allocation: freed flags (device mode)
+  bool owns_freed_ = false;
+  bool peer_open_ = false;        // receiver: the sender's freed flags are mapped
   hipStream_t copy_stream_ = nullptr;
-  hipEvent_t* local_events_ = nullptr;   // sender: full[k]; receiver: freed[k]
-  hipEvent_t* remote_events_ = nullptr;  // sender: freed[k]; receiver: full[k] (opened lazily)
-  bool remote_open_ = false;
+  hipEvent_t* events_ = nullptr;  // one per slot: sender after the copy, receiver after the release
   uint64_t next_seq_ = 0;
+  uint64_t last_done_seq_ = 0;    // receiver: 1 + last released sequence (host bookkeeping)
 };
-
-// Completed-copy publisher for links without interprocess events.
-void proxy_shutdown();
 
 }  // namespace ipc
 }  // namespace mipipe

@@ -180,7 +180,7 @@ class _Linear(torch.autograd.Function):
             # (GemmArgs::at): only when a backward will want this weight's
             # gradient in a flat-optimizer main_grad
             if (save and _EMIT_XT and x2.dtype == torch.bfloat16 and ctx.needs_input_grad[1]
-                    and getattr(weight, "main_grad", None) is not None):
+                    and getattr(weight, "main_grad", None) is not None and k.gemm_emit_ok(act, p, act == 2)):
                 xt = torch.empty((x2.shape[1], x2.shape[0]), dtype=x2.dtype, device=x2.device)
             # GELU's pre-activation is written only for a backward (not under no_grad)
             y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2, xt)

@@ -436,12 +436,19 @@ class PipelineEngine:
         recv_x = [[None] * m for _ in range(v)]
         recv_w = [[None] * m for _ in range(v)]
         with label_range("post recvs: activations"):
+            # zero-copy transports (IPC links) hand out the receive slot itself as the
+            # buffer, held until the step ends: only with a slot per message of the step
+            zc = getattr(chan, "zero_copy", False) and getattr(chan, "slots", 0) >= m * v
             for c in range(v):
                 if not self._first(c):
                     for i in range(m):
-                        recv_x[c][i] = self._new_act(c)
+                        if zc:
+                            recv_x[c][i], work = chan.recv_act_view(self.act_shapes[c], self.act_dtype)
+                        else:
+                            recv_x[c][i] = self._new_act(c)
+                            work = chan.recv_act(recv_x[c][i])
                         recv_w[c][i] = self._track(f"recv activation: virtual stage {self.vstage[c]} micro-batch {i} "
-                                                   f"from rank {(self.rank - 1) % n}", chan.recv_act(recv_x[c][i]))
+                                                   f"from rank {(self.rank - 1) % n}", work)
         # ... and every skip receive (each skip has its own directed link).
         sk_rx: Dict = {}
         sk_grad_rx: Dict = {}
@@ -540,9 +547,14 @@ class PipelineEngine:
 
         def post_grad_recv(c: int, i: int) -> None:
             if not self._last(c) and grad_w[c][i] is None:
-                grad_buf[c][i] = self._new_act(c, out_meta[c][i])
+                if zc:
+                    meta = out_meta[c][i]
+                    grad_buf[c][i], work = chan.recv_grad_view(meta.shape, meta.dtype)
+                else:
+                    grad_buf[c][i] = self._new_act(c, out_meta[c][i])
+                    work = chan.recv_grad(grad_buf[c][i])
                 grad_w[c][i] = self._track(f"recv gradient: virtual stage {self.vstage[c]} micro-batch {i} from rank "
-                                           f"{(self.rank + 1) % n}", chan.recv_grad(grad_buf[c][i]))
+                                           f"{(self.rank + 1) % n}", work)
 
         def backward(c: int, i: int) -> None:
             mod = self.modules[c]
@@ -669,6 +681,9 @@ class PipelineEngine:
             with label_range("wait sends"):
                 for w in sends:
                     w.wait()
+            end_step = getattr(chan, "end_step", None)
+            if end_step is not None:
+                end_step()  # zero-copy receive slots: released behind the step's last reader
         except BaseException as exc:
             self._on_error(exc)
             raise

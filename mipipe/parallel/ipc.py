@@ -5,33 +5,41 @@
 handles with ``wait()``), built on the native :class:`mipipe._C.IpcLink`
 (``csrc/runtime/ipc.{h,cpp}``):
 
-* every receiving rank owns a ring of device slots per incoming link,
-  exported once (``hipIpcGetMemHandle``); the sending rank maps them and
-  copies each message into the next slot on a dedicated copy stream with the
-  DMA engines (``hipMemcpyAsync``) or a blit kernel -- no RCCL kernel
-  occupies CUs next to the GEMMs, and several ranks may share ONE GPU (RCCL
-  refuses that: ``profiles/nccl_probe_one_gpu.txt``);
-* completion crosses the process boundary through a proxy thread that
-  publishes the slot once the sender's copy has completed (default), or
-  through interprocess events (``ipc_events=True``: the receiver's compute
-  stream waits for the sender's copy on the GPU -- limited on ROCm 7.2 to
-  about 32 records per event, see ``_ipc_events_default``);
-* the receiver's ``wait()`` copies the slot into the engine's tensor on the
-  current stream and releases the slot.
+* every receiving rank owns a ring of device slots per incoming link behind
+  an array of "full" flag words, exported once (``hipIpcGetMemHandle``); the
+  sender owns the matching "freed" flags, exported the same way;
+* the sender's copy stream waits (on the GPU) for the slot to be free, copies
+  the message into it with the DMA engines (``hipMemcpyAsync``) or a blit
+  kernel, and writes the sequence number into the receiver's full flag
+  (``hipStreamWriteValue64``) -- no RCCL kernel occupies CUs next to the GEMMs,
+  and several ranks may share ONE GPU (RCCL refuses that:
+  ``profiles/nccl_probe_one_gpu.txt``);
+* the receiver's compute stream waits for that flag (``hipStreamWaitValue64``)
+  and reads the slot IN PLACE (:meth:`IpcChannels.recv_act_view`: the slot is
+  the receive buffer, one copy per message), then releases the slot on the
+  GPU by writing the sender's freed flag.
 
-The reference moves activations with peer copies on copy streams
-(``/root/reference/README.md:196-212``); this is the same transport for one
-process per GPU.  Without a GPU (``device.type == "cpu"``) the links live in
-shared memory and copies are ``memcpy`` -- the same protocol, for CPU tests.
+No host waits on either side: completion is stream-ordered end to end, as the
+reference's ``Wait`` (an event record plus a stream wait,
+``/root/reference/README.md:332-369``) and ``Copy`` (a copy on copy streams,
+``/root/reference/README.md:193-213``).  The legacy ``recv_act(t)`` form
+copies the slot into ``t`` on the consumer stream and releases it right away.
+
+Slots: the engine sends ``chunks x virtual`` messages per link and step, each
+into its own slot (``slots`` >= that), so a slot is a persistent
+per-(chunk, micro-batch) receive buffer; the engine releases the slots it
+read in place at the end of each step (:meth:`end_step`).
+
+Without a GPU (``device.type == "cpu"``) the links live in shared memory and
+copies are ``memcpy`` -- the same protocol with host atomics, for CPU tests.
 
 Construction is collective over the default process group (it gathers each
 rank's incoming-message size and shares a job-unique name prefix).
 """
 from __future__ import annotations
 
-import os
 import uuid
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -43,16 +51,6 @@ from ..stream import record_stream
 __all__ = ["IpcChannels", "ENGINES"]
 
 ENGINES = {"sdma": 0, "blit": 1}
-
-
-def _ipc_events_default() -> bool:
-    # Off by default: ROCm 7.2's interprocess events stop working after about
-    # 32 records of one event (a record then blocks, a wait fails with
-    # "invalid argument"; tools/ipc_bw.py --events reproduces it), and a
-    # training run re-records every slot's event once per step.  The proxy
-    # thread completes a message once its copy is done, at the price of a
-    # host-side wait in the receiver.
-    return os.environ.get("MIPIPE_IPC_EVENTS", "0") == "1"
 
 
 class _SendWork:
@@ -72,14 +70,15 @@ class _SendWork:
 
 
 class _RecvWork:
+    """Copying receive: ``wait()`` enqueues (GPU-side wait for the message, copy
+    into ``dst``, slot release) on the current stream; the host never blocks
+    on a device link."""
+
     def __init__(self, link, seq: int, dst: Tensor, timeout: float) -> None:
         self.link, self.seq, self.dst, self.timeout = link, seq, dst, timeout
         self._done = False
 
     def wait(self) -> bool:
-        """Blocks the host until the sender has issued the message, then copies
-        it into the destination on the current stream (stream-ordered after the
-        sender's copy)."""
         if not self._done:
             dst = self.dst
             stream = torch.cuda.current_stream(dst.device).cuda_stream if dst.is_cuda else 0
@@ -89,7 +88,27 @@ class _RecvWork:
         return True
 
     def is_completed(self) -> bool:
-        return self._done or bool(self.link.done(self.seq))
+        return self._done and bool(self.link.done(self.seq))
+
+
+class _ViewWork:
+    """Zero-copy receive: ``wait()`` makes the current stream wait (on the GPU)
+    for the message; the tensor handed out with this work is the slot."""
+
+    def __init__(self, chan: "IpcChannels", link, seq: int, device: torch.device) -> None:
+        self.chan, self.link, self.seq, self.device = chan, link, seq, device
+        self.waited = False
+
+    def wait(self) -> bool:
+        if not self.waited:
+            self.link.acquire(self.seq, torch.cuda.current_stream(self.device).cuda_stream)
+            self.waited = True
+        return True
+
+    def is_completed(self) -> bool:
+        # arrival is a GPU-side event the host does not poll; a receive counts as
+        # complete once its wait is on the stream (the watchdog reports the rest)
+        return self.waited
 
 
 class IpcChannels:
@@ -102,23 +121,19 @@ class IpcChannels:
         device: this rank's device (``cpu``: shared-memory host links).
         recv_bytes: the largest activation (bytes) this rank RECEIVES; the
             gradients it receives are sized by its downstream neighbour's.
-        slots: messages in flight per link (default: 64); a sender blocks
-            its host only when all are unreleased.  ``chunks x virtual`` (what
-            the engine passes) never blocks within a step; fewer is safe for
-            a plain GPipe chain but can deadlock a looping placement.
+        slots: messages in flight per link (default: 64).  The engine passes
+            ``chunks x virtual`` so every message of a step has its own slot:
+            a slot read in place is released only at :meth:`end_step`.
         engine: ``"sdma"`` (DMA engines) or ``"blit"`` (copy kernel) for the
             sender's copy.
-        ipc_events: complete through interprocess events (``MIPIPE_IPC_EVENTS=1``)
-            instead of the proxy thread (default).
-        timeout: seconds a host wait may block before it raises (the engine's
-            watchdog usually fires first).
+        timeout: seconds a host-mode wait may block before it raises (the
+            engine's watchdog usually fires first).
     """
 
     host_staged = False
 
     def __init__(self, ranks: Sequence[int], wrap: bool = False, *, device: torch.device, recv_bytes: int,
-                 slots: int = 64, engine: str = "sdma", ipc_events: Optional[bool] = None,
-                 timeout: float = 300.0) -> None:
+                 slots: int = 64, engine: str = "sdma", timeout: float = 300.0) -> None:
         if engine not in ENGINES:
             raise ValueError(f"engine must be one of {sorted(ENGINES)}, got {engine!r}")
         k = _native_loader.kernels()
@@ -129,10 +144,14 @@ class IpcChannels:
         self.world = n
         self.device = torch.device(device)
         self.timeout = float(timeout)
+        # zero-copy receives hold their slot until end_step(): only with a slot
+        # per message of a step (the caller checks slots against its step)
+        self.zero_copy = self.device.type == "cuda"
+        self.slots = int(slots)
         dev_index = self.device.index if self.device.type == "cuda" else -1
         if self.device.type == "cuda" and dev_index is None:
             dev_index = torch.cuda.current_device()
-        use_events = _ipc_events_default() if ipc_events is None else bool(ipc_events)
+            self.device = torch.device("cuda", dev_index)
         # job-unique prefix + every rank's incoming activation size (collective)
         prefix = [uuid.uuid4().hex[:12] if me == 0 else None]
         dist.broadcast_object_list(prefix, src=0)
@@ -141,6 +160,8 @@ class IpcChannels:
         by_rank = dict(s for s in sizes)
         self._act_in = self._act_out = self._grad_in = self._grad_out = None
         self._links: list = []
+        self._copy_streams: Dict[int, torch.cuda.ExternalStream] = {}
+        self._held: List[Tuple[object, int]] = []  # (link, seq) read in place, released at end_step
         if self.rank < 0 or n < 2:
             dist.barrier()
             dist.barrier()
@@ -155,11 +176,10 @@ class IpcChannels:
 
         # receivers first (they create the shm blocks and slot rings) ...
         if has_prev:
-            self._act_in = k.IpcLink.create(name("act", prev_g, me), dev_index, slots,
-                                            max(by_rank[me], 256), use_events)
+            self._act_in = k.IpcLink.create(name("act", prev_g, me), dev_index, slots, max(by_rank[me], 256))
         if has_next:
             self._grad_in = k.IpcLink.create(name("grad", next_g, me), dev_index, slots,
-                                             max(by_rank[next_g], 256), use_events)
+                                             max(by_rank[next_g], 256))
         dist.barrier()
         # ... then senders attach to the neighbours' blocks
         eng = ENGINES[engine]
@@ -172,17 +192,28 @@ class IpcChannels:
         for link in self._links:
             if not link.is_sender:
                 link.unlink()  # everyone is attached: no name left behind in /dev/shm
-        self._copy_streams: Dict[int, torch.cuda.Stream] = {}
 
     # ------------------------------------------------------------------ API
     def warmup(self, device: torch.device) -> None:
         """Nothing to do: the links are connected at construction."""
 
+    warmup_s = 0.0
+
     def describe(self) -> List[str]:
         return [link.describe() for link in self._links]
 
+    def comm_info(self) -> List[dict]:
+        """This rank's links, for the bench JSON (the RCCL channels report theirs)."""
+        out = []
+        for kind, link, peer_is_src in (("act in", self._act_in, True), ("grad in", self._grad_in, True),
+                                        ("act out", self._act_out, False), ("grad out", self._grad_out, False)):
+            if link is not None:
+                out.append({"dir": kind, "backend": "ipc", "group_world": 2, "group_rank": int(not peer_is_src),
+                            "warmed": True, "slots": int(link.nslots), "slot_bytes": int(link.slot_bytes)})
+        return out
+
     def abort(self) -> None:
-        """Unblocks every peer waiting on this rank's links with an error."""
+        """Unblocks every host-mode wait on this rank's links with an error."""
         for link in self._links:
             link.abort()
 
@@ -215,11 +246,28 @@ class IpcChannels:
             raise ValueError("receive buffers must be contiguous")
         return _RecvWork(link, link.post(), t, self.timeout)
 
+    def _recv_view(self, link, shape, dtype) -> Tuple[Tensor, object]:
+        """Zero-copy receive: (the slot as a tensor, its work).  Read the tensor
+        only after ``work.wait()`` (on the stream that waited) and not after
+        :meth:`end_step`."""
+        if link is None:
+            raise RuntimeError(f"rank {self.rank}: no link in that direction")
+        if not self.zero_copy:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            return t, self._recv(link, t)
+        seq = link.post()
+        t = link.slot_tensor(seq, list(shape), dtype, self.device.index)  # the GPU wait comes with work.wait()
+        self._held.append((link, seq))
+        return t, _ViewWork(self, link, seq, self.device)
+
     def send_act(self, t: Tensor):
         return self._send(self._act_out, t)
 
     def recv_act(self, t: Tensor):
         return self._recv(self._act_in, t)
+
+    def recv_act_view(self, shape, dtype):
+        return self._recv_view(self._act_in, shape, dtype)
 
     def send_grad(self, t: Tensor):
         return self._send(self._grad_out, t)
@@ -227,15 +275,32 @@ class IpcChannels:
     def recv_grad(self, t: Tensor):
         return self._recv(self._grad_in, t)
 
+    def recv_grad_view(self, shape, dtype):
+        return self._recv_view(self._grad_in, shape, dtype)
+
+    def end_step(self) -> None:
+        """Releases every slot read in place this step, after the work queued on
+        the current stream (the step's last reader of them)."""
+        if not self._held:
+            return
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for link, seq in self._held:
+            link.release(seq, stream)
+        self._held = []
+
     def close(self) -> None:
         """Tears the links down: every sender unmaps its peer's ring, then (after
         a barrier, when a process group is up) every receiver frees its own.
         Collective when ``dist`` is initialised."""
         if self.device.type == "cuda":
+            self.end_step()
             torch.cuda.synchronize(self.device)
+        # the ExternalStream wrappers go before the links destroy their streams
+        self._copy_streams = {}
         self._act_out = self._grad_out = None
         self._links = [x for x in self._links if not x.is_sender]
         if dist.is_available() and dist.is_initialized():
             dist.barrier()
         self._links = []
         self._act_in = self._grad_in = None
+

@@ -526,9 +526,10 @@ def test_wgrad_split_k(k, N, K, T, nseg):
     (8192, 4096, 4096, True, 0),     # enc12 out-proj shape, one round
     (1000, 1000, 128, True, 1),      # edge rows (clamped), 256x128 blocks
     (2048, 9000, 512, True, 0),      # multi-round grid launched in chunks along N
-    (4608, 1024, 256, False, 2),     # chunks along M (the emitted columns shift)
+    (4608, 1024, 256, False, 0),     # chunks along M (the emitted columns shift)
     (1024, 1024, 8192, False, 0),    # long K on a small grid: split-K blocks each emit their K-tiles
-    (520, 264, 64, True, 2),         # one K-tile
+    (520, 264, 64, True, 1),         # one K-tile
+    (2048, 512, 1024, True, 2),      # GELU without the pre-activation output (eval-style forward)
 ])
 def test_linear_fwd_emits_x_transposed(k, M, N, K, bias, act):
     """The forward GEMM's A^T emission (GemmArgs::at): x^T bit-exact, and the
@@ -538,18 +539,24 @@ def test_linear_fwd_emits_x_transposed(k, M, N, K, bias, act):
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
     b = torch.randn(N, device=DEV).to(torch.bfloat16) if bias else None
     xt = torch.full((K, M), float("nan"), device=DEV).to(torch.bfloat16)
-    y1, pre1, _, _ = k.linear_fwd(x, w, b, act, 0.0, act == 2, None, xt)
-    y0, pre0, _, _ = k.linear_fwd(x, w, b, act, 0.0, act == 2)
+    p = 0.2 if act == 1 else 0.0  # ReLU + dropout: the enc12 FFN's extra-epilogue variant
+    torch.manual_seed(5)
+    y1, _, _, _ = k.linear_fwd(x, w, b, act, p, False, None, xt)
+    torch.manual_seed(5)
+    y0, _, _, _ = k.linear_fwd(x, w, b, act, p, False)
     assert torch.equal(xt, x.t())
     assert torch.equal(y1, y0)
-    if act == 2:
-        assert torch.equal(pre1, pre0)
+    # the GELU epilogue with a pre-activation output cannot emit: refused loudly
+    assert not k.gemm_emit_ok(2, 0.0, True) and not k.gemm_emit_ok(2, 0.1, False) and k.gemm_emit_ok(1, 0.2, False)
+    with pytest.raises(RuntimeError, match="xt"):
+        k.linear_fwd(x, w, b, 2, 0.0, True, None, xt)
 
 
 @pytest.mark.parametrize("N,Kin,T,nseg,bias", [
     (12288, 4096, 256, 3, True),   # enc12 qkv widths: the bias fold (>= 16 tile rows)
     (520, 4096, 128, 5, True),     # edge columns of C^T
-    (1600, 1600, 1024, 4, True),   # GPT-2-XL: 7 tile rows (slices spread over blocks and groups); split-K
+    (1600, 1600, 1024, 4, True),   # GPT-2-XL: 7 tile rows, no fold (< 8); split-K
+    (1600, 2048, 4096, 4, True),   # 8 tile rows, 56 tiles, K = 16384: the fold with split-K partials
     (6400, 1600, 512, 2, False),
     (1000, 4104, 128, 18, True),   # > 16 segments: two launches, the second accumulates
 ])
@@ -569,7 +576,8 @@ def test_wgrad_xt_segments(k, N, Kin, T, nseg, bias):
         err = ((main - base - expect).abs().max() / expect.abs().max()).item()
         assert err < 1e-3, (N, Kin, T, nseg, accumulate, err)
         if bias:
-            assert fused  # >= 4 tile rows of C^T (4 slices per block), split-K or not
+            # folded with >= 8 tile rows of C^T (2 slices per block), split-K or not
+            assert fused == (Kin >= 8 * 256 - 255), (Kin, fused)
         if bias and fused:
             ref = 0.5 + sum(d.float().sum(0) for d in dys)
             assert torch.allclose(bg, ref, atol=1e-2, rtol=1e-4), (bg - ref).abs().max()

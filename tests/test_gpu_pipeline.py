@@ -270,8 +270,10 @@ def test_engine_nccl_matches_single_rank(world, checkpoint, virtual, split, skip
 def test_engine_ipc_links_share_gpu(world, checkpoint, virtual, split, skips):
     """2 / 4 pipeline ranks on ONE MI355X, transport='ipc': every activation and
     gradient moves through device memory -- the sender's DMA copy into the
-    receiver's exported slot ring, completion via interprocess events -- no
-    host staging, no RCCL.  Against the single-rank engine (bf16 kernels)."""
+    receiver's exported slot ring, which the receiver reads in place; both
+    sides order each other on the GPU through flag words (stream write /
+    wait-value), no host wait, no host staging, no RCCL.  Against the
+    single-rank engine (bf16 kernels)."""
     run_engine_case("ipc_gpu", world, checkpoint, virtual, split, skips)
 
 
@@ -285,9 +287,9 @@ def test_engine_ipc_links_dropout_recompute_bit_identical(world, virtual):
 
 @pytest.mark.parametrize("world,virtual", [(2, 1), (4, 2)])
 def test_engine_ipc_links_slot_reuse_over_steps(world, virtual):
-    """Three steps: every slot, its interprocess events and its sequence
-    counters are reused (2-slot rings within the step for the plain chain,
-    step after step for the looping one) -- the last step still equals the
+    """Three steps: every slot, its flag words and its sequence counters are
+    reused step after step (a slot read in place is released at the end of
+    its step and refilled in the next) -- the last step still equals the
     single-rank engine."""
     run_engine_case("ipc_gpu", world, "except_last", virtual, virtual > 1, False, steps=3)
 

@@ -5,9 +5,12 @@ engine's channel classes, ping-pong, and report the one-way time per message
 (median of the round trips / 2) and the bandwidth it implies:
 
 * ``ipc``   -- :class:`mipipe.parallel.ipc.IpcChannels` (device-memory slots,
-  sender DMA copy, proxy-thread completion);
-* ``ipc-blit`` -- the same links with the blit-kernel copy engine;
-* ``ipc-events`` (``--events``) -- completion through interprocess events;
+  sender DMA copy, GPU-side flags), timed like the others: one ping-pong per
+  host iteration with a device sync and a barrier around it;
+* ``ipc-stream`` -- the same links driven the way the engine drives them: the
+  ping-pongs queued back to back with zero-copy receives and no host wait,
+  timed on the GPU (events) -- the transport's own one-way latency;
+* ``ipc-blit`` -- the ``ipc`` arm with the blit-kernel copy engine;
 * ``gloo``  -- :class:`mipipe.parallel.p2p.Channels` over gloo (host staging:
   D2H, TCP loopback, H2D) -- what multi-rank-on-one-GPU used before;
 * ``rccl``  -- the same Channels over RCCL, when the two ranks have GPUs of
@@ -47,7 +50,7 @@ def _channels(kind, dev, max_bytes):
 
     if kind.startswith("ipc"):
         return IpcChannels([0, 1], device=dev, recv_bytes=max_bytes, slots=4, timeout=30.0,
-                           engine="blit" if kind == "ipc-blit" else "sdma", ipc_events=kind == "ipc-events")
+                           engine="blit" if kind == "ipc-blit" else "sdma")
     ch = Channels([0, 1])
     ch.warmup(dev)
     return ch
@@ -79,6 +82,32 @@ def _worker(rank, ports, kinds, peer, iters, q, cpu=False):
                 n = (mib << 20) // 2
                 buf = torch.full((n,), float(rank), dtype=torch.bfloat16, device=dev)
                 rx = torch.empty_like(buf)
+                if kind == "ipc-stream":
+                    # back-to-back ping-pongs, zero-copy receives, no host wait; GPU-timed
+                    _sync(dev)
+                    dist.barrier()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    last = None
+                    for it in range(iters):
+                        if rank == 0:
+                            ch.send_act(buf).wait()
+                            last, w = ch.recv_grad_view(buf.shape, buf.dtype)
+                            w.wait()
+                        else:
+                            t, w = ch.recv_act_view(buf.shape, buf.dtype)
+                            w.wait()
+                            ch.send_grad(t).wait()  # the reply reads the slot: release after its copy
+                        if rank == 0:
+                            rx.copy_(last)
+                        ch.end_step()
+                    e1.record()
+                    _sync(dev)
+                    if rank == 0:
+                        assert float(rx[-1]) == 0.0
+                        one_way = e0.elapsed_time(e1) / 1e3 / iters / 2
+                        out[(kind, mib)] = (one_way * 1e6, (mib << 20) / one_way / 1e9)
+                    continue
                 times = []
                 for it in range(iters + 3):
                     if mib == 1 and it < 8:
@@ -113,12 +142,8 @@ def main():
     ap.add_argument("--peer", action="store_true", help="rank r on cuda:r (>= 2 GPUs); adds rccl")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cpu", action="store_true", help="host-mode links (protocol check, no GPU)")
-    ap.add_argument("--events", action="store_true",
-                    help="add the interprocess-event completion arm (fails after ~32 records per event on ROCm 7.2)")
     args = ap.parse_args()
-    kinds = ["ipc", "ipc-blit", "gloo"] + (["rccl"] if args.peer else [])
-    if args.events:
-        kinds = ["ipc-events"] + kinds
+    kinds = ["ipc-stream", "ipc", "ipc-blit", "gloo"] + (["rccl"] if args.peer else [])
     if args.cpu:
         kinds = ["ipc", "gloo"]
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
