@@ -72,7 +72,7 @@ def load(db: str):
         except ValueError:
             label = name
         regions.append((label, a, b))
-    kernels = con.execute("select start, end from kernels").fetchall()
+    kernels = con.execute("select start, end, name from kernels order by start").fetchall()
     return regions, kernels
 
 
@@ -80,6 +80,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("dbs", nargs="+")
     ap.add_argument("--step", type=int, default=-1, help="which 'engine step' range of each rank (default last)")
+    ap.add_argument("--end-kernel", default="sumsq_partial",
+                    help="a step's GPU work ends where the first kernel whose name contains this starts (the "
+                         "optimizer's grad-norm pass after PipelineEngine.step; '' = up to the next step's start "
+                         "or the last kernel)")
     args = ap.parse_args()
     paths = sorted({p for pat in args.dbs for p in glob.glob(pat, recursive=True)})
     ranks = []
@@ -91,9 +95,15 @@ def main() -> None:
             continue
         s0, s1 = steps[args.step]
         nxt = [a for a, _ in steps if a > s0]
-        limit = nxt[0] if nxt else max(b for _, b in kernels)
-        # kernels of this step: started after the step began, before the next one began
-        ks = [(a, b) for a, b in kernels if s0 <= a < limit]
+        limit = nxt[0] if nxt else max(b for _, b, _ in kernels)
+        if args.end_kernel:
+            # the GPU runs behind the host: a step's kernels end where the work queued
+            # after it (the optimizer) begins, not at the next step's host start
+            ends = [a for a, _, n in kernels if a >= s0 and args.end_kernel in n]
+            if ends:
+                limit = ends[0]
+        # kernels of this step: started after the step began, before the limit
+        ks = [(a, b) for a, b, _ in kernels if s0 <= a < limit]
         acts = [(n, a, b) for n, a, b in regions if s0 <= a and b <= s1 and n != "engine step"]
         ranks.append((p, s0, s1, ks, acts))
     if not ranks:
