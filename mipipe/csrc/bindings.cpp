@@ -703,6 +703,23 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad, bool accumulate) {
 // Deferred bias gradient over the micro-batches of a step: out (+)= column sums
 // of every [rows, cols] input, one stage-1 launch per input into a shared
 // partial buffer and ONE reduction.
+// x^T of a 2-D bf16/fp16 tensor [R, C] (row stride >= C, unit column stride)
+// into a new contiguous [C, R] tensor: the K-contiguous operand of
+// linear_wgrad_xt_segments when the flush transposes x itself (ops/linear.py).
+Tensor py_transpose_b16(Tensor x) {
+  check_cuda(x, "x");
+  MP_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.element_size() == 2, "transpose_b16: x must be 2-D, 2-byte, unit column stride");
+  const int64_t R = x.size(0), C = x.size(1), ld = x.stride(0);
+  MP_CHECK(R % 8 == 0 && C % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+           "transpose_b16: rows, cols and row stride must be multiples of 8, x 16-byte aligned");
+  MP_CHECK(C / 256 < 65536, "transpose_b16: too many columns");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto out = at::empty({C, R}, x.options());
+  mipipe::transpose_b16(reinterpret_cast<const uint16_t*>(x.data_ptr()), R, C, ld,
+                        reinterpret_cast<uint16_t*>(out.data_ptr()), R, cur_stream(x));
+  return out;
+}
+
 void py_column_sum_segments(std::vector<Tensor> xs, Tensor out, bool accumulate) {
   MP_CHECK(!xs.empty(), "column_sum_segments: empty list");
   check_cuda(out, "out");
@@ -1215,6 +1232,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_wgrad_segments", &py_linear_wgrad_segments, py::arg("dys"), py::arg("xs"), py::arg("main_grad"),
         py::arg("accumulate") = true, py::arg("bias_grad") = py::none());
   m.def("column_sum_segments", &py_column_sum_segments);
+  m.def("transpose_b16", &py_transpose_b16);
   m.def("gemm_f32", &py_gemm_f32);
   m.def("sumsq", &py_sumsq);
   m.def("adam_step", &py_adam);

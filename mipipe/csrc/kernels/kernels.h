@@ -289,5 +289,9 @@ void adam_step(float* master, M* model, const float* grad, float* m, float* v, i
 
 // ------------------------------------------------------------------ misc
 void gpu_sleep(int64_t microseconds, hipStream_t s);
+// out[c * ldo + r] = x[r * ldx + c], 2-byte elements; rows, cols, ldx, ldo
+// multiples of 8 and both pointers 16-byte aligned (the caller checks).
+void transpose_b16(const uint16_t* x, int64_t rows, int64_t cols, int64_t ldx, uint16_t* out, int64_t ldo,
+                   hipStream_t s);
 
 }  // namespace mipipe

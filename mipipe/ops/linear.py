@@ -310,10 +310,19 @@ _DEFERRED: Optional[dict] = None
 # Bias gradients folded into the weight-gradient GEMMs of the flush
 # (MIPIPE_FUSE_BIAS=0: separate column-sum kernels, for A/B runs).
 _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
-# Forward GEMMs write x^T for the transposed weight-gradient GEMM
-# (MIPIPE_WGRAD_XT=0: keep x and run the weight gradient with both operands
-# read I-contiguous, for A/B runs).
-_EMIT_XT = os.environ.get("MIPIPE_WGRAD_XT", "1") != "0"
+# Where the K-contiguous x^T of the transposed weight-gradient GEMM
+# (C^T = X^T . dY, ~15 % faster than reading both operands I-contiguous:
+# profiles/wgrad_layout_probe.txt) comes from -- MIPIPE_WGRAD_XT:
+#   auto (default): the flush transposes x (transpose_b16, a streaming kernel)
+#        for weights with at least _XT_MIN_N output features, where the GEMM
+#        saving outgrows the transpose (~N_out / 4000 x its cost);
+#   emit: the forward GEMM writes x^T from its staged A tiles (every tile-path
+#        linear; +x^T bytes of activation memory, and ~40 us per forward GEMM:
+#        a wash on enc12, profiles/wgrad_xt_ab.txt);
+#   0:   never (both operands read I-contiguous), for A/B runs.
+_XT_MODE = os.environ.get("MIPIPE_WGRAD_XT", "auto")
+_EMIT_XT = _XT_MODE in ("1", "emit")
+_XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "6144"))
 
 
 def _defer(w: Tensor, dy: Tensor, x: Tensor, transposed: bool = False) -> None:
@@ -431,6 +440,9 @@ def _flush_weight(k, w: Tensor, dys, xs, trans, bias_main: Optional[Tensor]) -> 
                 k.linear_wgrad_xt_segments([d], [xt], w.main_grad, _claim(w))
     if x_idx:
         pdys, pxs = [dys[i] for i in x_idx], [xs[i] for i in x_idx]
+        if not t_idx and _transpose_pays(w, pdys, pxs, T):
+            return k.linear_wgrad_xt_segments(pdys, [k.transpose_b16(x) for x in pxs], w.main_grad, _claim(w),
+                                              bias_main)
         if _uniform(pdys) and _uniform(pxs) and T % 64 == 0:
             fused = k.linear_wgrad_segments(pdys, pxs, w.main_grad, _claim(w),
                                             bias_main if not t_idx else None)
@@ -438,6 +450,17 @@ def _flush_weight(k, w: Tensor, dys, xs, trans, bias_main: Optional[Tensor]) -> 
             for d, x in zip(pdys, pxs):
                 k.linear_wgrad(d, x, w.main_grad, _claim(w))
     return fused
+
+
+def _transpose_pays(w: Tensor, dys, xs, T: int) -> bool:
+    """The flush transposes x for the transposed GEMM (MIPIPE_WGRAD_XT=auto):
+    wide enough outputs, bf16, shapes the transpose and the GEMM accept."""
+    if _XT_MODE != "auto" or w.shape[0] < _XT_MIN_N or T % 64 != 0:
+        return False
+    x0 = xs[0]
+    return (x0.dtype == torch.bfloat16 and dys[0].dtype == torch.bfloat16 and x0.dim() == 2
+            and x0.stride(1) == 1 and x0.shape[1] % 8 == 0 and x0.stride(0) % 8 == 0
+            and _uniform(dys) and _uniform(xs) and all(x.data_ptr() % 16 == 0 for x in xs))
 
 
 def begin_deferred_wgrad() -> bool:

@@ -586,9 +586,11 @@ def test_wgrad_xt_segments(k, N, Kin, T, nseg, bias):
 
 
 def test_linear_xt_path_matches_plain_wgrad(k):
-    """A FlatAdam-owned Linear trained through the x^T path (the default) gets
-    the same weight / bias gradients, deferred or not, as with MIPIPE_WGRAD_XT
-    off (x kept, both operands read I-contiguous)."""
+    """A Linear trained through either x^T source -- emitted by the forward GEMM
+    (MIPIPE_WGRAD_XT=emit) or transposed by the flush (auto; the width threshold
+    lowered so this shape takes it) -- gets the same weight / bias gradients,
+    deferred or not, as with the x^T path off (x kept, both operands read
+    I-contiguous)."""
     import importlib
 
     L = importlib.import_module("mipipe.ops.linear")  # the module (mipipe.ops.linear is also a function)
@@ -599,9 +601,9 @@ def test_linear_xt_path_matches_plain_wgrad(k):
     b = torch.nn.Parameter(torch.randn(N, device=DEV).to(torch.bfloat16))
     dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
 
-    def grads(emit, deferred):
-        old = L._EMIT_XT
-        L._EMIT_XT = emit
+    def grads(mode, deferred):
+        old = L._EMIT_XT, L._XT_MODE, L._XT_MIN_N
+        L._EMIT_XT, L._XT_MODE, L._XT_MIN_N = mode == "emit", mode, 0
         try:
             w.main_grad = torch.zeros(N, K, device=DEV)
             b.main_grad = torch.zeros(N, device=DEV)
@@ -614,13 +616,28 @@ def test_linear_xt_path_matches_plain_wgrad(k):
                 ctx.__exit__(None, None, None)
             return w.main_grad.clone(), b.main_grad.clone()
         finally:
-            L._EMIT_XT = old
+            L._EMIT_XT, L._XT_MODE, L._XT_MIN_N = old
 
     for deferred in (False, True):
-        gw1, gb1 = grads(True, deferred)
-        gw0, gb0 = grads(False, deferred)
-        assert ((gw1 - gw0).abs().max() / gw0.abs().max()).item() < 1e-5, deferred
-        assert torch.allclose(gb1, gb0, atol=1e-3, rtol=1e-5), deferred
+        gw0, gb0 = grads("0", deferred)
+        for mode in ("emit", "auto"):
+            gw1, gb1 = grads(mode, deferred)
+            assert ((gw1 - gw0).abs().max() / gw0.abs().max()).item() < 1e-5, (mode, deferred)
+            assert torch.allclose(gb1, gb0, atol=1e-3, rtol=1e-5), (mode, deferred)
+
+
+@pytest.mark.parametrize("R,C,ld", [(8192, 4096, 4096), (520, 264, 264), (64, 8, 8), (200, 1032, 1040), (8, 4104, 4104)])
+def test_transpose_b16(k, R, C, ld):
+    """transpose_b16 == torch's transpose, bit for bit, incl. partial 64-row/256-column tiles
+    and a row stride wider than the row."""
+    torch.manual_seed(R + C)
+    base = torch.randn(R, ld, device=DEV).to(torch.bfloat16)
+    x = base[:, :C]
+    out = k.transpose_b16(x)
+    assert out.shape == (C, R) and out.is_contiguous()
+    assert torch.equal(out, x.t().contiguous())
+    with pytest.raises(RuntimeError):
+        k.transpose_b16(base[:, 1:C])  # misaligned
 
 
 def test_gemm_round_launches_identical(k):

@@ -9,7 +9,10 @@ engine's channel classes, ping-pong, and report the one-way time per message
   host iteration with a device sync and a barrier around it;
 * ``ipc-stream`` -- the same links driven the way the engine drives them: the
   ping-pongs queued back to back with zero-copy receives and no host wait,
-  timed on the GPU (events) -- the transport's own one-way latency;
+  timed on the GPU (events) -- the transport's own one-way latency.  Both
+  ranks queue the whole loop behind a GPU sleep first, so the timed part runs
+  at the GPU's pace, not at Python's enqueue rate;
+* ``ipc-stream-blit`` -- ``ipc-stream`` with the blit-kernel copy engine;
 * ``ipc-blit`` -- the ``ipc`` arm with the blit-kernel copy engine;
 * ``gloo``  -- :class:`mipipe.parallel.p2p.Channels` over gloo (host staging:
   D2H, TCP loopback, H2D) -- what multi-rank-on-one-GPU used before;
@@ -50,7 +53,7 @@ def _channels(kind, dev, max_bytes):
 
     if kind.startswith("ipc"):
         return IpcChannels([0, 1], device=dev, recv_bytes=max_bytes, slots=4, timeout=30.0,
-                           engine="blit" if kind == "ipc-blit" else "sdma")
+                           engine="blit" if kind.endswith("blit") else "sdma")
     ch = Channels([0, 1])
     ch.warmup(dev)
     return ch
@@ -82,14 +85,19 @@ def _worker(rank, ports, kinds, peer, iters, q, cpu=False):
                 n = (mib << 20) // 2
                 buf = torch.full((n,), float(rank), dtype=torch.bfloat16, device=dev)
                 rx = torch.empty_like(buf)
-                if kind == "ipc-stream":
-                    # back-to-back ping-pongs, zero-copy receives, no host wait; GPU-timed
+                if kind.startswith("ipc-stream"):
+                    # back-to-back ping-pongs, zero-copy receives, no host wait; GPU-timed.
+                    # The loop is queued behind a sleep so it runs at the GPU's pace.
+                    n_it = max(iters, 200)
                     _sync(dev)
                     dist.barrier()
+                    from mipipe._native_loader import kernels
+                    kernels().gpu_sleep(300_000)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     last = None
-                    for it in range(iters):
+                    t_host = time.perf_counter()
+                    for it in range(n_it):
                         if rank == 0:
                             ch.send_act(buf).wait()
                             last, w = ch.recv_grad_view(buf.shape, buf.dtype)
@@ -102,10 +110,14 @@ def _worker(rank, ports, kinds, peer, iters, q, cpu=False):
                             rx.copy_(last)
                         ch.end_step()
                     e1.record()
+                    t_host = time.perf_counter() - t_host
                     _sync(dev)
+                    if t_host > 0.25:
+                        print(f"[rank {rank}] {kind}: queueing took {t_host:.3f} s, longer than the sleep: "
+                              "the time below is host-bound", flush=True)
                     if rank == 0:
                         assert float(rx[-1]) == 0.0
-                        one_way = e0.elapsed_time(e1) / 1e3 / iters / 2
+                        one_way = e0.elapsed_time(e1) / 1e3 / n_it / 2
                         out[(kind, mib)] = (one_way * 1e6, (mib << 20) / one_way / 1e9)
                     continue
                 times = []
@@ -143,7 +155,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cpu", action="store_true", help="host-mode links (protocol check, no GPU)")
     args = ap.parse_args()
-    kinds = ["ipc-stream", "ipc", "ipc-blit", "gloo"] + (["rccl"] if args.peer else [])
+    kinds = ["ipc-stream", "ipc-stream-blit", "ipc", "ipc-blit", "gloo"] + (["rccl"] if args.peer else [])
     if args.cpu:
         kinds = ["ipc", "gloo"]
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
