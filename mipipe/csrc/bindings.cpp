@@ -557,7 +557,8 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
                                                                            std::optional<Tensor> bias, int64_t act,
                                                                            double p, bool save_preact,
                                                                            std::optional<Tensor> res,
-                                                                           std::optional<Tensor> xt) {
+                                                                           std::optional<Tensor> xt,
+                                                                           bool aux_grad) {
   check_gemm_2d(x, "x");
   check_gemm_2d(w, "w");
   check_same_dtype(x, w, "linear_fwd");
@@ -566,6 +567,8 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   MP_CHECK(w.size(1) == K, "linear_fwd: inner dims differ");
   MP_CHECK(gemm_ok(dt, M, N, K), "linear_fwd: unsupported shape ", M, "x", N, "x", K);
   MP_CHECK(act >= 0 && act <= 2 && p >= 0.0 && p < 1.0, "linear_fwd: bad act/p");
+  MP_CHECK(!aux_grad || (act == kActGelu && save_preact && dt == at::kBFloat16),
+           "linear_fwd: aux_grad (GELU'(pre) as the saved tensor) needs bf16, GELU and save_preact");
   if (bias) {
     check_cuda(*bias, "bias");
     MP_CHECK(bias->scalar_type() == dt && bias->numel() == N, "linear_fwd: bad bias");
@@ -584,6 +587,7 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
   GemmArgs g;
   g.A = x.data_ptr(); g.B = w.data_ptr(); g.C = y.data_ptr();
   g.bias = bias ? bias->data_ptr() : nullptr; g.aux = pre ? pre->data_ptr() : nullptr;
+  g.aux_grad = aux_grad;
   if (res) {
     g.res = res->data_ptr();  // y = res + dropout(act(x . w^T + b)): the residual add in the epilogue
     g.ldr = row_stride(*res, "res");
@@ -636,7 +640,7 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res, std::opti
     check_same_dtype(dy, *res, "linear_dgrad res");
     MP_CHECK(res->size(0) == M && res->size(1) == K, "linear_dgrad: res must be [M, K]");
   }
-  MP_CHECK(act == kActNone || act == kActRelu || act == kActGelu, "linear_dgrad: bad act");
+  MP_CHECK(act == kActNone || act == kActRelu || act == kActGelu || act == kActSavedGrad, "linear_dgrad: bad act");
   if (act != kActNone) {
     MP_CHECK(saved.has_value() && dt == at::kBFloat16 && !res, "linear_dgrad: the activation backward needs bf16 "
              "operands, the saved tensor and no residual addend");
@@ -1219,7 +1223,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_rounds", &gemm_set_rounds, "1: launch multi-round GEMM grids one round of tiles at a time (default)");
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
-        py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none());
+        py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none(),
+        py::arg("aux_grad") = false);
   m.def("gemm_emit_ok", &gemm_emit_ok, py::arg("act"), py::arg("p"), py::arg("aux"),
         "whether linear_fwd can also write x^T for this activation / dropout / pre-activation output");
   m.def("linear_wgrad_xt_segments", &py_linear_wgrad_xt_segments, py::arg("dys"), py::arg("xts"),

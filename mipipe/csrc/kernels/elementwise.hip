@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
           for (int i = 0; i < 8; ++i) {
             if (ACT == kActRelu) a[i] = sv[i] > 0.f ? a[i] : 0.f;   // saved = the op's output
             if (ACT == kActGelu) a[i] *= gelu_grad(sv[i] + b[i]);  // saved = pre-bias input
+            if (ACT == kActSavedGrad) a[i] *= sv[i];              // saved = act'(pre) itself
           }
         }
         if (p > 0.f) {
@@ -175,6 +176,9 @@ void launch_bias_act(const T* in, const T* saved, const T* bias, T* out, int64_t
     case kActNone: hipLaunchKernelGGL((bias_act_kernel<T, kActNone, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset); break;
     case kActRelu: hipLaunchKernelGGL((bias_act_kernel<T, kActRelu, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset); break;
     case kActGelu: hipLaunchKernelGGL((bias_act_kernel<T, kActGelu, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset); break;
+    case kActSavedGrad:
+      if constexpr (BWD) hipLaunchKernelGGL((bias_act_kernel<T, kActSavedGrad, BWD>), grid, block, 0, s, in, saved, bias, out, rows, cols, p, thr, seed, offset);
+      break;
   }
 }
 

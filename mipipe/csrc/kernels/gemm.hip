@@ -137,9 +137,11 @@ __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_
 __device__ __forceinline__ float gelu_grad_f(float x) {
   return 0.5f * (1.f + erf_as(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
 }
-// act'(s) for the activation-backward epilogue (GemmArgs::dact): ReLU's from its output.
+// act'(s) for the activation-backward epilogue (GemmArgs::dact): ReLU's from its
+// output, GELU's from the pre-activation, or s itself (kActSavedGrad: the forward
+// stored GELU'(pre) -- one multiply, like ReLU's sign test).
 __device__ __forceinline__ float dact_f(int dact, float s) {
-  return dact == kActRelu ? (s > 0.f ? 1.f : 0.f) : gelu_grad_f(s);
+  return dact == kActRelu ? (s > 0.f ? 1.f : 0.f) : (dact == kActSavedGrad ? s : gelu_grad_f(s));
 }
 
 // Bijective XCD-aware remap + grouped (8 tile-rows) ordering.
@@ -263,7 +265,9 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
                       dact_f(g.dact, bf2f(reinterpret_cast<const bf16_t*>(g.dact_in)[(int64_t)(row0 + r) * g.ldd + col]));
           if (g.res != nullptr) out[r] += bf2f(reinterpret_cast<const bf16_t*>(g.res)[(int64_t)(row0 + r) * g.ldr + col]);
           C[(int64_t)(row0 + r) * g.ldc + col] = f2bf(out[r]);
-          if (g.aux != nullptr) reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] = f2bf(pre[r]);
+          if (g.aux != nullptr)
+            reinterpret_cast<bf16_t*>(g.aux)[(int64_t)(row0 + r) * g.ldc + col] =
+                f2bf(g.aux_grad ? gelu_grad_f(pre[r]) : pre[r]);
         }
       }
     }
@@ -442,7 +446,7 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
                                              int tid, int m0, int n0, int M, int N, int64_t ldc, void* out,
                                              const bf16_t* res, int64_t ldr = 0, const bf16_t* dact_in = nullptr,
                                              int64_t ldd = 0, int dact = 0, float dact_scale = 1.f,
-                                             bool trans = false) {
+                                             bool trans = false, bool dgelu = false) {
   constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512;
   const int quad = lane >> 4, col_in = lane & 15;
   float* stg = reinterpret_cast<float*>(smem);
@@ -471,6 +475,10 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
         const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8 + 4);
         const int64_t at = (int64_t)(rbase + row) * ldc + n0 + 8 * c8;
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dgelu) {  // GELU'(pre) for the backward instead of pre (GemmArgs::aux_grad)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_grad_f(v[e]);
+        }
         if (dact_in != nullptr) {  // activation backward: x act'(saved)
           const bf16x8 sv = *reinterpret_cast<const bf16x8*>(dact_in + (int64_t)(rbase + row) * ldd + n0 + 8 * c8);
 #pragma unroll
@@ -627,22 +635,30 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
       for (int e = 0; e < 4; ++e) rs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
     }
   };
-  // fused bias gradient on the B side (GemmArgs::colsum): the W/16 16-column
-  // slices of the tile column are spread over its tile rows -- block tm, wave
-  // group wm sums slice tm + tiles_m wm (so >= W/32 tile rows cover them all,
-  // gemm_colsum_ok); group-local thread t sums the 4 columns [16 s + 4 (t & 3),
-  // +4) of K-row t >> 2 of every B tile it reads.  Four accumulators per lane:
-  // more (two slices per lane) spilled the main loop's DMA offsets.
+  // fused bias gradient on the B side (GemmArgs::colsum): the tile column is cut
+  // into slices of 16 cm columns spread over its tile rows -- block tm, wave
+  // group wm sums slice tm + tiles_m wm; cm (1, 2, 4, 8) is the smallest that
+  // lets the 2 tiles_m slices cover all W columns (gemm_colsum_ok).  Group-local
+  // thread t sums the 4 columns [16 cm s + 4 q, +4), q = t mod 4 cm, of the
+  // cm K-rows t / (4 cm) + j 64 / cm of every B tile it reads.  Four
+  // accumulators per lane whatever cm is: more (two slices per lane) spilled
+  // the main loop's DMA offsets.
   const int tiles_m = (g.M + BM - 1) / BM;
+  const int cm_log = __builtin_amdgcn_readfirstlane(2 * tiles_m * 16 >= W ? 0 : 2 * tiles_m * 32 >= W ? 1
+                                                    : 2 * tiles_m * 64 >= W ? 2 : 3);
   const int csl = tm + tiles_m * wm;  // this group's slice
-  const bool csum = X == kXColsum && !B_KC && g.colsum != nullptr && csl < W / 16;
+  const bool csum = X == kXColsum && !B_KC && g.colsum != nullptr && csl < (W / 16 >> cm_log);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
   auto colsum_step = [&](const char* btile) {
     if (csum) {
       const int t = tid & 255;
-      const s16x4 v = *reinterpret_cast<const s16x4*>(btile + ic_off_w<W>(t >> 2, 4 * csl + (t & 3)));
+      const int q = t & ((4 << cm_log) - 1), r0 = t >> (2 + cm_log);
+      for (int j = 0; j < (1 << cm_log); ++j) {
+        const s16x4 v = *reinterpret_cast<const s16x4*>(
+            btile + ic_off_w<W>(r0 + (j << (6 - cm_log)), (4 << cm_log) * csl + q));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+        for (int e = 0; e < 4; ++e) cs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+      }
     }
   };
   // A^T emission is spread evenly: K-tile kt's 32 pieces (wave w, j = 0..3:
@@ -1022,23 +1038,23 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   }
   if (X == kXColsum && g.colsum != nullptr) {  // the same reduction for the B-side column sums, per group
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem) + 64;  // [8 waves][16 columns]
+    const int sw = 16 << cm_log;  // slice width
+    float* red = reinterpret_cast<float*>(smem) + 64;  // [8 waves][sw columns]
 #pragma unroll
     for (int e = 0; e < 4; ++e)
+      for (int o = 4 << cm_log; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
+    if (lane < (4 << cm_log))
 #pragma unroll
-      for (int o = 4; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
-    if (lane < 4)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) red[wave * 16 + 4 * lane + e] = cs[e];
+      for (int e = 0; e < 4; ++e) red[wave * sw + 4 * lane + e] = cs[e];
     __syncthreads();
-    if (tid < 32) {
-      const int gq = tid >> 4, c = tid & 15;
+    if (tid < 2 * sw) {
+      const int gq = tid >> (4 + cm_log), c = tid & (sw - 1);
       const int sl = tm + tiles_m * gq;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) v += red[(4 * gq + w) * 16 + c];
-      const int col = n0 + 16 * sl + c;
-      if (sl < W / 16 && col < g.N) {
+      for (int w = 0; w < 4; ++w) v += red[(4 * gq + w) * sw + c];
+      const int col = n0 + sw * sl + c;
+      if (sl < (W / 16 >> cm_log) && col < g.N) {
         if (g.k_splits > 1) g.colsum[(int64_t)blockIdx.y * g.N + col] = v;  // split-K: a partial per split
         else g.colsum[col] += v;
       }
@@ -1072,7 +1088,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         for (int j = 0; j < NJ; ++j) acc[i][j] += bias[j];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bias[j] = 0.f;
-      staged_store<kEpiStoreBf16, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, g.aux, nullptr);
+      staged_store<kEpiStoreBf16, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, g.aux, nullptr, 0,
+                                     nullptr, 0, 0, 1.f, false, ACT == kActGelu && g.aux_grad);
     }
     epi_rows<0, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
     epi_rows<1, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
@@ -1333,7 +1350,7 @@ bool gemm_colsum_ok(const GemmArgs& g) {
   GemmArgs b = g;
   b.k_splits = gemm_splitk_factor(g);  // as launched (split-K: per-split partials, reduced after)
   const int w = big_width(b);
-  return 2 * ((g.M + big::BM - 1) / big::BM) >= w / 16;  // 2 slices per block (1 per wave group)
+  return 2 * ((g.M + big::BM - 1) / big::BM) * 128 >= w;  // 2 slices of <= 128 columns per block
 }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {

@@ -61,6 +61,9 @@ template <typename T> void layernorm_bwd(const LnBwdArgs<T>& a, hipStream_t s);
 
 // ------------------------------------------------------------------ elementwise
 enum Activation : int { kActNone = 0, kActRelu = 1, kActGelu = 2 };
+// Backward-only activation code: the saved tensor IS act'(pre) (a GELU forward
+// GEMM wrote it with GemmArgs::aux_grad), so the backward is one multiply.
+constexpr int kActSavedGrad = 3;
 
 template <typename T>
 void bias_act_dropout_fwd(const T* x, const T* bias, T* y, int64_t rows, int cols, int act, float p, uint64_t seed,
@@ -96,6 +99,7 @@ struct GemmArgs {
   void* C = nullptr;        // bf16 or fp32 (epilogue)
   const void* bias = nullptr;  // bf16 [N] (kEpiStoreBf16 only)
   void* aux = nullptr;         // bf16 pre-activation output (optional)
+  bool aux_grad = false;       // aux holds GELU'(pre) instead of pre (bf16 GEMMs, ACT = GELU)
   const void* res = nullptr;   // bf16 [M, ldr] added to the bf16 output (optional, kEpiStoreBf16)
   int64_t lda = 0, ldb = 0, ldc = 0;
   int64_t ldr = 0;             // row stride of res (0: ldc)

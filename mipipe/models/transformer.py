@@ -35,12 +35,16 @@ from ..ops.linear import ActFold, mark_gemm_weight
 # MIPIPE_FANOUT=0 turns it off (A/B measurements).
 FANOUT = os.environ.get("MIPIPE_FANOUT", "1") != "0"
 # MLP activation backward in fc_out's dgrad epilogue (ops.linear.ActFold), for
-# the activations in FOLD_ACTS.  ReLU only by default: its backward is a sign
-# test on the saved output, nearly free in the epilogue (enc12 FFN dgrad + act
-# backward 240 -> 222 us), while GELU's erf/exp per element made the epilogue
-# slower than the separate memory-bound kernel (GPT-2-XL fc2 dgrad 244 -> 251
-# us; tools/gemm_dact_probe.py).  MIPIPE_FOLD_ACT=0: off, =all: GELU too.
-_FOLD_ENV = os.environ.get("MIPIPE_FOLD_ACT", "relu")
+# the activations in FOLD_ACTS.  ReLU's backward is a sign test on the saved
+# output, nearly free in the epilogue (enc12 FFN dgrad + act backward 240 -> 222
+# us).  GELU's is one multiply as well when its forward saves GELU'(pre)
+# (ops.linear MIPIPE_GELU_SAVE_GRAD, the default); with pre saved instead, the
+# erf/exp per element made the epilogue slower than the separate memory-bound
+# kernel (GPT-2-XL fc2 dgrad 244 -> 251 us; tools/gemm_dact_probe.py), so GELU
+# is then not folded.  MIPIPE_FOLD_ACT=0: off, =relu: ReLU only, =all: both.
+_FOLD_ENV = os.environ.get("MIPIPE_FOLD_ACT", "auto")
+if _FOLD_ENV == "auto":
+    _FOLD_ENV = "relu" if os.environ.get("MIPIPE_GELU_SAVE_GRAD", "1") == "0" else "all"
 FOLD_ACTS = () if _FOLD_ENV == "0" else (("relu", "gelu") if _FOLD_ENV == "all" else ("relu",))
 
 __all__ = [

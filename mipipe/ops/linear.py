@@ -167,6 +167,7 @@ class _Linear(torch.autograd.Function):
         fused_tile = _tile_ok(k, x2, w)
         seed = offset = 0
         preact = xt = None
+        saved_act = act  # the activation code the backward applies to the saved tensor
         ctx.has_res = res is not None
         if fused_tile:
             r2 = None
@@ -182,8 +183,13 @@ class _Linear(torch.autograd.Function):
             if (save and _EMIT_XT and x2.dtype == torch.bfloat16 and ctx.needs_input_grad[1]
                     and getattr(weight, "main_grad", None) is not None and k.gemm_emit_ok(act, p, act == 2)):
                 xt = torch.empty((x2.shape[1], x2.shape[0]), dtype=x2.dtype, device=x2.device)
-            # GELU's pre-activation is written only for a backward (not under no_grad)
-            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2, xt)
+            # GELU's saved tensor is written only for a backward (not under no_grad):
+            # GELU'(pre) itself on the bf16 path (aux_grad), so the backward --
+            # a separate pass or the consumer's dgrad epilogue -- is one multiply
+            aux_grad = _GELU_SAVE_GRAD and act == 2 and save and x2.dtype == torch.bfloat16
+            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2, xt, aux_grad)
+            if aux_grad:
+                saved_act = KACT_SAVED_GRAD
             res = None  # added in the epilogue
         else:
             y = torch.matmul(x2, w.t())
@@ -200,7 +206,7 @@ class _Linear(torch.autograd.Function):
         ctx.fold_out = ctx.fold_in = None
         fold_saved = None
         if fold_out is not None and fused_tile and act != 0 and x2.dtype == torch.bfloat16 and saved is not None:
-            fold_out.offer(act, saved, p, seed, offset)
+            fold_out.offer(saved_act, saved, p, seed, offset)
             ctx.fold_out = fold_out
         if fold_in is not None and fused_tile and fold_in.ready_for(x2) and ctx.needs_input_grad[0]:
             ctx.fold_in = fold_in
@@ -211,7 +217,7 @@ class _Linear(torch.autograd.Function):
         # x is kept for the weight gradient only: x^T replaces it when written
         ctx.x_is_t = xt is not None
         ctx.save_for_backward(xt if xt is not None else x2, w, bias, saved, fold_saved)
-        ctx.act, ctx.p, ctx.seed, ctx.offset = act, p, seed, offset
+        ctx.act, ctx.p, ctx.seed, ctx.offset = saved_act, p, seed, offset
         ctx.fused_tile = fused_tile
         ctx.in_shape = shape
         y = y.view(*shape[:-1], w.shape[0])
@@ -323,6 +329,9 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 _XT_MODE = os.environ.get("MIPIPE_WGRAD_XT", "auto")
 _EMIT_XT = _XT_MODE in ("1", "emit")
 _XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "6144"))
+# GELU forwards save GELU'(pre) rather than pre (MIPIPE_GELU_SAVE_GRAD=0: pre, for A/B runs)
+_GELU_SAVE_GRAD = os.environ.get("MIPIPE_GELU_SAVE_GRAD", "1") != "0"
+KACT_SAVED_GRAD = 3  # kernels.h kActSavedGrad
 
 
 def _defer(w: Tensor, dy: Tensor, x: Tensor, transposed: bool = False) -> None:

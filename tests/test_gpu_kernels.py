@@ -553,11 +553,14 @@ def test_linear_fwd_emits_x_transposed(k, M, N, K, bias, act):
 
 
 @pytest.mark.parametrize("N,Kin,T,nseg,bias", [
-    (12288, 4096, 256, 3, True),   # enc12 qkv widths: the bias fold (>= 16 tile rows)
+    (12288, 4096, 256, 3, True),   # enc12 qkv widths: the bias fold, 16-column slices (>= 8 tile rows)
     (520, 4096, 128, 5, True),     # edge columns of C^T
-    (1600, 1600, 1024, 4, True),   # GPT-2-XL: 7 tile rows (folds on 256x128 blocks)
-    (1600, 1600, 4096, 4, True),   # ... and with split-K (256-wide: 7 tile rows < 8, no fold)
+    (1600, 1600, 1024, 4, True),   # GPT-2-XL: 7 tile rows -> 32-column slices
+    (1600, 1600, 4096, 4, True),   # ... and with split-K
     (1600, 2048, 4096, 4, True),   # 8 tile rows, 56 tiles, K = 16384: the fold with split-K partials
+    (6400, 1600, 512, 2, True),    # GPT-2-XL fc1
+    (4800, 520, 256, 2, True),     # 3 tile rows (the last partial) -> 64-column slices
+    (600, 256, 192, 3, True),      # 1 tile row -> 128-column slices, edge tile column
     (6400, 1600, 512, 2, False),
     (1000, 4104, 128, 18, True),   # > 16 segments: two launches, the second accumulates
 ])
@@ -576,8 +579,8 @@ def test_wgrad_xt_segments(k, N, Kin, T, nseg, bias):
         fused = k.linear_wgrad_xt_segments(dys, xts, main, accumulate, bg)
         err = ((main - base - expect).abs().max() / expect.abs().max()).item()
         assert err < 1e-3, (N, Kin, T, nseg, accumulate, err)
-        if bias and Kin >= 4096:
-            assert fused  # the enc12 shapes always fold (>= 16 tile rows of C^T)
+        if bias:
+            assert fused  # the slices widen until the tile rows cover the tile column
         if bias and fused:
             ref = 0.5 + sum(d.float().sum(0) for d in dys)
             assert torch.allclose(bg, ref, atol=1e-2, rtol=1e-4), (bg - ref).abs().max()
@@ -805,31 +808,74 @@ def test_deferred_wgrad_op(k):
     assert err < 2e-2, err
 
 
-@pytest.mark.parametrize("act,p,T", [(2, 0.0, 512), (2, 0.1, 512), (1, 0.2, 512), (2, 0.1, 8192), (1, 0.0, 384)])
+@pytest.mark.parametrize("act,p,T", [(2, 0.0, 512), (2, 0.1, 512), (1, 0.2, 512), (2, 0.1, 8192), (1, 0.0, 384),
+                                     (3, 0.0, 512), (3, 0.1, 8192), (3, 0.1, 384)])
 def test_linear_dgrad_activation_backward_epilogue(k, act, p, T):
     """dgrad with the activation backward in the epilogue == (dy W) * mask * act'(saved):
-    the mask regenerated from the forward GEMM's Philox layout (big and 128x128 kernels)."""
+    the mask regenerated from the forward GEMM's Philox layout (big and 128x128 kernels).
+    act 3: a GELU forward that saved GELU'(pre) (aux_grad) and the one-multiply backward."""
     torch.manual_seed(30)
     E, F = 256, 1024
     x = torch.randn(T, E, device=DEV).to(torch.bfloat16)
     w1 = (torch.randn(F, E, device=DEV) * 0.05).to(torch.bfloat16)
     b1 = (torch.randn(F, device=DEV) * 0.1).to(torch.bfloat16)
     w2 = (torch.randn(E, F, device=DEV) * 0.05).to(torch.bfloat16)
-    y, pre, seed, offset = k.linear_fwd(x, w1, b1, act, p, act == 2)
-    saved = pre if act == 2 else y
+    fwd_act = 2 if act == 3 else act
+    y, saved_t, seed, offset = k.linear_fwd(x, w1, b1, fwd_act, p, fwd_act == 2, None, None, act == 3)
+    saved = saved_t if fwd_act == 2 else y
     dy = torch.randn(T, E, device=DEV).to(torch.bfloat16)
     got = k.linear_dgrad(dy, w2, None, None, act, saved, p, seed, offset)
     dh = dy.float() @ w2.float()
     keep = (y != 0).float()  # GELU output is 0 only where dropped
     scale = 1.0 / (1.0 - p) if p > 0 else 1.0
-    if act == 2:
-        s = pre.float()
-        grad = 0.5 * (1 + torch.erf(s / math.sqrt(2))) + s * torch.exp(-0.5 * s * s) / math.sqrt(2 * math.pi)
+    s = x.float() @ w1.float().t() + b1.float()  # the pre-activation, fp32
+    grad = 0.5 * (1 + torch.erf(s / math.sqrt(2))) + s * torch.exp(-0.5 * s * s) / math.sqrt(2 * math.pi)
+    if act == 3:
+        # the saved tensor is GELU'(pre) itself, to bf16 rounding
+        assert ((saved.float() - grad).abs().max()).item() < 2e-2
+        # the elementwise backward with the same code: dy * saved * mask
+        dpre, _ = k.bias_act_bwd(dh.to(torch.bfloat16), saved, None, 3, p, seed, offset, False)
+        ref_e = dh * keep * scale * grad
+        assert ((dpre.float() - ref_e).abs().max() / ref_e.abs().max()).item() < 2e-2
+    if act in (2, 3):
         ref = dh * keep * scale * grad
     else:
         ref = dh * keep * scale
     err = ((got.float() - ref).abs().max() / ref.abs().max()).item()
-    assert err < 1e-2, err
+    assert err < 2e-2 if act == 3 else 1e-2, err
+
+
+@pytest.mark.parametrize("norm_first", [True, False])
+def test_gelu_saved_grad_matches_saved_preactivation(k, norm_first):
+    """A GELU FeedForwardBlock trained with GELU'(pre) saved (default; folded into fc_out's
+    dgrad) gets the gradients of the pre-activation-saving path (unfolded elementwise GELU
+    backward), same dropout masks."""
+    import importlib
+
+    from mipipe.models.transformer import FeedForwardBlock
+
+    L = importlib.import_module("mipipe.ops.linear")
+    torch.manual_seed(33)
+    blk = FeedForwardBlock(256, 1024, 0.1, "gelu", norm_first=norm_first, device=DEV, dtype=torch.bfloat16)
+    x0 = torch.randn(4, 128, 256, device=DEV).to(torch.bfloat16)
+    grads = []
+    for save_grad in (True, False):
+        old = L._GELU_SAVE_GRAD
+        L._GELU_SAVE_GRAD = save_grad
+        try:
+            for prm in blk.parameters():
+                prm.grad = None
+            x = x0.clone().requires_grad_()
+            torch.cuda.manual_seed(6)
+            f = ActFold() if save_grad else None
+            h, xr = blk.fc_in.forward_fanout(x, True, f)
+            out = blk.fc_out(xr, h, f)
+            out.float().square().sum().backward()
+            grads.append([x.grad.float().clone()] + [prm.grad.float().clone() for prm in blk.parameters()])
+        finally:
+            L._GELU_SAVE_GRAD = old
+    for a, b in zip(*grads):
+        assert ((a - b).abs().max() / (b.abs().max() + 1e-12)).item() < 2e-2
 
 
 @pytest.mark.parametrize("activation,norm_first", [("relu", False), ("gelu", True), ("gelu", False)])

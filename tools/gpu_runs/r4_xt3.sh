@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py \
-  -k "transpose or xt_path or wgrad_xt or x_transposed" > gpurun_out/xt3_tests.log 2>&1 || { tail -40 gpurun_out/xt3_tests.log; exit 1; }
+  -k "transpose or xt_path or wgrad_xt or x_transposed or activation_backward or act_fold or gelu_saved or feedforward" > gpurun_out/xt3_tests.log 2>&1 || { tail -40 gpurun_out/xt3_tests.log; exit 1; }
 tail -2 gpurun_out/xt3_tests.log
 timeout -k 10 120 python -u tools/transpose_bw.py 2>&1 | tee gpurun_out/transpose_bw.txt
 val() { grep -o '"value": [0-9.]*' "$1" | head -1; }
