@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--no-bubble", action="store_true", help="skip the extra instrumented step")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = gloo + fp32 plumbing check of the multi-rank path (tests only)")
+    ap.add_argument("--plan", default="auto", choices=["auto", "analytic", "measured"],
+                    help="stage-plan unit costs: analytic FLOPs, or measured unit times (mipipe.parallel.calibrate: "
+                         "each unit kind timed on this GPU, all-reduced over the ranks; cached).  auto = measured "
+                         "on GPUs at PP > 1")
     ap.add_argument("--split-decoder", default="auto", choices=["auto", "on", "off"],
                     help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
@@ -168,11 +172,21 @@ def main() -> int:
     # backward / forward cost: 2, plus the recomputed forward of checkpointed micro-batches
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
     bwd_ratio = 2.0 + recompute
+    plan_mode = args.plan if args.plan != "auto" else ("measured" if on_gpu and pp > 1 else "analytic")
+    cost_fn = None
+    if plan_mode == "measured" and pp > 1:
+        from mipipe.parallel.calibrate import calibrated_times, unit_costs
+
+        unit_times = calibrated_times(cfg, mb, device=device, dtype=dtype, chunks=min(m, 4))
+        cost_fn = lambda split: unit_costs(cfg, unit_times, split, recompute)  # noqa: E731
     if args.virtual == "auto":
-        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb)
+        virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb,
+                                       cost_fn=cost_fn)
     else:
         virtual = int(args.virtual)
-        plan = plan_stages(cfg, pp, virtual, m, split_decoder=splits[-1] and pp > 1, bwd_ratio=bwd_ratio)
+        split = splits[-1] and pp > 1
+        plan = plan_stages(cfg, pp, virtual, m, split_decoder=split, bwd_ratio=bwd_ratio,
+                           costs=cost_fn(split) if cost_fn is not None else None)
     torch.manual_seed(1234 + prank)  # same initial weights in every data-parallel replica
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     from mipipe.models.long_skip import unet_pairs
@@ -351,6 +365,7 @@ def main() -> int:
                 "shared_gpu": bool(args.shared_gpu),
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
+                "plan_costs": "measured unit times" if cost_fn is not None else "analytic FLOPs",
             },
             "bubble_pct": None if bubble is None else round(bubble, 2),
             "work_note": (f"checkpoint={args.checkpoint!r} re-runs the forward of {stop_n} of {m} micro-batches: "

@@ -711,7 +711,7 @@ void py_linear_wgrad(Tensor dy, Tensor x, Tensor main_grad, bool accumulate) {
 // into a new contiguous [C, R] tensor: the K-contiguous operand of
 // linear_wgrad_xt_segments when the flush transposes x itself (ops/linear.py).
 Tensor py_transpose_b16(Tensor x) {
-  check_cuda(x, "x");
+  MP_CHECK(x.is_cuda(), "x must be a GPU tensor");
   MP_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.element_size() == 2, "transpose_b16: x must be 2-D, 2-byte, unit column stride");
   const int64_t R = x.size(0), C = x.size(1), ld = x.stride(0);
   MP_CHECK(R % 8 == 0 && C % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
@@ -1160,6 +1160,7 @@ PYBIND11_MODULE(_C, m) {
       .def("unlink", &ipc::Link::unlink)
       .def("describe", &ipc::Link::describe)
       .def_property_readonly("copy_stream", [](const ipc::Link& L) { return reinterpret_cast<int64_t>(L.copy_stream()); })
+      .def_property_readonly("inline_copy", &ipc::Link::inline_copy)
       .def_property_readonly("nslots", &ipc::Link::nslots)
       .def_property_readonly("slot_bytes", &ipc::Link::slot_bytes)
       .def_property_readonly("host_mode", &ipc::Link::host_mode)

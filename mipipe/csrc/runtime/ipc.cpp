@@ -314,17 +314,21 @@ uint64_t Link::send(const void* src, size_t bytes, hipStream_t producer, double 
     return s;
   }
   DeviceGuard g(device_);
-  rt::stream_wait(copy_stream_, producer, device_);
+  // inline engines (2, 3) run the whole send on the producer's stream: no
+  // cross-stream hop at all, the copy ordered behind the producer's later work
+  const bool in_line = engine_ >= 2;
+  hipStream_t cs = in_line ? producer : copy_stream_;
+  if (!in_line) rt::stream_wait(copy_stream_, producer, device_);
   if (s >= uint64_t(n))  // the slot's previous message released by the receiver's stream
-    check(hipStreamWaitValue64(copy_stream_, freed_ + int64_t(k) * kFlagStride, s - uint64_t(n) + 1,
+    check(hipStreamWaitValue64(cs, freed_ + int64_t(k) * kFlagStride, s - uint64_t(n) + 1,
                                hipStreamWaitValueGte, ~0ull),
           "hipStreamWaitValue64(freed)");
   if (bytes) {
-    if (engine_ == 1) rt::blit_copy(dst, src, bytes, copy_stream_);
-    else check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, copy_stream_), "hipMemcpyAsync(send)");
+    if (engine_ == 1 || engine_ == 2) rt::blit_copy(dst, src, bytes, cs);
+    else check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync(send)");
   }
-  check(hipStreamWriteValue64(copy_stream_, ring_ + int64_t(k) * kFlagStride, s + 1, 0), "hipStreamWriteValue64(full)");
-  check(hipEventRecord(events_[k], copy_stream_), "hipEventRecord(sent)");
+  check(hipStreamWriteValue64(cs, ring_ + int64_t(k) * kFlagStride, s + 1, 0), "hipStreamWriteValue64(full)");
+  check(hipEventRecord(events_[k], cs), "hipEventRecord(sent)");
   c.bytes = bytes;
   sh_->sent.store(s + 1, std::memory_order_release);
   ++next_seq_;

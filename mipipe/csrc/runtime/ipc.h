@@ -49,7 +49,9 @@ class Link {
   // device < 0: host mode (slots in shared memory).
   static std::unique_ptr<Link> create(const std::string& name, int device, int64_t nslots, int64_t slot_bytes);
   // Sender side: attaches to the receiver's block (waits up to `timeout_s`
-  // for it to appear).  engine: 0 = hipMemcpyAsync, 1 = blit kernel.
+  // for it to appear).  engine: 0 = hipMemcpyAsync, 1 = blit kernel, on the
+  // link's copy stream; 2 = blit kernel, 3 = hipMemcpyAsync, on the producer's
+  // stream itself (inline: no cross-stream dependency per message).
   static std::unique_ptr<Link> attach(const std::string& name, int device, int engine, double timeout_s);
   ~Link();
 
@@ -59,6 +61,8 @@ class Link {
   int64_t slot_bytes() const;
   // Copy stream of a sender (0 in host mode / on the receiver).
   hipStream_t copy_stream() const { return copy_stream_; }
+  // The sender copies on the producer's stream (engines 2, 3).
+  bool inline_copy() const { return sender_ && engine_ >= 2; }
 
   // Sender: enqueue message `bytes` from `src` after the work queued on
   // `producer` so far.  Never blocks the host in device mode (host mode:

@@ -50,7 +50,11 @@ from ..stream import record_stream
 
 __all__ = ["IpcChannels", "ENGINES"]
 
-ENGINES = {"sdma": 0, "blit": 1}
+# sdma / blit: the sender's copy on the link's own copy stream (overlaps the
+# producer's next kernels; two cross-stream dependencies per message);
+# inline / inline-sdma: the copy on the producer's stream (no cross-stream hop:
+# the lowest latency, ordered before the producer's later work)
+ENGINES = {"sdma": 0, "blit": 1, "inline": 2, "inline-sdma": 3}
 
 
 class _SendWork:
@@ -59,7 +63,7 @@ class _SendWork:
 
     def wait(self) -> bool:
         """Orders the current stream after the copy (the RCCL isend contract)."""
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and not self.link.inline_copy:  # inline: already on the producer's stream
             rt = _native_loader.kernels()
             rt.stream_wait(torch.cuda.current_stream(self.device).cuda_stream, self.link.copy_stream,
                            self.device.index)
@@ -233,7 +237,8 @@ class IpcChannels:
         if src.is_cuda:
             # the copy runs on the link's stream after the current one: keep the
             # source block alive until then
-            record_stream(src, self._copy_stream(link))
+            if not link.inline_copy:
+                record_stream(src, self._copy_stream(link))
             seq = link.send(src, torch.cuda.current_stream(src.device).cuda_stream, self.timeout)
         else:
             seq = link.send(src, 0, self.timeout)

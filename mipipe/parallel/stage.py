@@ -265,14 +265,19 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
 
 
 def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, split_decoder: bool = False,
-                bwd_ratio: float = 2.0) -> StagePlan:
+                bwd_ratio: float = 2.0, costs: Optional[List[float]] = None) -> StagePlan:
     """Plan for ``stages`` ranks with ``virtual`` chunks each (looping placement).
 
     With ``virtual > 1`` the split starts from the rank-total-balanced one and
     is refined against the simulated step time for ``chunks`` micro-batches
     (default 4 x stages): a chunk far larger than its neighbours stalls the
-    micro-batch flow even when rank totals are even."""
-    costs = block_costs(cfg, split_decoder)
+    micro-batch flow even when rank totals are even.  ``costs``: per-unit
+    costs to plan with instead of the analytic :func:`block_costs` (e.g.
+    measured ones, :mod:`mipipe.parallel.calibrate`)."""
+    if costs is None:
+        costs = block_costs(cfg, split_decoder)
+    elif len(costs) != len(block_costs(cfg, split_decoder)):
+        raise ValueError(f"{len(costs)} unit costs for {len(block_costs(cfg, split_decoder))} pipeline units")
     if stages * virtual > len(costs):
         raise ValueError(f"{stages} x {virtual} virtual stages exceed the {len(costs)} pipeline units")
     if virtual == 1:
@@ -405,16 +410,21 @@ ACHIEVED_FLOP_PER_S = 1.2e15
 LAUNCH_GAP_S = 30e-6
 
 
-def boundary_terms(cfg: LMConfig, micro_batch: Optional[int]) -> Tuple[float, float]:
-    """(transfer, launch) for :func:`simulate_step`, in per-token FLOP-equivalents."""
-    transfer = 2.0 * cfg.d_model / LINK_BYTES_PER_S * ACHIEVED_FLOP_PER_S
+def boundary_terms(cfg: LMConfig, micro_batch: Optional[int], unit: str = "flop") -> Tuple[float, float]:
+    """(transfer, launch) for :func:`simulate_step`: in per-token FLOP-equivalents
+    (``unit="flop"``, the analytic costs) or in ms per micro-batch (``"ms"``,
+    measured costs)."""
     tokens = (micro_batch or 8) * cfg.seq_len
+    if unit == "ms":
+        return 2.0 * cfg.d_model * tokens / LINK_BYTES_PER_S * 1e3, LAUNCH_GAP_S * 1e3
+    transfer = 2.0 * cfg.d_model / LINK_BYTES_PER_S * ACHIEVED_FLOP_PER_S
     return transfer, LAUNCH_GAP_S * ACHIEVED_FLOP_PER_S / tokens
 
 
 def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional[Sequence[int]] = None,
                    split_options: Sequence[bool] = (False, True), bwd_ratio: float = 2.0,
-                   micro_batch: Optional[int] = None, max_virtual: int = 8) -> Tuple[int, StagePlan]:
+                   micro_batch: Optional[int] = None, max_virtual: int = 8,
+                   cost_fn=None) -> Tuple[int, StagePlan]:
     """Chunks per rank (and whether to split the decoder) with the shortest
     simulated step; ties (within 0.5 %) keep the simpler plan.  ``bwd_ratio``
     is backward / forward cost (2, or 3 when every micro-batch is recomputed).
@@ -423,8 +433,10 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
     virtual stage at least one pipeline unit.  The simulation charges each
     stage-boundary message and each chunk action (:func:`boundary_terms`), so a
     deeper looping placement is chosen only when its shorter fill/drain pays
-    for its extra boundaries."""
-    transfer, launch = boundary_terms(cfg, micro_batch)
+    for its extra boundaries.  ``cost_fn(split_decoder)``: per-unit costs in ms
+    per micro-batch (measured, :mod:`mipipe.parallel.calibrate`) instead of
+    the analytic FLOP model."""
+    transfer, launch = boundary_terms(cfg, micro_batch, "ms" if cost_fn is not None else "flop")
 
     def sim(plan: StagePlan, v: int) -> float:
         return simulate_step([plan.stage_cost(g) for g in range(stages * v)], stages, v, chunks, bwd_ratio,
@@ -437,7 +449,7 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
     for split in split_options:
         if split and stages == 1:
             continue
-        costs = block_costs(cfg, split)
+        costs = cost_fn(split) if cost_fn is not None else block_costs(cfg, split)
         units = len(costs)
         cands = candidates if candidates is not None else range(1, max(1, min(max_virtual, units // stages)) + 1)
         for v in cands:
@@ -448,7 +460,8 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
     screened.sort()
     best = None
     for _, v, split in screened[:6]:
-        plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio)
+        plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio,
+                           costs=cost_fn(split) if cost_fn is not None else None)
         t = sim(plan, v)
         # ties (within 0.5 %) keep the simpler plan: fewer chunks, no split
         key = (v, split)

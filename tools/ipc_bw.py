@@ -13,6 +13,8 @@ engine's channel classes, ping-pong, and report the one-way time per message
   ranks queue the whole loop behind a GPU sleep first, so the timed part runs
   at the GPU's pace, not at Python's enqueue rate;
 * ``ipc-stream-blit`` -- ``ipc-stream`` with the blit-kernel copy engine;
+* ``ipc-stream-inline`` -- ``ipc-stream`` with the copy (blit) on the producer's
+  stream itself: no cross-stream dependency per message;
 * ``ipc-blit`` -- the ``ipc`` arm with the blit-kernel copy engine;
 * ``gloo``  -- :class:`mipipe.parallel.p2p.Channels` over gloo (host staging:
   D2H, TCP loopback, H2D) -- what multi-rank-on-one-GPU used before;
@@ -53,7 +55,8 @@ def _channels(kind, dev, max_bytes):
 
     if kind.startswith("ipc"):
         return IpcChannels([0, 1], device=dev, recv_bytes=max_bytes, slots=4, timeout=30.0,
-                           engine="blit" if kind.endswith("blit") else "sdma")
+                           engine="inline" if kind.endswith("inline") else ("blit" if kind.endswith("blit")
+                                                                            else "sdma"))
     ch = Channels([0, 1])
     ch.warmup(dev)
     return ch
@@ -88,7 +91,7 @@ def _worker(rank, ports, kinds, peer, iters, q, cpu=False):
                 if kind.startswith("ipc-stream"):
                     # back-to-back ping-pongs, zero-copy receives, no host wait; GPU-timed.
                     # The loop is queued behind a sleep so it runs at the GPU's pace.
-                    n_it = max(iters, 200)
+                    n_it = max(iters, 50)  # ~13 queue packets per iteration: stays within the HW queue
                     _sync(dev)
                     dist.barrier()
                     from mipipe._native_loader import kernels
@@ -115,6 +118,9 @@ def _worker(rank, ports, kinds, peer, iters, q, cpu=False):
                     if t_host > 0.25:
                         print(f"[rank {rank}] {kind}: queueing took {t_host:.3f} s, longer than the sleep: "
                               "the time below is host-bound", flush=True)
+                    elif mib == 1:
+                        print(f"[rank {rank}] {kind}: host enqueue {t_host / n_it * 1e6:.1f} us per ping-pong "
+                              "(all queued behind the sleep)", flush=True)
                     if rank == 0:
                         assert float(rx[-1]) == 0.0
                         one_way = e0.elapsed_time(e1) / 1e3 / n_it / 2
@@ -155,7 +161,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cpu", action="store_true", help="host-mode links (protocol check, no GPU)")
     args = ap.parse_args()
-    kinds = ["ipc-stream", "ipc-stream-blit", "ipc", "ipc-blit", "gloo"] + (["rccl"] if args.peer else [])
+    kinds = ["ipc-stream", "ipc-stream-blit", "ipc-stream-inline", "ipc", "ipc-blit", "gloo"] + (["rccl"] if args.peer else [])
     if args.cpu:
         kinds = ["ipc", "gloo"]
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")

@@ -82,6 +82,8 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--plan", default="analytic", choices=["analytic", "measured"],
+                    help="stage-plan unit costs: analytic FLOPs or measured unit times (mipipe.parallel.calibrate)")
     args = ap.parse_args()
     d_chunks, d_mb, d_ck = DEFAULTS[args.config]
     args.chunks = args.chunks or d_chunks
@@ -91,7 +93,17 @@ def main() -> int:
     cfg = CONFIGS[args.config]
     pp, m, mb = args.pp, args.chunks, args.micro_batch
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
-    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb)
+    cost_fn = None
+    if args.plan == "measured":
+        from mipipe.parallel.calibrate import calibrated_times, unit_costs
+
+        times = calibrated_times(cfg, mb, device=torch.device("cuda", 0), chunks=min(m, 4))
+        print("# measured unit times (fwd, bwd ms per micro-batch): "
+              + ", ".join(f"{k} {f:.2f}/{b:.2f}" for k, (f, b) in sorted(times.items())), flush=True)
+        cost_fn = lambda split: unit_costs(cfg, times, split, recompute)  # noqa: E731
+    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb, cost_fn=cost_fn)
+    print(f"# plan ({args.plan} costs): v={virtual}, split head {plan.split_decoder}, balance {plan.balance}",
+          flush=True)
     if args.ranks:
         ranks = list(range(pp)) if args.ranks == "all" else [int(r) for r in args.ranks.split(",")]
     else:
@@ -112,6 +124,9 @@ def main() -> int:
         bub = 1.0 - max(sim_busy) / sim_t  # the slowest rank's idle share
         est = walls[slow] * (1.0 + bub)
         tokens = m * mb * cfg.seq_len
+        fastest = min(walls.values())
+        print(f"# per-rank wall spread: {fastest:.1f} .. {walls[slow]:.1f} ms = "
+              f"{100 * (walls[slow] / fastest - 1):.1f} % ({args.plan} plan costs)")
         print(f"# slowest rank {slow}: {walls[slow]:.1f} ms/step; planner-simulated bubble {100 * bub:.1f} % -> "
               f"PP={pp} step ~{est:.1f} ms = {tokens / est * 1e3:,.0f} tokens/s for the job "
               f"({m} x {mb} x {cfg.seq_len} tokens per step)")
