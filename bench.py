@@ -73,9 +73,9 @@ def parse():
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = gloo + fp32 plumbing check of the multi-rank path (tests only)")
     ap.add_argument("--plan", default="auto", choices=["auto", "analytic", "measured"],
-                    help="stage-plan unit costs: analytic FLOPs, or measured unit times (mipipe.parallel.calibrate: "
-                         "each unit kind timed on this GPU, all-reduced over the ranks; cached).  auto = measured "
-                         "on GPUs at PP > 1")
+                    help="stage-plan unit costs: analytic FLOPs, or measured (mipipe.parallel.calibrate: layer / head / "
+                         "tail stages timed in the engine on this GPU, all-reduced over the ranks; cached).  auto = "
+                         "measured on GPUs at PP > 1")
     ap.add_argument("--split-decoder", default="auto", choices=["auto", "on", "off"],
                     help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
@@ -172,13 +172,15 @@ def main() -> int:
     # backward / forward cost: 2, plus the recomputed forward of checkpointed micro-batches
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
     bwd_ratio = 2.0 + recompute
-    plan_mode = args.plan if args.plan != "auto" else ("measured" if on_gpu and pp > 1 else "analytic")
+    # measured by default on GPUs at PP > 1 (not in the one-GPU rehearsal: its ranks would time each other)
+    plan_mode = args.plan if args.plan != "auto" else ("measured" if on_gpu and pp > 1 and not args.shared_gpu
+                                                       else "analytic")
     cost_fn = None
     if plan_mode == "measured" and pp > 1:
-        from mipipe.parallel.calibrate import calibrated_times, unit_costs
+        from mipipe.parallel.calibrate import calibrated_costs, engine_unit_costs
 
-        unit_times = calibrated_times(cfg, mb, device=device, dtype=dtype, chunks=min(m, 4))
-        cost_fn = lambda split: unit_costs(cfg, unit_times, split, recompute)  # noqa: E731
+        unit_ms = calibrated_costs(cfg, mb, m, args.checkpoint, device=device, dtype=dtype)
+        cost_fn = lambda split: engine_unit_costs(cfg, unit_ms, split)  # noqa: E731
     if args.virtual == "auto":
         virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb,
                                        cost_fn=cost_fn)
@@ -365,7 +367,7 @@ def main() -> int:
                 "shared_gpu": bool(args.shared_gpu),
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
-                "plan_costs": "measured unit times" if cost_fn is not None else "analytic FLOPs",
+                "plan_costs": "measured (engine-context unit costs)" if cost_fn is not None else "analytic FLOPs",
             },
             "bubble_pct": None if bubble is None else round(bubble, 2),
             "work_note": (f"checkpoint={args.checkpoint!r} re-runs the forward of {stop_n} of {m} micro-batches: "

@@ -4,24 +4,33 @@ The reference points its users at profile-driven balancing: time every layer of
 the model on a sample batch and split by the measured times
 (``/root/reference/pipe.py:42-58``, ``torchgpipe.balance.balance_by_time``).
 The engine's planner (:mod:`mipipe.parallel.stage`) prices pipeline units with
-an analytic FLOP model; this module replaces that model with GPU times:
+an analytic FLOP model; this module replaces that model with GPU times, in two
+layers:
 
-* every DISTINCT unit kind of the model (embedding, attention core, attention
-  output, MLP halves, final norm, decoder or its two vocabulary halves) is
-  built once -- one unit, never the model -- with the flat optimizer's
-  ``main_grad`` buffers, and run for ``chunks`` micro-batches of the real
-  shape: forwards timed alone, then forward + backward inside
-  ``deferred_wgrad`` (the weight gradients as ONE K-segmented GEMM per weight,
-  as the engine flushes them), so ``bwd = (fwd+bwd) - fwd`` includes the
-  batched weight-gradient cost;
-* a unit's cost is ``fwd x (1 + recompute share) + bwd`` in ms per
-  micro-batch, the recomputed forward of checkpointed micro-batches included;
-* with a process group up, the times are averaged over the ranks
-  (``all_reduce``) so every rank derives the same plan from the same numbers;
-* results are cached as JSON under ``$MIPIPE_CALIB_DIR`` (default
-  ``~/.cache/mipipe/calibration``), keyed by model, micro-batch, dtype, device
-  name and the native-source digest, and the tables measured on MI355X for the
-  BASELINE configs ship in ``mipipe/parallel/calibration/``.
+* :func:`measure_unit_times` -- every DISTINCT unit kind (embedding, attention
+  core, attention output, MLP halves, final norm, decoder or its two
+  vocabulary halves) built once, alone, with the flat optimizer's
+  ``main_grad`` buffers, and run for a few micro-batches: forwards timed
+  alone, then forward + backward inside ``deferred_wgrad``.  Cheap, but a unit
+  run by itself is priced with the host overhead and launch gaps the engine
+  hides behind longer kernels: on the PP=8 rank emulations these costs put the
+  ranks' measured step times 36-38 % apart (profiles/pp_planning_r4.txt);
+* :func:`measure_engine_costs` -- what the planner uses: the real
+  :class:`~mipipe.parallel.engine.PipelineEngine` (one process, loop-back
+  channels, as ``tools/pp_rank_emulation.py`` runs a rank) on synthetic
+  stages -- two whole layers in the middle of the pipeline, the embedding +
+  one layer at its head, one layer + final norm + decoder (or its vocabulary
+  halves) at its tail -- with the configured micro-batch count, checkpoint
+  mode and optimizer step.  Differences of the stage times give a layer, the
+  embedding and the decoder end in engine context; the layer is split into
+  its four units in the proportions the per-unit times give.
+
+Costs are ms per micro-batch.  With a process group up every rank measures and
+the costs are averaged (``all_reduce``), so all ranks derive one plan.  Results
+are cached as JSON under ``$MIPIPE_CALIB_DIR`` (default
+``~/.cache/mipipe/calibration``), keyed by model, micro-batch, chunks,
+checkpoint mode, dtype and device name, and valid for the native sources they
+were measured with.
 """
 from __future__ import annotations
 
@@ -35,9 +44,8 @@ import torch.distributed as dist
 
 from ..models.lm import LMConfig
 
-__all__ = ["unit_kinds", "measure_unit_times", "unit_costs", "calibrated_times", "cache_key"]
-
-SHIPPED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "calibration")
+__all__ = ["unit_kinds", "measure_unit_times", "unit_costs", "measure_engine_costs", "engine_unit_costs",
+           "calibrated_costs", "cache_key"]
 
 
 def unit_kinds(cfg: LMConfig, split_decoder: bool = False) -> List[str]:
@@ -62,9 +70,10 @@ def _digest() -> str:
         return "na"
 
 
-def cache_key(cfg: LMConfig, micro_batch: int, dtype: torch.dtype, device: torch.device, chunks: int) -> str:
+def cache_key(cfg: LMConfig, micro_batch: int, dtype: torch.dtype, device: torch.device, chunks: int,
+              checkpoint: str = "never") -> str:
     dt = str(dtype).replace("torch.", "")
-    return f"{cfg.name}-mb{micro_batch}-m{chunks}-{dt}-{_device_name(device)}"
+    return f"{cfg.name}-mb{micro_batch}-m{chunks}-{checkpoint}-{dt}-{_device_name(device)}"
 
 
 def _single_unit_plan(cfg: LMConfig, split_decoder: bool):
@@ -178,6 +187,140 @@ def unit_costs(cfg: LMConfig, times: Dict[str, Tuple[float, float]], split_decod
     return [times[k][0] * (1.0 + recompute) + times[k][1] for k in unit_kinds(cfg, split_decoder)]
 
 
+class _Done:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+class Loopback:
+    """Channels stand-in for one rank run alone: every transfer completes at
+    once, no bytes move (receive buffers keep whatever they hold)."""
+
+    host_staged = False
+
+    def __init__(self, rank: int, world: int) -> None:
+        self.rank, self.world, self.ranks = rank, world, list(range(world))
+
+    def warmup(self, device) -> None:
+        pass
+
+    def send_act(self, t):
+        return _Done()
+
+    recv_act = send_grad = recv_grad = send_act
+
+
+def _range_stage(cfg: LMConfig, a: int, b: int, split_decoder: bool, *, device, dtype):
+    """The stage of pipeline units [a, b) and its input shape (per micro-batch: filled in by the caller)."""
+    from .stage import StagePlan, block_costs, build_stage
+
+    n = len(block_costs(cfg, split_decoder))
+    bal = ([a] if a else []) + [b - a] + ([n - b] if b < n else [])
+    plan = StagePlan(bal, [0.0] * n, 1, split_decoder)
+    vs = 1 if a else 0
+    return build_stage(cfg, plan, vs, device=device, dtype=dtype).train(), plan, vs, n
+
+
+def _engine_step_ms(cfg: LMConfig, a: int, b: int, split_decoder: bool, micro_batch: int, chunks: int,
+                    checkpoint: str, *, device, dtype, steps: int = 3) -> float:
+    """Median wall time (ms) of one engine step + optimizer step of the stage
+    made of units [a, b), run as the head / middle / tail rank of a pipeline."""
+    from .. import ops
+    from ..optim import FlatAdam
+    from .engine import PipelineEngine
+    from .stage import stage_input_shape
+
+    stage, plan, vs, n = _range_stage(cfg, a, b, split_decoder, device=device, dtype=dtype)
+    first, last = a == 0, b == n
+    rank, world = (0, 1) if first and last else ((0, 2) if first else ((1, 2) if last else (1, 3)))
+    S, V = cfg.seq_len, cfg.vocab
+    opt = FlatAdam(list(stage.parameters()), lr=1e-6, max_grad_norm=1.0)
+
+    def loss_fn(y, t):
+        return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
+
+    engine = PipelineEngine([stage], chunks=chunks, checkpoint=checkpoint,
+                            act_shape=[stage_input_shape(cfg, plan, vs, micro_batch)], act_dtype=dtype,
+                            loss_fn=loss_fn if last else None, group=Loopback(rank, world), device=device,
+                            skip_routes={})
+    g = torch.Generator(device="cpu").manual_seed(a)
+    tokens = torch.randint(0, V, (chunks, micro_batch, S + 1), generator=g)
+    inputs = [tokens[i, :, :S].to(device) for i in range(chunks)] if first else None
+    targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(chunks)]
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    def step():
+        opt.zero_grad()
+        engine.step(inputs, targets)
+        opt.step(opt.grad_sumsq())
+
+    step()
+    walls = []
+    for _ in range(steps):
+        sync()
+        t0 = time.perf_counter()
+        step()
+        sync()
+        walls.append((time.perf_counter() - t0) * 1e3)
+    del engine, opt, stage
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    return sorted(walls)[len(walls) // 2]
+
+
+LAYER_KINDS = ("core", "out", "mlp_in", "mlp_out")
+
+
+def measure_engine_costs(cfg: LMConfig, micro_batch: int, chunks: int, checkpoint: str = "never", *,
+                         device: torch.device, dtype: torch.dtype = torch.bfloat16,
+                         steps: int = 3) -> Dict[str, float]:
+    """``{kind: ms per micro-batch}`` in engine context (module docstring):
+    checkpoint recompute, the deferred weight-gradient flush, the optimizer
+    step and the host's issue overhead included as a pipeline rank pays them."""
+    from .stage import UNITS_PER_LAYER, block_costs
+
+    device = torch.device(device)
+    if cfg.num_layers < 3:
+        raise ValueError("engine-context calibration needs >= 3 layers")
+    iso = measure_unit_times(cfg, micro_batch, chunks=min(chunks, 4), device=device, dtype=dtype,
+                             kinds=LAYER_KINDS + ("norm", "dec", "dec_head", "dec_tail"))
+    rec = {"never": 0.0, "except_last": (chunks - 1) / chunks, "always": 1.0}[checkpoint]
+    iso_cost = {k: f * (1.0 + rec) + b for k, (f, b) in iso.items()}
+    per = lambda ms: ms / chunks  # noqa: E731  -- per micro-batch
+    run = lambda a, b, split=False: per(_engine_step_ms(cfg, a, b, split, micro_batch, chunks, checkpoint,  # noqa: E731
+                                                        device=device, dtype=dtype, steps=steps))
+    L = UNITS_PER_LAYER
+    layer = run(1, 1 + 2 * L) / 2.0
+    out = {"enc": max(run(0, 1 + L) - layer, 0.0)}
+    tot = sum(iso_cost[k] for k in LAYER_KINDS)
+    for k in LAYER_KINDS:
+        out[k] = layer * iso_cost[k] / tot
+    norm = 1 if cfg.norm_first else 0
+    n = len(block_costs(cfg, False))
+    end = max(run(n - 1 - norm - L, n) - layer, 0.0)  # norm + decoder
+    if norm:
+        share = iso_cost["norm"] / (iso_cost["norm"] + iso_cost["dec"])
+        out["norm"], out["dec"] = end * share, end * (1 - share)
+    else:
+        out["dec"] = end
+    ns = len(block_costs(cfg, True))
+    tail = run(ns - 1, ns, True)
+    head = max(run(ns - 2 - norm - L, ns - 1, True) - layer - out.get("norm", 0.0), 0.0)
+    out["dec_head"], out["dec_tail"] = head, tail
+    return out
+
+
+def engine_unit_costs(cfg: LMConfig, costs: Dict[str, float], split_decoder: bool = False) -> List[float]:
+    """Per-unit cost list for the planner from :func:`measure_engine_costs`."""
+    return [costs[k] for k in unit_kinds(cfg, split_decoder)]
+
+
 def _load(path: str) -> Optional[dict]:
     try:
         with open(path) as f:
@@ -186,53 +329,49 @@ def _load(path: str) -> Optional[dict]:
         return None
 
 
-def calibrated_times(cfg: LMConfig, micro_batch: int, *, device: torch.device, dtype: torch.dtype = torch.bfloat16,
-                     chunks: int = 4, refresh: bool = False, use_shipped: bool = True,
-                     group=None) -> Dict[str, Tuple[float, float]]:
-    """Unit times from the cache (or the shipped table for this device), else
-    measured -- and then identical on every rank of ``group`` (default: the
-    world, when initialised): each rank measures, the times are averaged with
-    one ``all_reduce``; a cache hit on one rank is used only if every rank hit
-    the same table (an all-reduced flag), so plans never diverge."""
+def calibrated_costs(cfg: LMConfig, micro_batch: int, chunks: int, checkpoint: str = "never", *,
+                     device: torch.device, dtype: torch.dtype = torch.bfloat16, refresh: bool = False,
+                     group=None, measure=None) -> Dict[str, float]:
+    """Engine-context unit costs (:func:`measure_engine_costs`, or ``measure()``)
+    from the cache or measured -- and then identical on every rank of
+    ``group`` (default: the world, when initialised): each rank measures on its
+    own GPU and the costs are averaged with one ``all_reduce``; a cached table
+    is used only if every rank has one (an all-reduced flag), so plans never
+    diverge."""
     device = torch.device(device)
-    key = cache_key(cfg, micro_batch, dtype, device, chunks)
+    key = cache_key(cfg, micro_batch, dtype, device, chunks, checkpoint)
     cache_dir = os.environ.get("MIPIPE_CALIB_DIR", os.path.join(os.path.expanduser("~"), ".cache", "mipipe",
                                                                 "calibration"))
     found = None
     if not refresh:
-        for d in ([cache_dir] + ([SHIPPED] if use_shipped else [])):
-            rec = _load(os.path.join(d, key + ".json"))
-            if rec is not None and rec.get("digest") in (_digest(), "any"):
-                found = rec
-                break
-    kinds = sorted(set(unit_kinds(cfg, False)) | set(unit_kinds(cfg, True)))
+        rec = _load(os.path.join(cache_dir, key + ".json"))
+        if rec is not None and rec.get("digest") == _digest():
+            found = rec
     distributed = dist.is_available() and dist.is_initialized()
+    nccl = distributed and dist.get_backend(group) == "nccl"
     if distributed:
-        # every rank must take the same branch: measure unless ALL found a table
-        # (tables could still differ between ranks: averaged below like measurements)
-        flag = torch.tensor([0.0 if found is not None else 1.0])
-        if dist.get_backend(group) == "nccl":
-            flag = flag.to(device)
+        # every rank takes the same branch: measure unless ALL ranks found a table
+        flag = torch.tensor([0.0 if found is not None else 1.0], device=device if nccl else "cpu")
         dist.all_reduce(flag, group=group)
         if flag.item() > 0:
             found = None
     if found is not None:
-        times = {k: tuple(v) for k, v in found["times"].items()}
+        costs = {k: float(v) for k, v in found["costs"].items()}
+    elif measure is not None:
+        costs = measure()
     else:
-        times = measure_unit_times(cfg, micro_batch, chunks=chunks, device=device, dtype=dtype, kinds=kinds)
+        costs = measure_engine_costs(cfg, micro_batch, chunks, checkpoint, device=device, dtype=dtype)
     if distributed:
-        vec = torch.tensor([times[k][j] for k in kinds for j in (0, 1)], dtype=torch.float64)
-        if dist.get_backend(group) == "nccl":
-            vec = vec.to(device)
+        kinds = sorted(costs)
+        vec = torch.tensor([costs[k] for k in kinds], dtype=torch.float64, device=device if nccl else "cpu")
         dist.all_reduce(vec, group=group)
         vec = (vec / dist.get_world_size(group)).cpu().tolist()
-        times = {k: (vec[2 * i], vec[2 * i + 1]) for i, k in enumerate(kinds)}
+        costs = dict(zip(kinds, vec))
     if found is None and (not distributed or dist.get_rank() == 0):
         try:
             os.makedirs(cache_dir, exist_ok=True)
             with open(os.path.join(cache_dir, key + ".json"), "w") as f:
-                json.dump({"key": key, "digest": _digest(), "chunks": chunks,
-                           "times": {k: list(v) for k, v in times.items()}}, f, indent=1, sort_keys=True)
+                json.dump({"key": key, "digest": _digest(), "costs": costs}, f, indent=1, sort_keys=True)
         except OSError:
             pass
-    return times
+    return costs

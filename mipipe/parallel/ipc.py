@@ -38,6 +38,7 @@ rank's incoming-message size and shares a job-unique name prefix).
 """
 from __future__ import annotations
 
+import os
 import uuid
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -128,8 +129,8 @@ class IpcChannels:
         slots: messages in flight per link (default: 64).  The engine passes
             ``chunks x virtual`` so every message of a step has its own slot:
             a slot read in place is released only at :meth:`end_step`.
-        engine: ``"sdma"`` (DMA engines) or ``"blit"`` (copy kernel) for the
-            sender's copy.
+        engine: the sender's copy (:data:`ENGINES`); default ``$MIPIPE_IPC_ENGINE``
+            or ``"sdma"``.
         timeout: seconds a host-mode wait may block before it raises (the
             engine's watchdog usually fires first).
     """
@@ -137,7 +138,8 @@ class IpcChannels:
     host_staged = False
 
     def __init__(self, ranks: Sequence[int], wrap: bool = False, *, device: torch.device, recv_bytes: int,
-                 slots: int = 64, engine: str = "sdma", timeout: float = 300.0) -> None:
+                 slots: int = 64, engine: Optional[str] = None, timeout: float = 300.0) -> None:
+        engine = engine or os.environ.get("MIPIPE_IPC_ENGINE", "sdma")
         if engine not in ENGINES:
             raise ValueError(f"engine must be one of {sorted(ENGINES)}, got {engine!r}")
         k = _native_loader.kernels()

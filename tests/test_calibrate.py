@@ -1,7 +1,10 @@
 """Measured-cost stage planning (mipipe.parallel.calibrate): unit kinds timed on
-the CPU here (the same code times them on the GPU in bench.py --plan measured),
-costs fed to the planner, and every rank of a gloo group deriving the same
-numbers -- hence the same plan -- whether measured or read from the cache."""
+the CPU here -- alone, and in engine context (head / middle / tail stages run by
+the PipelineEngine over loop-back channels; the same code times them on the GPU
+in bench.py --plan measured) -- costs fed to the planner, and every rank of a
+gloo group deriving the same numbers, hence the same plan, whether measured or
+read from the cache."""
+import dataclasses
 import os
 import socket
 
@@ -11,7 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from mipipe.models import CONFIGS
-from mipipe.parallel.calibrate import calibrated_times, measure_unit_times, unit_costs, unit_kinds
+from mipipe.parallel.calibrate import (calibrated_costs, engine_unit_costs, measure_engine_costs, measure_unit_times,
+                                       unit_costs, unit_kinds)
 from mipipe.parallel.stage import block_costs, choose_virtual, plan_stages
 
 CPU = torch.device("cpu")
@@ -45,34 +49,50 @@ def test_measure_unit_times_cpu():
     assert plan.ranks == 2 and plan.virtual == v
 
 
+def _cfg3():
+    return dataclasses.replace(CONFIGS["tiny"], num_layers=3)
+
+
+def test_measure_engine_costs_cpu():
+    cfg = _cfg3()
+    costs = measure_engine_costs(cfg, 2, 4, "except_last", device=CPU, dtype=torch.float32, steps=1)
+    kinds = set(unit_kinds(cfg, False)) | set(unit_kinds(cfg, True))
+    assert kinds <= set(costs)
+    assert all(c >= 0 for c in costs.values()) and costs["dec"] > 0 and costs["core"] > 0
+    for split in (False, True):
+        plan = plan_stages(cfg, 2, 1, 4, split, costs=engine_unit_costs(cfg, costs, split))
+        assert sum(plan.balance) == len(block_costs(cfg, split))
+
+
 def _worker(rank, port, cache, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MIPIPE_CALIB_DIR=cache)
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
-        cfg = CONFIGS["tiny"]
+        cfg = _cfg3()
         out = []
         for refresh in (True, False):  # measured (and cached by rank 0), then read back
-            times = calibrated_times(cfg, 2, device=CPU, dtype=torch.float32, chunks=2, refresh=refresh,
-                                     use_shipped=False)
-            v, plan = choose_virtual(cfg, 2, 4, micro_batch=2, cost_fn=lambda s: unit_costs(cfg, times, s, 0.0))
-            out.append((sorted(times.items()), v, plan.balance, plan.split_decoder))
+            costs = calibrated_costs(cfg, 2, 4, "never", device=CPU, dtype=torch.float32, refresh=refresh,
+                                     measure=lambda: measure_engine_costs(cfg, 2, 4, device=CPU,
+                                                                          dtype=torch.float32, steps=1))
+            v, plan = choose_virtual(cfg, 2, 4, micro_batch=2, cost_fn=lambda s: engine_unit_costs(cfg, costs, s))
+            out.append((sorted(costs.items()), v, plan.balance, plan.split_decoder))
             dist.barrier()  # rank 0's cache file exists before the second round
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-def test_calibrated_times_agree_across_ranks(tmp_path):
+def test_calibrated_costs_agree_across_ranks(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path), q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = dict(q.get(timeout=300) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0] == res[1]  # same times (all-reduced), same plan, in both rounds
+    assert res[0] == res[1]  # same costs (all-reduced), same plan, in both rounds
     assert res[0][0] == res[0][1]  # the cached table is what was measured
     assert len(list(tmp_path.iterdir())) == 1

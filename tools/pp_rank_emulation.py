@@ -33,39 +33,10 @@ from mipipe import ops  # noqa: E402
 from mipipe.models import CONFIGS  # noqa: E402
 from mipipe.optim import FlatAdam  # noqa: E402
 from mipipe.parallel import PipelineEngine  # noqa: E402
-from mipipe.parallel.p2p import Channels  # noqa: E402
 from mipipe.parallel.stage import build_stage, choose_virtual, stage_input_shape  # noqa: E402
 
 
-class _Done:
-    def wait(self):
-        return True
-
-    def is_completed(self):
-        return True
-
-
-class Loopback(Channels):
-    """Channels stand-in: every transfer completes at once (no bytes move)."""
-
-    def __init__(self, rank: int, world: int) -> None:  # no process groups
-        self.rank, self.world, self.ranks = rank, world, list(range(world))
-        self.host_staged = False
-
-    def warmup(self, device) -> None:  # nothing to connect
-        pass
-
-    def send_act(self, t):
-        return _Done()
-
-    def recv_act(self, t):
-        return _Done()
-
-    def send_grad(self, t):
-        return _Done()
-
-    def recv_grad(self, t):
-        return _Done()
+from mipipe.parallel.calibrate import Loopback  # noqa: E402
 
 
 # per-config defaults: BASELINE.json's PP=8 configs (#3 enc12 chunks 32 except_last, #4 GPT-2-XL chunks 8 always)
@@ -95,12 +66,13 @@ def main() -> int:
     recompute = {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[args.checkpoint]
     cost_fn = None
     if args.plan == "measured":
-        from mipipe.parallel.calibrate import calibrated_times, unit_costs
+        from mipipe.parallel.calibrate import calibrated_costs, engine_unit_costs
 
-        times = calibrated_times(cfg, mb, device=torch.device("cuda", 0), chunks=min(m, 4))
-        print("# measured unit times (fwd, bwd ms per micro-batch): "
-              + ", ".join(f"{k} {f:.2f}/{b:.2f}" for k, (f, b) in sorted(times.items())), flush=True)
-        cost_fn = lambda split: unit_costs(cfg, times, split, recompute)  # noqa: E731
+        t0 = time.perf_counter()
+        costs = calibrated_costs(cfg, mb, m, args.checkpoint, device=torch.device("cuda", 0))
+        print(f"# measured engine-context unit costs (ms per micro-batch, {time.perf_counter() - t0:.1f} s): "
+              + ", ".join(f"{k} {c:.3f}" for k, c in sorted(costs.items())), flush=True)
+        cost_fn = lambda split: engine_unit_costs(cfg, costs, split)  # noqa: E731
     virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb, cost_fn=cost_fn)
     print(f"# plan ({args.plan} costs): v={virtual}, split head {plan.split_decoder}, balance {plan.balance}",
           flush=True)
