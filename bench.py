@@ -76,6 +76,9 @@ def parse():
                     help="stage-plan unit costs: analytic FLOPs, or measured (mipipe.parallel.calibrate: layer / head / "
                          "tail stages timed in the engine on this GPU, all-reduced over the ranks; cached).  auto = "
                          "measured on GPUs at PP > 1")
+    ap.add_argument("--plan-objective", default="makespan", choices=["makespan", "balance"],
+                    help="stage plan: shortest simulated step (may load ranks unevenly to shorten fill / drain) "
+                         "or the most even per-rank work")
     ap.add_argument("--split-decoder", default="auto", choices=["auto", "on", "off"],
                     help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
@@ -183,12 +186,12 @@ def main() -> int:
         cost_fn = lambda split: engine_unit_costs(cfg, unit_ms, split)  # noqa: E731
     if args.virtual == "auto":
         virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb,
-                                       cost_fn=cost_fn)
+                                       cost_fn=cost_fn, objective=args.plan_objective)
     else:
         virtual = int(args.virtual)
         split = splits[-1] and pp > 1
         plan = plan_stages(cfg, pp, virtual, m, split_decoder=split, bwd_ratio=bwd_ratio,
-                           costs=cost_fn(split) if cost_fn is not None else None)
+                           costs=cost_fn(split) if cost_fn is not None else None, objective=args.plan_objective)
     torch.manual_seed(1234 + prank)  # same initial weights in every data-parallel replica
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     from mipipe.models.long_skip import unet_pairs

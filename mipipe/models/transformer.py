@@ -38,13 +38,13 @@ FANOUT = os.environ.get("MIPIPE_FANOUT", "1") != "0"
 # the activations in FOLD_ACTS.  ReLU's backward is a sign test on the saved
 # output, nearly free in the epilogue (enc12 FFN dgrad + act backward 240 -> 222
 # us).  GELU's is one multiply as well when its forward saves GELU'(pre)
-# (ops.linear MIPIPE_GELU_SAVE_GRAD, the default); with pre saved instead, the
+# (ops.linear MIPIPE_GELU_SAVE_GRAD=1, not the default); with pre saved, the
 # erf/exp per element made the epilogue slower than the separate memory-bound
 # kernel (GPT-2-XL fc2 dgrad 244 -> 251 us; tools/gemm_dact_probe.py), so GELU
 # is then not folded.  MIPIPE_FOLD_ACT=0: off, =relu: ReLU only, =all: both.
 _FOLD_ENV = os.environ.get("MIPIPE_FOLD_ACT", "auto")
 if _FOLD_ENV == "auto":
-    _FOLD_ENV = "relu" if os.environ.get("MIPIPE_GELU_SAVE_GRAD", "1") == "0" else "all"
+    _FOLD_ENV = "all" if os.environ.get("MIPIPE_GELU_SAVE_GRAD", "0") == "1" else "relu"
 FOLD_ACTS = () if _FOLD_ENV == "0" else (("relu", "gelu") if _FOLD_ENV == "all" else ("relu",))
 
 

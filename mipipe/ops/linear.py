@@ -320,8 +320,8 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 # (C^T = X^T . dY, ~15 % faster than reading both operands I-contiguous:
 # profiles/wgrad_layout_probe.txt) comes from -- MIPIPE_WGRAD_XT:
 #   auto (default): the flush transposes x (transpose_b16, a streaming kernel)
-#        for weights with at least _XT_MIN_N output features, where the GEMM
-#        saving outgrows the transpose (~N_out / 4000 x its cost);
+#        for weights with at least _XT_MIN_N output features and >= 512 tiles,
+#        where the GEMM saving outgrows the transpose (~N_out / 3600 x its cost);
 #   emit: the forward GEMM writes x^T from its staged A tiles (every tile-path
 #        linear; +x^T bytes of activation memory, and ~40 us per forward GEMM:
 #        a wash on enc12, profiles/wgrad_xt_ab.txt);
@@ -329,8 +329,12 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 _XT_MODE = os.environ.get("MIPIPE_WGRAD_XT", "auto")
 _EMIT_XT = _XT_MODE in ("1", "emit")
 _XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "6144"))
-# GELU forwards save GELU'(pre) rather than pre (MIPIPE_GELU_SAVE_GRAD=0: pre, for A/B runs)
-_GELU_SAVE_GRAD = os.environ.get("MIPIPE_GELU_SAVE_GRAD", "1") != "0"
+# GELU forwards save GELU'(pre) rather than pre (MIPIPE_GELU_SAVE_GRAD=1).  Off by
+# default: the second erf/exp per element in the forward GEMM's epilogue cost the
+# GPT-2-XL step more than the one-multiply backward saved (the elementwise GELU
+# backward is memory-bound either way: 157 -> 149 us); it pays where the
+# backward folds into the consumer's dgrad (GELU without dropout after it).
+_GELU_SAVE_GRAD = os.environ.get("MIPIPE_GELU_SAVE_GRAD", "0") == "1"
 KACT_SAVED_GRAD = 3  # kernels.h kActSavedGrad
 
 
@@ -465,6 +469,10 @@ def _transpose_pays(w: Tensor, dys, xs, T: int) -> bool:
     """The flush transposes x for the transposed GEMM (MIPIPE_WGRAD_XT=auto):
     wide enough outputs, bf16, shapes the transpose and the GEMM accept."""
     if _XT_MODE != "auto" or w.shape[0] < _XT_MIN_N or T % 64 != 0:
+        return False
+    # grids of < 2 rounds of 256x256 tiles run split-K and quantise the same in
+    # either layout (GPT-2-XL fc1: 175 tiles, 1454 vs 1461 us): no gain to pay for
+    if ((w.shape[1] + 255) // 256) * ((w.shape[0] + 255) // 256) < 512:
         return False
     x0 = xs[0]
     return (x0.dtype == torch.bfloat16 and dys[0].dtype == torch.bfloat16 and x0.dim() == 2

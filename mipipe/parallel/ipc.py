@@ -130,7 +130,9 @@ class IpcChannels:
             ``chunks x virtual`` so every message of a step has its own slot:
             a slot read in place is released only at :meth:`end_step`.
         engine: the sender's copy (:data:`ENGINES`); default ``$MIPIPE_IPC_ENGINE``
-            or ``"sdma"``.
+            or ``"inline"`` (one-way 15.7 us at 1 MiB against ~150 us through a
+            copy stream; the 2-rank shared-GPU step +3.2 %:
+            profiles/ipc_stream_ordered.txt).
         timeout: seconds a host-mode wait may block before it raises (the
             engine's watchdog usually fires first).
     """
@@ -139,7 +141,7 @@ class IpcChannels:
 
     def __init__(self, ranks: Sequence[int], wrap: bool = False, *, device: torch.device, recv_bytes: int,
                  slots: int = 64, engine: Optional[str] = None, timeout: float = 300.0) -> None:
-        engine = engine or os.environ.get("MIPIPE_IPC_ENGINE", "sdma")
+        engine = engine or os.environ.get("MIPIPE_IPC_ENGINE", "inline")
         if engine not in ENGINES:
             raise ValueError(f"engine must be one of {sorted(ENGINES)}, got {engine!r}")
         k = _native_loader.kernels()

@@ -265,7 +265,8 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
 
 
 def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, split_decoder: bool = False,
-                bwd_ratio: float = 2.0, costs: Optional[List[float]] = None) -> StagePlan:
+                bwd_ratio: float = 2.0, costs: Optional[List[float]] = None,
+                objective: str = "makespan") -> StagePlan:
     """Plan for ``stages`` ranks with ``virtual`` chunks each (looping placement).
 
     With ``virtual > 1`` the split starts from the rank-total-balanced one and
@@ -273,15 +274,24 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, s
     (default 4 x stages): a chunk far larger than its neighbours stalls the
     micro-batch flow even when rank totals are even.  ``costs``: per-unit
     costs to plan with instead of the analytic :func:`block_costs` (e.g.
-    measured ones, :mod:`mipipe.parallel.calibrate`)."""
+    measured ones, :mod:`mipipe.parallel.calibrate`).
+
+    ``objective="balance"``: the split with the most even RANK totals
+    (``balance_by_time``'s goal), without the makespan refinement -- which
+    may load ranks unevenly when that shortens the simulated fill / drain
+    (profiles/pp_planning_r4.txt compares the two)."""
     if costs is None:
         costs = block_costs(cfg, split_decoder)
     elif len(costs) != len(block_costs(cfg, split_decoder)):
         raise ValueError(f"{len(costs)} unit costs for {len(block_costs(cfg, split_decoder))} pipeline units")
     if stages * virtual > len(costs):
         raise ValueError(f"{stages} x {virtual} virtual stages exceed the {len(costs)} pipeline units")
+    if objective not in ("makespan", "balance"):
+        raise ValueError(f"objective must be 'makespan' or 'balance', got {objective!r}")
     if virtual == 1:
         return StagePlan(balance_cost(costs, stages), costs, 1, split_decoder)
+    if objective == "balance":
+        return StagePlan(_rank_balanced(costs, stages, virtual), costs, virtual, split_decoder)
     m = chunks or 4 * stages
     best = None
     for start in (balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)):
@@ -424,7 +434,7 @@ def boundary_terms(cfg: LMConfig, micro_batch: Optional[int], unit: str = "flop"
 def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional[Sequence[int]] = None,
                    split_options: Sequence[bool] = (False, True), bwd_ratio: float = 2.0,
                    micro_batch: Optional[int] = None, max_virtual: int = 8,
-                   cost_fn=None) -> Tuple[int, StagePlan]:
+                   cost_fn=None, objective: str = "makespan") -> Tuple[int, StagePlan]:
     """Chunks per rank (and whether to split the decoder) with the shortest
     simulated step; ties (within 0.5 %) keep the simpler plan.  ``bwd_ratio``
     is backward / forward cost (2, or 3 when every micro-batch is recomputed).
@@ -435,7 +445,8 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
     deeper looping placement is chosen only when its shorter fill/drain pays
     for its extra boundaries.  ``cost_fn(split_decoder)``: per-unit costs in ms
     per micro-batch (measured, :mod:`mipipe.parallel.calibrate`) instead of
-    the analytic FLOP model."""
+    the analytic FLOP model.  ``objective``: see :func:`plan_stages` (the
+    chunk count is chosen by simulated step time either way)."""
     transfer, launch = boundary_terms(cfg, micro_batch, "ms" if cost_fn is not None else "flop")
 
     def sim(plan: StagePlan, v: int) -> float:
@@ -461,7 +472,7 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
     best = None
     for _, v, split in screened[:6]:
         plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio,
-                           costs=cost_fn(split) if cost_fn is not None else None)
+                           costs=cost_fn(split) if cost_fn is not None else None, objective=objective)
         t = sim(plan, v)
         # ties (within 0.5 %) keep the simpler plan: fewer chunks, no split
         key = (v, split)

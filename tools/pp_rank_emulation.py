@@ -53,6 +53,8 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--objective", default="makespan", choices=["makespan", "balance"],
+                    help="planner objective (mipipe.parallel.stage.plan_stages)")
     ap.add_argument("--plan", default="analytic", choices=["analytic", "measured"],
                     help="stage-plan unit costs: analytic FLOPs or measured unit times (mipipe.parallel.calibrate)")
     args = ap.parse_args()
@@ -73,9 +75,10 @@ def main() -> int:
         print(f"# measured engine-context unit costs (ms per micro-batch, {time.perf_counter() - t0:.1f} s): "
               + ", ".join(f"{k} {c:.3f}" for k, c in sorted(costs.items())), flush=True)
         cost_fn = lambda split: engine_unit_costs(cfg, costs, split)  # noqa: E731
-    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb, cost_fn=cost_fn)
-    print(f"# plan ({args.plan} costs): v={virtual}, split head {plan.split_decoder}, balance {plan.balance}",
-          flush=True)
+    virtual, plan = choose_virtual(cfg, pp, m, bwd_ratio=2.0 + recompute, micro_batch=mb, cost_fn=cost_fn,
+                                   objective=args.objective)
+    print(f"# plan ({args.plan} costs, {args.objective}): v={virtual}, split head {plan.split_decoder}, "
+          f"balance {plan.balance}", flush=True)
     if args.ranks:
         ranks = list(range(pp)) if args.ranks == "all" else [int(r) for r in args.ranks.split(",")]
     else:
@@ -98,7 +101,7 @@ def main() -> int:
         tokens = m * mb * cfg.seq_len
         fastest = min(walls.values())
         print(f"# per-rank wall spread: {fastest:.1f} .. {walls[slow]:.1f} ms = "
-              f"{100 * (walls[slow] / fastest - 1):.1f} % ({args.plan} plan costs)")
+              f"{100 * (walls[slow] / fastest - 1):.1f} % ({args.plan} plan costs, {args.objective})")
         print(f"# slowest rank {slow}: {walls[slow]:.1f} ms/step; planner-simulated bubble {100 * bub:.1f} % -> "
               f"PP={pp} step ~{est:.1f} ms = {tokens / est * 1e3:,.0f} tokens/s for the job "
               f"({m} x {mb} x {cfg.seq_len} tokens per step)")
