@@ -536,6 +536,100 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
   }
 }
 
+// The EXTRA epilogue (dropout and / or the aux output) in the STAGED layout:
+// the pre-activation (acc + bias) goes through the LDS image once, and each
+// thread then owns 4-row x 8-column blocks of it -- the 8 Philox calls of a
+// block give exactly its 32 mask words (the (row / 4, col) layout of
+// epi_rows and bias_act), and the block's rows leave as 16-byte stores of the
+// output AND of the aux tensor (pre or GELU'(pre)).  In the register layout
+// the aux tensor needed a staging pass of its own and the activation /
+// dropout ran on the accumulator registers: GPT-2-XL's fc1 forward
+// (18432 x 6400 x 1600, GELU, p 0.1, pre saved) cost 542 us against 358 plain
+// (tools/epilogue_cost_probe.py).  Also the activation backward of a dgrad
+// whose forward had dropout (dact_in with the mask regenerated).
+template <int ACT, int W>
+__device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[8][W / 64], int wm, int wn,
+                                                 int lane, int tid, int m0, int n0, const GemmArgs& g) {
+  constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512, CB = W / 8;
+  const int quad = lane >> 4, col_in = lane & 15;
+  float* stg = reinterpret_cast<float*>(smem);
+  bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+  bf16_t* aux = reinterpret_cast<bf16_t*>(g.aux);
+  const bf16_t* res = reinterpret_cast<const bf16_t*>(g.res);
+  const bf16_t* dact_in = reinterpret_cast<const bf16_t*>(g.dact_in);
+  const int64_t ldr = g.ldr > 0 ? g.ldr : g.ldc;
+  const bool drop = g.p > 0.f;
+  const float pscale = drop ? 1.f / (1.f - g.p) : 1.f;
+  const int64_t mask_ld = g.mask_ld > 0 ? g.mask_ld : g.N;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(16 * i + 4 * quad + r) * kStride + wn * WN + 16 * j + col_in] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int rbase = m0 + pass * 128;
+#pragma unroll
+    for (int u = 0; u < 32 * CB / kT; ++u) {
+      const int idx = tid + u * kT;
+      const int rq = idx / CB, c8 = idx % CB;  // consecutive lanes on consecutive 8-column chunks
+      const int col = n0 + 8 * c8, row0 = rbase + 4 * rq;
+      if (col >= g.N || row0 >= g.M) continue;
+      uint32_t wd[8][4];
+      if (drop) {
+        const uint64_t sub = (uint64_t)((row0 + g.mask_row0) >> 2) * (uint64_t)mask_ld + (uint64_t)(col + g.mask_col0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint4 w = Philox(g.seed, sub + e, g.offset).next4();
+          wd[e][0] = w.x; wd[e][1] = w.y; wd[e][2] = w.z; wd[e][3] = w.w;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + r;
+        if (row >= g.M) break;
+        const float* sp = stg + (4 * rq + r) * kStride + 8 * c8;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(sp);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(sp + 4);
+        const float pre[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (aux != nullptr) {
+          bf16x8 a;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] = (__bf16)(ACT == kActGelu && g.aux_grad ? gelu_grad_f(pre[e]) : pre[e]);
+          *reinterpret_cast<bf16x8*>(aux + (int64_t)row * g.ldc + col) = a;
+        }
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float o = ACT == kActRelu ? fmaxf(pre[e], 0.f) : (ACT == kActGelu ? gelu_f(pre[e]) : pre[e]);
+          if (drop) o = wd[e][r] >= g.threshold ? o * pscale : 0.f;
+          v[e] = o;
+        }
+        if (dact_in != nullptr) {
+          const bf16x8 sv = *reinterpret_cast<const bf16x8*>(dact_in + (int64_t)row * g.ldd + col);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= g.dact_scale * dact_f(g.dact, (float)sv[e]);
+        }
+        if (res != nullptr) {
+          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (int64_t)row * ldr + col);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+        *reinterpret_cast<bf16x8*>(C + (int64_t)row * g.ldc + col) = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Ping-pong main loop (PP = true).  The two wave groups (wm = 0: waves 0-3,
 // wm = 1: waves 4-7; each SIMD hosts one wave of each) run one barrier
 // interval apart, so in every interval one wave per SIMD issues its 16-MFMA
@@ -1072,7 +1166,20 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   //    K = 64 more than this path: tools/gemm_k_sweep.py.)
   const int quad = lane >> 4, col_in = lane & 15;
   __syncthreads();  // every wave is done reading the operand buffers
-  if (EPI == kEpiStoreBf16 && (EXTRA || ACT != kActNone || g.bias != nullptr)) {
+  if (EPI == kEpiStoreBf16 && EXTRA) {  // dropout and / or aux: the staged-layout epilogue does it all
+    const int ncol = n0 + wn * WN + col_in;
+    if (g.bias != nullptr) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float b = ncol + 16 * j < g.N ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[ncol + 16 * j]) : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] += b;
+      }
+    }
+    staged_store_act<ACT, W>(smem, acc, wm, wn, lane, tid, m0, n0, g);
+    return;
+  }
+  if (EPI == kEpiStoreBf16 && (ACT != kActNone || g.bias != nullptr)) {
     const int ncol = n0 + wn * WN + col_in, nrow = m0 + wm * 128 + 4 * quad;
     const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
     const EpiParams ep{g.seed, g.offset, g.N, g.p, pscale, g.threshold, g.mask_row0, g.mask_col0,
@@ -1081,16 +1188,6 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       bias[j] = (g.bias != nullptr && ncol + 16 * j < g.N) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[ncol + 16 * j]) : 0.f;
-    if (EXTRA && g.aux != nullptr) {  // pre-activation output
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] += bias[j];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) bias[j] = 0.f;
-      staged_store<kEpiStoreBf16, W>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, g.aux, nullptr, 0,
-                                     nullptr, 0, 0, 1.f, false, ACT == kActGelu && g.aux_grad);
-    }
     epi_rows<0, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
     epi_rows<1, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
     epi_rows<2, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);

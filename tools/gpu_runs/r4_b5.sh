@@ -20,3 +20,4 @@ for spec in "gpt2_xl measured balance always" "enc12_d4096 measured balance neve
   timeout -k 10 500 python -u tools/pp_rank_emulation.py --config $1 --ranks all --steps 4 --plan $2 --objective $3 --checkpoint $4 > gpurun_out/emu5_$1_$2_$3_$4.log 2>&1 || { tail -20 gpurun_out/emu5_$1_$2_$3_$4.log; exit 1; }
   grep "^# plan\|^# per-rank\|^# slowest\|^# measured" gpurun_out/emu5_$1_$2_$3_$4.log
 done
+timeout -k 10 200 python -u tools/epilogue_cost_probe.py > gpurun_out/epilogue_probe.txt 2>&1; cat gpurun_out/epilogue_probe.txt
