@@ -167,6 +167,21 @@ __device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset
   return keep;
 }
 
+// The dropout layout of the GEMM epilogues and the bias + activation kernels
+// (fwd, and every backward that regenerates the mask): element (row, col) of
+// an [*, ld] activation (ld even) draws the 16-bit half (col & 1) of word
+// (row & 3) of Philox block (row / 4) * (ld / 2) + col / 2 -- one block per
+// 4 rows x 2 columns, half the blocks of one 32-bit uniform per element (the
+// Philox rounds are most of a dropout epilogue's cost: +70 us on an 18432 x
+// 6400 output, tools/epilogue_cost_probe.py) -- and is kept iff that uniform
+// is >= floor(p * 2^16).
+__device__ __forceinline__ uint64_t drop_sub(int64_t row, int64_t col, int64_t ld) {
+  return (uint64_t)(row >> 2) * (uint64_t)(ld >> 1) + (uint64_t)(col >> 1);
+}
+__device__ __forceinline__ bool drop_keep(uint32_t word, int half, uint32_t thr16) {
+  return ((word >> (16 * half)) & 0xFFFFu) >= thr16;
+}
+
 __host__ __device__ inline uint32_t dropout_threshold(float p) {
   double t = (double)p * 4294967296.0;
   if (t >= 4294967295.0) return 0xFFFFFFFFu;

@@ -23,10 +23,10 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return cdf + x * pdf;
 }
 
-// Dropout mask layout shared with the GEMM epilogue (gemm.hip): element
-// (row, col) uses word (row & 3) of Philox(seed, (row / 4) * cols + col, offset).
-// Each thread therefore owns a 4-row x 8-column tile: 8 Philox calls produce
-// exactly its 32 mask words.
+// Dropout mask layout shared with the GEMM epilogues (common.h drop_sub):
+// element (row, col) draws half (col & 1) of word (row & 3) of Philox block
+// (row / 4) * (cols / 2) + col / 2.  Each thread owns a 4-row x 8-column tile:
+// 4 Philox calls produce exactly its 32 16-bit uniforms.
 template <typename T, int ACT, bool BWD>
 __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in, const T* __restrict__ saved,
                                                        const T* __restrict__ bias, T* __restrict__ out,
@@ -46,11 +46,13 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
 #pragma unroll
       for (int i = 0; i < 8; ++i) b[i] = 0.f;
     }
-    uint32_t w[8][4];
+    uint32_t w[4][4];  // [column pair][row]
+    const uint32_t thr16 = threshold >> 16;
     if (p > 0.f) {
+      const uint64_t sub = drop_sub(q * 4, c0, cols);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint4 r = Philox(seed, (uint64_t)q * (uint64_t)cols + (uint64_t)(c0 + i), offset).next4();
+      for (int i = 0; i < 4; ++i) {
+        const uint4 r = Philox(seed, sub + i, offset).next4();
         w[i][0] = r.x; w[i][1] = r.y; w[i][2] = r.z; w[i][3] = r.w;
       }
     }
@@ -67,7 +69,7 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
           float v = a[i] + b[i];
           if (ACT == kActRelu) v = fmaxf(v, 0.f);
           if (ACT == kActGelu) v = gelu_f(v);
-          if (p > 0.f) v = w[i][rr] >= threshold ? v * scale : 0.f;
+          if (p > 0.f) v = drop_keep(w[i >> 1][rr], i & 1, thr16) ? v * scale : 0.f;
           a[i] = v;
         }
       } else {
@@ -83,7 +85,7 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
         }
         if (p > 0.f) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = w[i][rr] >= threshold ? a[i] * scale : 0.f;
+          for (int i = 0; i < 8; ++i) a[i] = drop_keep(w[i >> 1][rr], i & 1, thr16) ? a[i] * scale : 0.f;
         }
       }
       Io<T>::store8(out + e, a);

@@ -251,12 +251,11 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
           out[r] = ACT == kActRelu ? fmaxf(pre[r], 0.f) : (ACT == kActGelu ? gelu_f(pre[r]) : pre[r]);
         }
         if (g.p > 0.f) {
-          // column-quad mask layout: subsequence (row/4) * N + col, word row & 3
-          const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
-          const uint4 w = Philox(g.seed, sub, g.offset).next4();
+          // the dropout layout (common.h drop_sub): word row & 3, half col & 1
+          const uint4 w = Philox(g.seed, drop_sub(row0, col, g.N), g.offset).next4();
           const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) out[r] = ws[r] >= g.threshold ? out[r] * pscale : 0.f;
+          for (int r = 0; r < 4; ++r) out[r] = drop_keep(ws[r], col & 1, g.threshold >> 16) ? out[r] * pscale : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -420,15 +419,14 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
     const float b = bias[j];
     uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     if (ep.p > 0.f) {
-      const uint64_t sub = (uint64_t)((row0 + ep.mask_row0) >> 2) * (uint64_t)ep.mask_ld + (uint64_t)(col + ep.mask_col0);
-      const uint4 w = Philox(ep.seed, sub, ep.offset).next4();
+      const uint4 w = Philox(ep.seed, drop_sub(row0 + ep.mask_row0, col + ep.mask_col0, ep.mask_ld), ep.offset).next4();
       ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float pre = acc[I][j][r] + b;
       float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
-      if (ep.p > 0.f) out = ws[r] >= ep.threshold ? out * ep.pscale : 0.f;
+      if (ep.p > 0.f) out = drop_keep(ws[r], (col + ep.mask_col0) & 1, ep.threshold >> 16) ? out * ep.pscale : 0.f;
       acc[I][j][r] = out;
     }
   }
@@ -561,6 +559,7 @@ __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[
   const bool drop = g.p > 0.f;
   const float pscale = drop ? 1.f / (1.f - g.p) : 1.f;
   const int64_t mask_ld = g.mask_ld > 0 ? g.mask_ld : g.N;
+  const uint32_t thr16 = g.threshold >> 16;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wm == pass) {
@@ -580,11 +579,11 @@ __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[
       const int rq = idx / CB, c8 = idx % CB;  // consecutive lanes on consecutive 8-column chunks
       const int col = n0 + 8 * c8, row0 = rbase + 4 * rq;
       if (col >= g.N || row0 >= g.M) continue;
-      uint32_t wd[8][4];
+      uint32_t wd[4][4];  // [column pair][row]: two 16-bit uniforms per word
       if (drop) {
-        const uint64_t sub = (uint64_t)((row0 + g.mask_row0) >> 2) * (uint64_t)mask_ld + (uint64_t)(col + g.mask_col0);
+        const uint64_t sub = drop_sub(row0 + g.mask_row0, col + g.mask_col0, mask_ld);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < 4; ++e) {
           const uint4 w = Philox(g.seed, sub + e, g.offset).next4();
           wd[e][0] = w.x; wd[e][1] = w.y; wd[e][2] = w.z; wd[e][3] = w.w;
         }
@@ -607,7 +606,7 @@ __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float o = ACT == kActRelu ? fmaxf(pre[e], 0.f) : (ACT == kActGelu ? gelu_f(pre[e]) : pre[e]);
-          if (drop) o = wd[e][r] >= g.threshold ? o * pscale : 0.f;
+          if (drop) o = drop_keep(wd[e >> 1][r], e & 1, thr16) ? o * pscale : 0.f;
           v[e] = o;
         }
         if (dact_in != nullptr) {

@@ -249,9 +249,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (Cfg<WM, WN, TM, TN>::kBlocksPer
         if (EPI == kEpiStoreAct) {
           uint32_t ws[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
           if (g.p > 0.f) {
-            // column-quad mask layout: subsequence (row/4) * N + col, word row & 3
-            const uint64_t sub = (uint64_t)(row0 >> 2) * (uint64_t)g.N + (uint64_t)col;
-            const uint4 w = Philox(g.seed, sub, g.offset).next4();
+            // the dropout layout (common.h drop_sub): word row & 3, half col & 1
+            const uint4 w = Philox(g.seed, drop_sub(row0, col, g.N), g.offset).next4();
             ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
           }
 #pragma unroll
@@ -259,7 +258,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (Cfg<WM, WN, TM, TN>::kBlocksPer
             const int row = row0 + r;
             const float pre = acc[t][u][4 * gq + r] + b;
             float out = ACT == kActRelu ? fmaxf(pre, 0.f) : (ACT == kActGelu ? gelu_f(pre) : pre);
-            if (g.p > 0.f) out = ws[r] >= g.threshold ? out * pscale : 0.f;
+            if (g.p > 0.f) out = drop_keep(ws[r], col & 1, g.threshold >> 16) ? out * pscale : 0.f;
             if (col_ok && row < g.M) {
               const int64_t o = (int64_t)row * g.ldc + col;
               if (g.res != nullptr) out += reinterpret_cast<const float*>(g.res)[(int64_t)row * g.ldr + col];
