@@ -180,10 +180,13 @@ def main() -> int:
                                                        else "analytic")
     cost_fn = None
     if plan_mode == "measured" and pp > 1:
-        from mipipe.parallel.calibrate import calibrated_costs, engine_unit_costs
+        from mipipe.parallel.calibrate import CalibrationError, calibrated_costs, engine_unit_costs
 
-        unit_ms = calibrated_costs(cfg, mb, m, args.checkpoint, device=device, dtype=dtype)
-        cost_fn = lambda split: engine_unit_costs(cfg, unit_ms, split)  # noqa: E731
+        try:
+            unit_ms = calibrated_costs(cfg, mb, m, args.checkpoint, device=device, dtype=dtype)
+            cost_fn = lambda split: engine_unit_costs(cfg, unit_ms, split)  # noqa: E731
+        except CalibrationError as exc:  # raised on every rank alike: all fall back together
+            print(f"warning: {exc}; planning with analytic costs", file=sys.stderr)
     if args.virtual == "auto":
         virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb,
                                        cost_fn=cost_fn, objective=args.plan_objective)

@@ -45,7 +45,7 @@ import torch.distributed as dist
 from ..models.lm import LMConfig
 
 __all__ = ["unit_kinds", "measure_unit_times", "unit_costs", "measure_engine_costs", "engine_unit_costs",
-           "calibrated_costs", "cache_key"]
+           "calibrated_costs", "cache_key", "CalibrationError"]
 
 
 def unit_kinds(cfg: LMConfig, split_decoder: bool = False) -> List[str]:
@@ -321,6 +321,10 @@ def engine_unit_costs(cfg: LMConfig, costs: Dict[str, float], split_decoder: boo
     return [costs[k] for k in unit_kinds(cfg, split_decoder)]
 
 
+class CalibrationError(RuntimeError):
+    """Raised on EVERY rank when any rank's calibration failed (callers fall back to analytic costs together)."""
+
+
 def _load(path: str) -> Optional[dict]:
     try:
         with open(path) as f:
@@ -355,18 +359,31 @@ def calibrated_costs(cfg: LMConfig, micro_batch: int, chunks: int, checkpoint: s
         dist.all_reduce(flag, group=group)
         if flag.item() > 0:
             found = None
-    if found is not None:
-        costs = {k: float(v) for k, v in found["costs"].items()}
-    elif measure is not None:
-        costs = measure()
-    else:
-        costs = measure_engine_costs(cfg, micro_batch, chunks, checkpoint, device=device, dtype=dtype)
+    kinds = sorted(set(unit_kinds(cfg, False)) | set(unit_kinds(cfg, True)))
+    ok, err = 1.0, None
+    try:
+        if found is not None:
+            costs = {k: float(v) for k, v in found["costs"].items()}
+        elif measure is not None:
+            costs = measure()
+        else:
+            costs = measure_engine_costs(cfg, micro_batch, chunks, checkpoint, device=device, dtype=dtype)
+        costs = {k: float(costs[k]) for k in kinds}
+    except Exception as exc:  # noqa: BLE001 -- reported on every rank below, identically
+        ok, err, costs = 0.0, exc, {k: 0.0 for k in kinds}
     if distributed:
-        kinds = sorted(costs)
-        vec = torch.tensor([costs[k] for k in kinds], dtype=torch.float64, device=device if nccl else "cpu")
+        # ONE collective whatever happened locally: a rank whose measurement
+        # failed must not leave the others waiting in a different collective
+        vec = torch.tensor([ok] + [costs[k] for k in kinds], dtype=torch.float64, device=device if nccl else "cpu")
         dist.all_reduce(vec, group=group)
-        vec = (vec / dist.get_world_size(group)).cpu().tolist()
-        costs = dict(zip(kinds, vec))
+        vec = vec.cpu().tolist()
+        n = dist.get_world_size(group)
+        if vec[0] < n:
+            raise CalibrationError(f"calibration failed on {n - int(vec[0])} of {n} ranks"
+                                   + (f" (here: {err!r})" if err is not None else ""))
+        costs = {k: v / n for k, v in zip(kinds, vec[1:])}
+    elif err is not None:
+        raise CalibrationError(f"calibration failed: {err!r}") from err
     if found is None and (not distributed or dist.get_rank() == 0):
         try:
             os.makedirs(cache_dir, exist_ok=True)

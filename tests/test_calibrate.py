@@ -97,3 +97,42 @@ def test_calibrated_costs_agree_across_ranks(tmp_path):
     assert res[0] == res[1]  # same costs (all-reduced), same plan, in both rounds
     assert res[0][0] == res[0][1]  # the cached table is what was measured
     assert len(list(tmp_path.iterdir())) == 1
+
+
+def _fail_worker(rank, port, cache, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MIPIPE_CALIB_DIR=cache)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from mipipe.parallel.calibrate import CalibrationError
+
+        cfg = _cfg3()
+
+        def measure():
+            if rank == 1:
+                raise RuntimeError("boom")
+            return measure_engine_costs(cfg, 2, 4, device=CPU, dtype=torch.float32, steps=1)
+
+        try:
+            calibrated_costs(cfg, 2, 4, "never", device=CPU, dtype=torch.float32, refresh=True, measure=measure)
+            q.put((rank, "no error"))
+        except CalibrationError as exc:
+            dist.barrier()  # both ranks are still in step after the failure
+            q.put((rank, str(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_calibration_failure_raises_on_every_rank(tmp_path):
+    """One rank's failed measurement makes EVERY rank raise CalibrationError (no rank left in a collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all("failed on 1 of 2 ranks" in m for m in res.values()), res
+    assert "boom" in res[1]
