@@ -1221,7 +1221,9 @@ PYBIND11_MODULE(_C, m) {
         "--gemm-ab build also has the A/B schedules 0-6 (kernels.h).  Returns false for a schedule not built in.");
   m.def("gemm_get_schedule", &gemm_get_schedule);
   m.def("gemm_ab_build", &gemm_ab_build, "true if the A/B GEMM schedules 0-6 are compiled in (-DMIPIPE_GEMM_AB)");
-  m.def("gemm_set_rounds", &gemm_set_rounds, "1: launch multi-round GEMM grids one round of tiles at a time (default)");
+  m.def("gemm_set_rounds", &gemm_set_rounds,
+        "multi-round GEMM grids whose last round is at most half full: 0 one launch, 1 (default) one launch per round "
+        "of tiles when K >= 4096, 2 one launch per round at any K");
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none(),

@@ -1233,7 +1233,7 @@ bool use_big(const GemmArgs& g) {
 // idle, or 256 256x128 tiles (1.2x faster, profiles/gemm_vs_hipblaslt.txt).
 // gemm_set_width(128 / 256) or MIPIPE_GEMM_W forces one (A/B, tests).
 int g_gemm_width = -1;  // -1: not read from the environment yet, 0: auto
-int g_gemm_rounds = -1;  // MIPIPE_GEMM_ROUNDS=0: multi-round grids in one launch (A/B); -1 unread
+int g_gemm_rounds = -1;  // MIPIPE_GEMM_ROUNDS: 0 one launch, 1 per round at K >= 4096 (default), 2 per round; -1 unread
 
 int big_width(const GemmArgs& g) {
   if (g_gemm_width < 0) {
@@ -1492,8 +1492,8 @@ int gemm_splitk_factor(const GemmArgs& g) {
   return best;
 }
 
-// Grids of several rounds whose last round is at most half full are launched
-// one round of tiles at a time: the LM head (4096 x 28928 x 4096, 1808 tiles =
+// Grids of several rounds whose last round is at most half full -- and whose
+// K is >= 4096 (below) -- are launched one round of tiles at a time: the LM head (4096 x 28928 x 4096, 1808 tiles =
 // 7 rounds + 16 tiles) 812 -> 786 us, 2048 x 12288 x 4096 (384 tiles) 176 ->
 // 167 us (hipBLASLt's time).  Whole rounds (4096 x 12288: 768 tiles, 292 vs
 // 296 us) and a last round over half full (2048 x 28928: 904 tiles, 407 vs
@@ -1512,6 +1512,11 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
     g_gemm_rounds = e ? atoi(e) : 1;
   }
   if (g_gemm_rounds == 0 || g.k_splits > 1 || !use_big(g) || big_width(g) != 256) return false;
+  // short main loops (K < 4096: GPT-2-XL's K = 1600 GEMMs) go as ONE launch: a CU
+  // that finishes its tile starts the next round's while the others store, so
+  // the fixed per-tile prologue / epilogue overlaps across rounds (GPT-2-XL PP=1
+  // 64.7-64.8k -> 66.2-66.3k tok/s on one box; enc12, all K = 4096: unchanged)
+  if (g_gemm_rounds == 1 && g.K < 4096) return false;
   const int tm = (g.M + 255) / 256, tn = (g.N + 255) / 256;
   // only when the last round is at most half full (see above)
   if (tm * tn <= 256 || (tm * tn) % 256 == 0 || (tm * tn) % 256 > 128) return false;

@@ -677,7 +677,7 @@ def test_gemm_round_launches_identical(k):
     try:
         k.gemm_set_rounds(0)
         ref = run()
-        k.gemm_set_rounds(1)
+        k.gemm_set_rounds(2)  # per-round launches at any K (the default 1 keeps K < 4096 in one launch)
         got = run()
     finally:
         k.gemm_set_rounds(1)

@@ -57,7 +57,7 @@ k.gemm_set_rounds(0)
 ref = run()
 ref2 = run()
 print("one launch, repeat:", [diff(a, bb) for a, bb in zip(ref, ref2)], flush=True)
-k.gemm_set_rounds(1)
+k.gemm_set_rounds(2)  # per-round launches at any K
 first = run()
 for it in range(reps):
     got = run()
