@@ -787,9 +787,17 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     kt0 = (int)blockIdx.y * total / g.k_splits;
     nk = ((int)blockIdx.y + 1) * total / g.k_splits - kt0;
   }
+  // Staging shares of the PP == 4 schedule (see its loop): for a K-contiguous
+  // operand the waves of group 1 (which restage the buffer their siblings are
+  // still reading) take rows no sibling reads -- A rows 0-127 (group 0's half:
+  // share of "wave" w ^ 4) and, for B, the first 32 of the 64 rows the wave
+  // itself reads (share 2 wn; group 0 the other 32: 2 wn + 1).  I-contiguous
+  // operands keep the per-wave k-row shares.
+  const int shA = PP == 4 && A_KC ? wave ^ 4 : wave;
+  const int shB = PP == 4 && B_KC ? 2 * wn + (wm == 0 ? 1 : 0) : wave;
   uint32_t offA[4], offB[NJ];
-  stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave, lane, offA);
-  stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave, lane, offB);
+  stage_offsets<A_KC, 256>(g.lda, m0, g.M, shA, lane, offA);
+  stage_offsets<B_KC, W>(g.ldb, n0, g.N, shB, lane, offB);
   // PP == 2 (LEADB): the B tile of K-tile u+2 is staged in phase 3 of tile u,
   // into the buffer tile u is being computed from -- its B region is dead by
   // then (B fragments are read in phases 0/1 and kept in registers; group 1's
@@ -802,9 +810,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   {
     int kl;
     const bf16_t* A = seg_base(g, true, kt0 * BK, kl);
-    stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem, wave);
+    stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem, shA);
     const bf16_t* B = seg_base(g, false, kt0 * BK, kl);
-    stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kTileBytes, wave);
+    stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kTileBytes, shB);
     if ((PP == 2 || PP == 3) && nk > 1) {
       B = seg_base(g, false, (kt0 + 1) * BK, kl);
       stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, wave);
@@ -815,9 +823,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     }
     if (PP == 4 && wm == 1 && nk > 1) {  // group 1 stages whole tiles one tile earlier (below)
       A = seg_base(g, true, (kt0 + 1) * BK, kl);
-      stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem + kBuf, wave);
+      stage_fast<A_KC, 256>(A, g.lda, kl, offA, smem + kBuf, shA);
       B = seg_base(g, false, (kt0 + 1) * BK, kl);
-      stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, wave);
+      stage_fast<B_KC, W>(B, g.ldb, kl, offB, smem + kBuf + kTileBytes, shB);
     }
   }
 
@@ -827,7 +835,15 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     // MFMA cycles.  Group 0 loads tile u in interval 2u, group 1 in 2u+1
     // (global count).  Tile u+1 goes into tile u-1's buffer, last read by
     // group 1 in 2u-1: group 1 stages its share right after those reads
-    // (program order), group 0 in its load interval 2u.  Tile u+1 must have
+    // (program order), group 0 in its load interval 2u.  Group 1's DMA into
+    // tile u's buffer may land while a SIBLING wave still has reads of it
+    // queued (no barrier separates the waves of a group; a sibling delayed by
+    // its A^T emission piece was seen to read the next tile's rows once), so
+    // for K-contiguous operands the shares are chosen (shA / shB above) such
+    // that group 1 restages only rows none of its siblings reads.  For
+    // I-contiguous operands every wave reads every k-row of the tile: their
+    // group-1 shares keep that window (it needs a sibling more than a DMA
+    // latency behind; no screen has caught one there).  Tile u+1 must have
     // landed by the barrier ending 2u+1: group 0 drains after its MFMAs
     // (vmcnt(0)), group 1 in its load interval 2u+1 after staging tile u+2
     // (vmcnt(NA + NB)).
@@ -882,9 +898,9 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         int kl;
         char* dst = wm == 0 ? nxt : cur;
         const bf16_t* A = seg_base(g, true, (kt0 + u + ahead) * BK, kl);
-        stage_fast<A_KC, 256>(A, g.lda, kl, offA, dst, wave);
+        stage_fast<A_KC, 256>(A, g.lda, kl, offA, dst, shA);
         const bf16_t* B = seg_base(g, false, (kt0 + u + ahead) * BK, kl);
-        stage_fast<B_KC, W>(B, g.ldb, kl, offB, dst + kTileBytes, wave);
+        stage_fast<B_KC, W>(B, g.ldb, kl, offB, dst + kTileBytes, shB);
       }
       if (wm == 1) {
         if (u + 2 < nk) vmcnt_keep<NA + NB>();
