@@ -329,6 +329,7 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 _XT_MODE = os.environ.get("MIPIPE_WGRAD_XT", "auto")
 _EMIT_XT = _XT_MODE in ("1", "emit")
 _XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "6144"))
+_XT_MIN_TILES = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_TILES", "512"))
 # GELU forwards save GELU'(pre) rather than pre (MIPIPE_GELU_SAVE_GRAD=1).  Off by
 # default: the second erf/exp per element in the forward GEMM's epilogue cost the
 # GPT-2-XL step more than the one-multiply backward saved (the elementwise GELU
@@ -472,7 +473,7 @@ def _transpose_pays(w: Tensor, dys, xs, T: int) -> bool:
         return False
     # grids of < 2 rounds of 256x256 tiles run split-K and quantise the same in
     # either layout (GPT-2-XL fc1: 175 tiles, 1454 vs 1461 us): no gain to pay for
-    if ((w.shape[1] + 255) // 256) * ((w.shape[0] + 255) // 256) < 512:
+    if ((w.shape[1] + 255) // 256) * ((w.shape[0] + 255) // 256) < _XT_MIN_TILES:
         return False
     x0 = xs[0]
     return (x0.dtype == torch.bfloat16 and dys[0].dtype == torch.bfloat16 and x0.dim() == 2
