@@ -15,13 +15,7 @@ namespace mipipe {
 
 namespace {
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+__device__ __forceinline__ float gelu_grad(float x) { return gelu_grad_f(x); }  // common.h (erf_as)
 
 // Dropout mask layout shared with the GEMM epilogues (common.h drop_sub):
 // element (row, col) draws half (col & 1) of word (row & 3) of Philox block

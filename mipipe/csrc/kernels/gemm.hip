@@ -122,21 +122,6 @@ __device__ __forceinline__ bf16x8 read_frag(const char* tile, int ib, int s, int
   }
 }
 
-// Exact-erf GELU with erf from Abramowitz & Stegun 7.1.26 (|error| < 1.5e-7,
-// far below the bf16 output rounding): one rcp + one exp and a handful of
-// registers, where ocml's erff keeps so many values live that the 16-value
-// epilogue row blocks spilled (1.2 KB scratch per lane).
-__device__ __forceinline__ float erf_as(float x) {
-  const float ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
-  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  const float y = 1.f - poly * __expf(-ax * ax);
-  return copysignf(y, x);
-}
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad_f(float x) {
-  return 0.5f * (1.f + erf_as(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-}
 // act'(s) for the activation-backward epilogue (GemmArgs::dact): ReLU's from its
 // output, GELU's from the pre-activation, or s itself (kActSavedGrad: the forward
 // stored GELU'(pre) -- one multiply, like ReLU's sign test).
