@@ -271,6 +271,14 @@ constexpr int kThreads = 512;
 constexpr int kTileBytes = BM * BK * 2;      // 32 KiB per operand tile
 constexpr int kSmemBytes = 128 * 260 * 4;    // 130 KiB: 2 x 64 KiB operand buffers, reused by the epilogue
 
+// The PP == 4 loop keeps an I-contiguous B operand in THREE buffers (A in two;
+// see the loop): 2 (A + B) + B = 160 KiB at W = 256, all of the CU's LDS.
+template <bool B_KC, int PP, int W>
+constexpr int smem_bytes() {
+  constexpr int b3 = 2 * (kTileBytes + W * BK * 2) + W * BK * 2;
+  return PP == 4 && !B_KC && b3 > kSmemBytes ? b3 : kSmemBytes;
+}
+
 // I-contiguous image with 2W-byte rows (W = 256 or 128 i values; the B tile of
 // the 256x128 variant is 128 wide).
 template <int W>
@@ -304,6 +312,22 @@ __device__ __forceinline__ void stage_offsets(int64_t ld, int i0, int lim, int w
       const int gi = min(i0 + 8 * c16, lim - 8);
       off[u] = (uint32_t)(((int64_t)row * ld + gi) * 2);
     }
+  }
+}
+
+// The I-contiguous A tile of the PP == 4 loop is kept as two 128-wide halves
+// (i 0-127, then 128-255; 16 KiB each, the W = 128 image), so each half is read
+// by one wave group only.  Share s (0-7) stages rows 16 (s & 3) .. +16 of half
+// s >> 2 -- the same LDS pieces stage_fast gives share s (4 KiB at 4 s KiB).
+__device__ __forceinline__ void stage_offsets_halves(int64_t ld, int i0, int lim, int share, int lane,
+                                                     uint32_t (&off)[4]) {
+  const int half = share >> 2;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = 4 * (4 * (share & 3) + u) + (lane >> 4);
+    const int c16 = (lane & 15) ^ (ic_rk(row) << 1);
+    const int gi = min(i0 + 128 * half + 8 * c16, lim - 8);
+    off[u] = (uint32_t)(((int64_t)row * ld + gi) * 2);
   }
 }
 
@@ -684,6 +708,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   constexpr int JJ = NJ / 2;          // ... per ping-pong quadrant
   constexpr int WN = W / 4;           // wave tile width
   constexpr int kBuf = kTileBytes + W * BK * 2;  // A + B tile
+  constexpr bool AH = PP == 4 && !A_KC;          // A tile as two 128-wide halves (stage_offsets_halves)
+  constexpr bool B3 = PP == 4 && !B_KC;          // B tiles in three buffers (smem_bytes)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -708,7 +734,8 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
   auto rowsum_step = [&](const char* tile) {
     if (rsum && wm == 0) {
       const int r = tid >> 2, c8 = 4 * tn + (tid & 3);
-      const s16x4 v = *reinterpret_cast<const s16x4*>(tile + ic_off_w<256>(r, c8));
+      const s16x4 v = *reinterpret_cast<const s16x4*>(
+          AH ? tile + (tn >> 3) * (kTileBytes / 2) + ic_off_w<128>(r, c8 & 31) : tile + ic_off_w<256>(r, c8));
 #pragma unroll
       for (int e = 0; e < 4; ++e) rs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
     }
@@ -772,16 +799,19 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     kt0 = (int)blockIdx.y * total / g.k_splits;
     nk = ((int)blockIdx.y + 1) * total / g.k_splits - kt0;
   }
-  // Staging shares of the PP == 4 schedule (see its loop): for a K-contiguous
-  // operand the waves of group 1 (which restage the buffer their siblings are
-  // still reading) take rows no sibling reads -- A rows 0-127 (group 0's half:
-  // share of "wave" w ^ 4) and, for B, the first 32 of the 64 rows the wave
-  // itself reads (share 2 wn; group 0 the other 32: 2 wn + 1).  I-contiguous
-  // operands keep the per-wave k-row shares.
-  const int shA = PP == 4 && A_KC ? wave ^ 4 : wave;
+  // Staging shares of the PP == 4 schedule (see its loop): the waves of group 1
+  // (which restage the buffer their siblings are still reading) take bytes no
+  // sibling reads -- A rows 0-127 (group 0's half: share of "wave" w ^ 4; for
+  // an I-contiguous A the tile is kept as two halves for this) and, for a
+  // K-contiguous B, the first 32 of the 64 rows the wave itself reads (share
+  // 2 wn; group 0 the other 32: 2 wn + 1).  An I-contiguous B (every wave
+  // reads every k-row) rotates through three buffers instead and keeps the
+  // per-wave k-row shares.
+  const int shA = PP == 4 ? wave ^ 4 : wave;
   const int shB = PP == 4 && B_KC ? 2 * wn + (wm == 0 ? 1 : 0) : wave;
   uint32_t offA[4], offB[NJ];
-  stage_offsets<A_KC, 256>(g.lda, m0, g.M, shA, lane, offA);
+  if constexpr (AH) stage_offsets_halves(g.lda, m0, g.M, shA, lane, offA);
+  else stage_offsets<A_KC, 256>(g.lda, m0, g.M, shA, lane, offA);
   stage_offsets<B_KC, W>(g.ldb, n0, g.N, shB, lane, offB);
   // PP == 2 (LEADB): the B tile of K-tile u+2 is staged in phase 3 of tile u,
   // into the buffer tile u is being computed from -- its B region is dead by
@@ -824,12 +854,14 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     // tile u's buffer may land while a SIBLING wave still has reads of it
     // queued (no barrier separates the waves of a group; a sibling delayed by
     // its A^T emission piece was seen to read the next tile's rows once), so
-    // for K-contiguous operands the shares are chosen (shA / shB above) such
-    // that group 1 restages only rows none of its siblings reads.  For
-    // I-contiguous operands every wave reads every k-row of the tile: their
-    // group-1 shares keep that window (it needs a sibling more than a DMA
-    // latency behind; no screen has caught one there).  Tile u+1 must have
-    // landed by the barrier ending 2u+1: group 0 drains after its MFMAs
+    // group 1 restages only bytes none of its siblings reads: A rows 0-127
+    // (shA above; an I-contiguous A is kept as two 128-row halves for that)
+    // and, for a K-contiguous B, half of the i-rows the wave itself reads
+    // (shB).  An I-contiguous B has no such share (every wave reads every
+    // k-row of its columns), so its tiles rotate through three buffers: tile
+    // u+2 goes into tile u-1's B buffer, whose last reads (group 1, interval
+    // 2u-1) retired before the barrier ending that interval.  Tile u+1 must
+    // have landed by the barrier ending 2u+1: group 0 drains after its MFMAs
     // (vmcnt(0)), group 1 in its load interval 2u+1 after staging tile u+2
     // (vmcnt(NA + NB)).
     if (wm == 1 && nk > 1) vmcnt_keep<NA + NB>();
@@ -838,9 +870,13 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
     if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one interval
     bf16x8 af[8][2], bq[NJ][2];
     int ekt = kt0 % ntn;  // (kt0 + u) mod tiles_n (A^T emission rotation)
+    // B3: B buffer of slot s (tiles kt0, kt0 + 1 were staged into slots 0, 1)
+    auto bslot = [&](int s) { return s == 2 ? smem + 2 * kBuf : smem + s * kBuf + kTileBytes; };
+    int bs = 0;  // B3: slot of tile u (u mod 3)
     for (int u = 0; u < nk; ++u) {
       char* cur = smem + (u & 1) * kBuf;
       char* nxt = smem + ((u + 1) & 1) * kBuf;
+      char* bcur = B3 ? bslot(bs) : cur + kTileBytes;
       // emission first: its reads precede this wave's DMA that may restage
       // `cur`, and its stores (waiting for those reads) precede the fragment
       // reads, so its 16 data registers are dead before the fragments load
@@ -869,13 +905,15 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
 #pragma unroll
       for (int ii = 0; ii < 8; ++ii)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) af[ii][s] = frag<A_KC, 256>(cur, wm * 128 + 16 * ii, s, lane);
+        for (int s = 0; s < 2; ++s)
+          af[ii][s] = AH ? frag<false, 128>(cur + wm * (kTileBytes / 2), 16 * ii, s, lane)
+                         : frag<A_KC, 256>(cur, wm * 128 + 16 * ii, s, lane);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) bq[j][s] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * j, s, lane);
+        for (int s = 0; s < 2; ++s) bq[j][s] = frag<B_KC, W>(bcur, wn * WN + 16 * j, s, lane);
       rowsum_step(cur);
-      colsum_step(cur + kTileBytes);
+      colsum_step(bcur);
       if (X == kXEmit && A_KC && ej >= 0) emit_store(kt0 + u, ej, ea, eb);
       ekt = ekt + 1 == ntn ? 0 : ekt + 1;
       const int ahead = wm == 0 ? 1 : 2;  // the tile this group stages now
@@ -885,8 +923,11 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
         const bf16_t* A = seg_base(g, true, (kt0 + u + ahead) * BK, kl);
         stage_fast<A_KC, 256>(A, g.lda, kl, offA, dst, shA);
         const bf16_t* B = seg_base(g, false, (kt0 + u + ahead) * BK, kl);
-        stage_fast<B_KC, W>(B, g.ldb, kl, offB, dst + kTileBytes, shB);
+        int bn = bs + ahead;
+        if (bn >= 3) bn -= 3;
+        stage_fast<B_KC, W>(B, g.ldb, kl, offB, B3 ? bslot(bn) : dst + kTileBytes, shB);
       }
+      bs = bs == 2 ? 0 : bs + 1;
       if (wm == 1) {
         if (u + 2 < nk) vmcnt_keep<NA + NB>();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1250,15 +1291,16 @@ int big_width(const GemmArgs& g) {
 
 template <bool A_KC, bool B_KC, int EPI, int ACT, int PP, int W, bool EXTRA, int X = 0>
 void launch_big(const GemmArgs& g, hipStream_t s) {
+  constexpr int smem = big::smem_bytes<B_KC, PP, W>();
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(
         reinterpret_cast<const void*>(&big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA, X>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, big::kSmemBytes);
+        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
   hipLaunchKernelGGL((big::gemm256_kernel<A_KC, B_KC, EPI, ACT, PP, W, EXTRA, X>), dim3(big_tiles(g, W), g.k_splits),
-                     dim3(big::kThreads), big::kSmemBytes, s, g);
+                     dim3(big::kThreads), smem, s, g);
 }
 
 // The product build instantiates the default main loop only (schedule 7, the
