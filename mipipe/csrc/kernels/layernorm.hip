@@ -94,7 +94,10 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(
 }
 
 // Row reduction of a pair over one 256-thread row group of a G-group block
-// (every thread of the block calls it: the barriers are block-wide).
+// (every thread of the block calls it: the barrier is block-wide).  Callers
+// alternate two scratch buffers by row parity, so one barrier per row is
+// enough: a buffer is written again two rows later, behind the next row's
+// barrier, which a thread reaches only after reading this row's sums.
 template <int G>
 __device__ __forceinline__ void group_sum2(float& a, float& b, float (*scratch)[8], int grp, int t) {
   const int lane = t & 63, wid = t >> 6;
@@ -107,8 +110,28 @@ __device__ __forceinline__ void group_sum2(float& a, float& b, float (*scratch)[
   __syncthreads();
   a = scratch[grp][0] + scratch[grp][1] + scratch[grp][2] + scratch[grp][3];
   b = scratch[grp][4] + scratch[grp][5] + scratch[grp][6] + scratch[grp][7];
-  __syncthreads();
 }
+
+// 8 elements kept as loaded (bf16: 4 registers instead of 8), converted on use.
+template <typename T> struct Raw8;
+template <> struct Raw8<float> {
+  float v[8];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+  __device__ __forceinline__ void load(const float* p) { Io<float>::load8(p, v); }
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+};
+template <> struct Raw8<bf16_t> {
+  u16x8 v;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0;
+  }
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const u16x8*>(p); }
+  __device__ __forceinline__ float get(int i) const { return bf2f(v[i]); }
+};
 
 // G row groups of 256 threads per block, each on its own row; the groups'
 // dgamma/dbeta partials are folded through LDS so a block writes ONE partial
@@ -119,11 +142,12 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
     const float* __restrict__ rstd_in, const T* __restrict__ gamma, T* __restrict__ dz, T* __restrict__ dx,
     float* __restrict__ dgamma_part, float* __restrict__ dbeta_part, int rows, int cols, float p,
     uint32_t threshold, uint64_t seed, uint64_t offset, const T* __restrict__ addend) {
-  __shared__ float scratch[G][8];
+  __shared__ float scratch[2][G][8];
   __shared__ float fold[G > 1 ? 2 * MAXV * 8 * kThreads : 1];
   const int grp = threadIdx.x / kThreads, t = threadIdx.x % kThreads;
   const int nvec = cols >> 3;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const float inv_n = 1.f / (float)cols;
 
   float g[MAXV][8];
   float dg[MAXV][8], db[MAXV][8];
@@ -135,76 +159,64 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
     if (vi < nvec) Io<T>::load8(gamma + vi * 8, g[k]);
   }
 
-  // Rows are software-pipelined: the next row's z / dy loads are in flight
-  // while this row's reductions and stores run.
   const int stride = gridDim.x * G;
   const int iters = (rows + stride - 1) / stride;  // uniform over the block (barriers inside)
   auto row_of = [&](int it) { return it * stride + blockIdx.x * G + grp; };
-  // The fan-out addend (the residual stream's other gradient) is prefetched
-  // with z and dy: loaded in the store loop it was a dependent HBM round trip
-  // on every row.
-  float zn[MAXV][8], dn[MAXV][8], an[MAXV][8];
   const bool has_add = addend != nullptr;
-  auto load_row = [&](int row) {
+  // A row as loaded -- z, dy and the fan-out addend kept raw (bf16: 4 registers
+  // per 8 elements, converted on use), its mean and rstd -- so rows can be
+  // loaded ahead without the conversion waiting on the load.
+  struct RowBuf {
+    Raw8<T> z[MAXV], d[MAXV], a[MAXV];
+    float mean, rstd;
+  };
+  auto load_row = [&](int row, RowBuf& r) {
+    const bool valid = row < rows;
+    r.mean = valid ? mean_in[row] : 0.f;
+    r.rstd = valid ? rstd_in[row] : 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
       const int vi = t + k * kThreads;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) zn[k][i] = dn[k][i] = an[k][i] = 0.f;
-      if (vi < nvec && row < rows) {
+      r.z[k].zero();
+      r.d[k].zero();
+      r.a[k].zero();
+      if (vi < nvec && valid) {
         const size_t e = (size_t)row * cols + (size_t)vi * 8;
-        Io<T>::load8(z + e, zn[k]);
-        Io<T>::load8(dy + e, dn[k]);
-        if (has_add) Io<T>::load8(addend + e, an[k]);
+        r.z[k].load(z + e);
+        r.d[k].load(dy + e);
+        if (has_add) r.a[k].load(addend + e);
       }
     }
   };
-  constexpr bool kPrefetch = MAXV <= 2;  // wider rows: the extra row would spill
-  if (kPrefetch) load_row(row_of(0));
-  for (int it = 0; it < iters; ++it) {
+  auto process = [&](int it, const RowBuf& r) {
     const int row = row_of(it);
-    const bool valid = row < rows;
-    const size_t base = (size_t)row * cols;
-    const float mean = valid ? mean_in[row] : 0.f;
-    const float rstd = valid ? rstd_in[row] : 0.f;
-    if (!kPrefetch) load_row(row);
-    float zc[MAXV][8], dc[MAXV][8], ac[MAXV][8];
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        zc[k][i] = zn[k][i];
-        dc[k][i] = dn[k][i];
-        ac[k][i] = an[k][i];
-      }
-    if (kPrefetch && it + 1 < iters) load_row(row_of(it + 1));
     float xh[MAXV][8], gy[MAXV][8];
     float a = 0.f, b = 0.f;  // sum(g*dy), sum(g*dy*xhat)
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        xh[k][i] = (zc[k][i] - mean) * rstd;
-        gy[k][i] = dc[k][i] * g[k][i];
-        dg[k][i] += dc[k][i] * xh[k][i];
-        db[k][i] += dc[k][i];
+        const float dv = r.d[k].get(i);
+        xh[k][i] = (r.z[k].get(i) - r.mean) * r.rstd;
+        gy[k][i] = dv * g[k][i];
+        dg[k][i] += dv * xh[k][i];
+        db[k][i] += dv;
         a += gy[k][i];
         b += gy[k][i] * xh[k][i];
       }
     }
-    group_sum2<G>(a, b, scratch, grp, t);
-    const float inv_n = 1.f / (float)cols;
+    group_sum2<G>(a, b, scratch[it & 1], grp, t);
     a *= inv_n;
     b *= inv_n;
-    if (valid) {
+    if (row < rows) {
 #pragma unroll
       for (int k = 0; k < MAXV; ++k) {
         const int vi = t + k * kThreads;
         if (vi < nvec) {
-          const size_t e = base + (size_t)vi * 8;
+          const size_t e = (size_t)row * cols + (size_t)vi * 8;
           float o[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = rstd * (gy[k][i] - a - xh[k][i] * b) + ac[k][i];
+          for (int i = 0; i < 8; ++i) o[i] = r.rstd * (gy[k][i] - a - xh[k][i] * b) + r.a[k].get(i);
           Io<T>::store8(dz + e, o);
           if (dx != nullptr) {
             const uint32_t keep = dropout_keep8(seed, offset, e, threshold);
@@ -214,6 +226,30 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
           }
         }
       }
+    }
+  };
+  if constexpr (MAXV <= 2) {
+    // Two rows in flight per group while one is reduced and stored: the loop is
+    // unrolled by two over two named buffers (a copy between buffers would wait
+    // for the loads in flight).  The mean / rstd loads travel with their row:
+    // read at the top of the row's iteration they were a dependent HBM round
+    // trip per row.
+    RowBuf b0, b1;
+    load_row(row_of(0), b0);
+    load_row(row_of(1), b1);
+    for (int it = 0; it < iters; it += 2) {
+      process(it, b0);
+      if (it + 2 < iters) load_row(row_of(it + 2), b0);
+      if (it + 1 < iters) {
+        process(it + 1, b1);
+        if (it + 3 < iters) load_row(row_of(it + 3), b1);
+      }
+    }
+  } else {  // wider rows: one row at a time (a second buffer would spill)
+    RowBuf b0;
+    for (int it = 0; it < iters; ++it) {
+      load_row(row_of(it), b0);
+      process(it, b0);
     }
   }
   if constexpr (G > 1) {
@@ -264,27 +300,6 @@ __global__ void __launch_bounds__(kThreads * G) ln_bwd_kernel(
 // Lane l holds 16-byte vectors l, l + 64, l + 128, l + 192 of its row.
 constexpr int kRowWaves = 8;
 constexpr int kRowNV = 4;
-
-// 8 elements kept as loaded (bf16: 4 registers instead of 8), converted on use.
-template <typename T> struct Raw8;
-template <> struct Raw8<float> {
-  float v[8];
-  __device__ __forceinline__ void zero() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 0.f;
-  }
-  __device__ __forceinline__ void load(const float* p) { Io<float>::load8(p, v); }
-  __device__ __forceinline__ float get(int i) const { return v[i]; }
-};
-template <> struct Raw8<bf16_t> {
-  u16x8 v;
-  __device__ __forceinline__ void zero() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 0;
-  }
-  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const u16x8*>(p); }
-  __device__ __forceinline__ float get(int i) const { return bf2f(v[i]); }
-};
 
 template <typename T>
 __global__ void __launch_bounds__(64 * kRowWaves) ln_fwd_rows_kernel(
