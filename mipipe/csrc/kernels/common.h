@@ -196,8 +196,15 @@ __device__ __forceinline__ float erf_as(float x) {
   return copysignf(y, x);
 }
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
+// GELU'(x) = Phi(x) + x phi(x).  erf_as(x / sqrt 2)'s exp(-x^2 / 2) is the
+// density's exponential: computed once (one transcendental fewer per element).
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  return 0.5f * (1.f + erf_as(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+  const float e = __expf(-0.5f * x * x);
+  const float ax = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float erf = copysignf(1.f - poly * e, x);
+  return 0.5f * (1.f + erf) + x * 0.3989422804014327f * e;
 }
 __host__ __device__ inline uint32_t dropout_threshold(float p) {
   double t = (double)p * 4294967296.0;

@@ -50,39 +50,52 @@ __global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ in,
         w[i][0] = r.x; w[i][1] = r.y; w[i][2] = r.z; w[i][3] = r.w;
       }
     }
+    // Activation backward: every load of the tile first (4 rows x 2 tensors, 16
+    // bytes each), then the math and the stores -- GELU' 153 -> 141 us at
+    // 18432 x 6400.  The one-tensor kernels (forward, dropout-only backward) load
+    // row by row: all-loads-first cost the dropout backward 92 -> 100 us
+    // (tools/bias_act_ab.py).
+    constexpr bool kAhead = BWD && ACT != kActNone;
+    const int nr = (int)(rows - q * 4 < 4 ? rows - q * 4 : 4);
+    float a[4][8], sv[4][8];
+    if (kAhead) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        if (rr < nr) {
+          const int64_t e = (q * 4 + rr) * cols + c0;
+          Io<T>::load8(in + e, a[rr]);
+          Io<T>::load8(saved + e, sv[rr]);
+        }
+      }
+    }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const int64_t row = q * 4 + rr;
-      if (row >= rows) break;
-      const int64_t e = row * cols + c0;
-      float a[8];
-      Io<T>::load8(in + e, a);
+      if (rr >= nr) break;
+      if (!kAhead) Io<T>::load8(in + (q * 4 + rr) * cols + c0, a[rr]);
       if (!BWD) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          float v = a[i] + b[i];
+          float v = a[rr][i] + b[i];
           if (ACT == kActRelu) v = fmaxf(v, 0.f);
           if (ACT == kActGelu) v = gelu_f(v);
           if (p > 0.f) v = drop_keep(w[i >> 1][rr], i & 1, thr16) ? v * scale : 0.f;
-          a[i] = v;
+          a[rr][i] = v;
         }
       } else {
         if (ACT != kActNone) {
-          float sv[8];
-          Io<T>::load8(saved + e, sv);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            if (ACT == kActRelu) a[i] = sv[i] > 0.f ? a[i] : 0.f;   // saved = the op's output
-            if (ACT == kActGelu) a[i] *= gelu_grad(sv[i] + b[i]);  // saved = pre-bias input
-            if (ACT == kActSavedGrad) a[i] *= sv[i];              // saved = act'(pre) itself
+            if (ACT == kActRelu) a[rr][i] = sv[rr][i] > 0.f ? a[rr][i] : 0.f;   // saved = the op's output
+            if (ACT == kActGelu) a[rr][i] *= gelu_grad(sv[rr][i] + b[i]);  // saved = pre-bias input
+            if (ACT == kActSavedGrad) a[rr][i] *= sv[rr][i];              // saved = act'(pre) itself
           }
         }
         if (p > 0.f) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = drop_keep(w[i >> 1][rr], i & 1, thr16) ? a[i] * scale : 0.f;
+          for (int i = 0; i < 8; ++i) a[rr][i] = drop_keep(w[i >> 1][rr], i & 1, thr16) ? a[rr][i] * scale : 0.f;
         }
       }
-      Io<T>::store8(out + e, a);
+      Io<T>::store8(out + (q * 4 + rr) * cols + c0, a[rr]);
     }
   }
 }
