@@ -3,7 +3,7 @@
 K-contiguous (the dgrad layout <A_KC, !B_KC>), plus what a transposition of X costs (torch copy).
 One process, arms interleaved, medians; fp32 output (the main_grad store epilogue).
 
-    python tools/wgrad_layout_probe.py > profiles/wgrad_layout_probe.txt
+    python tools/wgrad_layout_probe.py [T] [gpt2xl] > profiles/wgrad_layout_probe.txt
 """
 import statistics
 import sys
@@ -40,8 +40,11 @@ def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
     print(f"# T = {T} (K of the flush GEMM); TF/s of 2*M*N*T")
     print(f"{'case':10s} {'n_out':>6s} {'k_in':>6s} | {'II ms':>7s} {'TF/s':>6s} | {'KC^T ms':>7s} {'TF/s':>6s} | {'X^T copy ms':>11s}")
-    for name, n_out, k_in in [("qkv", 12288, 4096), ("out", 4096, 4096), ("dec", 28928, 4096), ("gpt fc1", 6400, 1600),
-                              ("gpt fc2", 1600, 6400)]:
+    shapes = [("qkv", 12288, 4096), ("out", 4096, 4096), ("dec", 28928, 4096), ("gpt fc1", 6400, 1600),
+              ("gpt fc2", 1600, 6400)]
+    if len(sys.argv) > 2 and sys.argv[2] == "gpt2xl":
+        shapes = [("gpt qkv", 4800, 1600), ("gpt out", 1600, 1600), ("gpt fc1", 6400, 1600), ("gpt fc2", 1600, 6400)]
+    for name, n_out, k_in in shapes:
         dy = torch.randn(T, n_out, device=dev).to(torch.bfloat16)
         x = torch.randn(T, k_in, device=dev).to(torch.bfloat16)
         xt = x.t().contiguous()
