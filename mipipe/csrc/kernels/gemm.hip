@@ -1441,7 +1441,7 @@ __global__ void __launch_bounds__(256) colsum_splits_kernel(const float* __restr
   colsum[n] += v;
 }
 
-int g_gemm_splitk = -1;  // MIPIPE_GEMM_SPLITK=0 disables (A/B); -1 unread
+int g_gemm_splitk = -1;  // MIPIPE_GEMM_SPLITK: 0 off, 1 auto (default), n >= 2 forced n ways (A/B); -1 unread
 
 template <bool A_KC, bool B_KC, int EPI>
 void launch_act(const GemmArgs& g, hipStream_t s) {
@@ -1472,6 +1472,7 @@ bool gemm_ab_build() {
 }
 void gemm_set_width(int w) { g_gemm_width = w; }
 void gemm_set_rounds(int on) { g_gemm_rounds = on; }
+void gemm_set_splitk(int n) { g_gemm_splitk = n; }
 int gemm_get_schedule() { return big::gemm_sched(); }
 
 bool gemm_rowsum_ok(const GemmArgs& g) {
@@ -1521,6 +1522,7 @@ int gemm_splitk_factor(const GemmArgs& g) {
   if (!(plain_bf16 || f32_out) || !use_big(g) || g.K < 8192) return 1;
   const int tiles = big_tiles(g, 256);
   const int kt = g.K / BK;
+  if (g_gemm_splitk >= 2) return std::max(1, std::min(g_gemm_splitk, kt / 16));  // forced (gemm_set_splitk, A/B)
   const double t_tile = 2.0 * 256 * 256 * (double)g.K / 4.5e12;
   const double mn = (double)g.M * g.N;
   int best = 1;

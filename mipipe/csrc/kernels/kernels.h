@@ -184,6 +184,7 @@ bool gemm_set_schedule(int mode);
 bool gemm_ab_build();
 void gemm_set_width(int w);    // 256-row GEMM block width: 0 auto, 128, 256
 void gemm_set_rounds(int on);  // 1: multi-round grids launched one round at a time (default), 0: one launch
+void gemm_set_splitk(int n);  // split-K factor: 0 off, 1 auto (gemm_splitk_factor), n >= 2 forced (A/B tools)
 int gemm_get_schedule();
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
 // Same interface with fp32 operands (and fp32 bias / res / aux / C): v_mfma_f32_32x32x2_f32.
