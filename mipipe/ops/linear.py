@@ -320,8 +320,10 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 # (C^T = X^T . dY, ~15 % faster than reading both operands I-contiguous:
 # profiles/wgrad_layout_probe.txt) comes from -- MIPIPE_WGRAD_XT:
 #   auto (default): the flush transposes x (transpose_b16, a streaming kernel)
-#        for weights with at least _XT_MIN_N output features and >= 512 tiles,
-#        where the GEMM saving outgrows the transpose (~N_out / 3600 x its cost);
+#        for weights with at least _XT_MIN_N output features, where the GEMM
+#        saving outgrows the transpose (~N_out / 3600 x its cost) -- and the
+#        bias gradient folds into the GEMM (split-K grids included) instead of
+#        a column-sum pass over dY;
 #   emit: the forward GEMM writes x^T from its staged A tiles (every tile-path
 #        linear; +x^T bytes of activation memory, and ~40 us per forward GEMM:
 #        a wash on enc12, profiles/wgrad_xt_ab.txt);
@@ -329,7 +331,7 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 _XT_MODE = os.environ.get("MIPIPE_WGRAD_XT", "auto")
 _EMIT_XT = _XT_MODE in ("1", "emit")
 _XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "6144"))
-_XT_MIN_TILES = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_TILES", "512"))
+_XT_MIN_TILES = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_TILES", "0"))
 # GELU forwards save GELU'(pre) rather than pre (MIPIPE_GELU_SAVE_GRAD=1).  Off by
 # default: the second erf/exp per element in the forward GEMM's epilogue cost the
 # GPT-2-XL step more than the one-multiply backward saved (the elementwise GELU
@@ -471,8 +473,10 @@ def _transpose_pays(w: Tensor, dys, xs, T: int) -> bool:
     wide enough outputs, bf16, shapes the transpose and the GEMM accept."""
     if _XT_MODE != "auto" or w.shape[0] < _XT_MIN_N or T % 64 != 0:
         return False
-    # grids of < 2 rounds of 256x256 tiles run split-K and quantise the same in
-    # either layout (GPT-2-XL fc1: 175 tiles, 1454 vs 1461 us): no gain to pay for
+    # split-K grids too: GPT-2-XL's fc1 (175 tiles, split 7 ways) runs the two
+    # layouts level, but its 6400-wide bias gradient folds into the transposed
+    # GEMM instead of a column-sum pass over dY -- +0.47 % on the GPT-2-XL step
+    # (tools/gpu_runs/r4_b20.sh; MIPIPE_WGRAD_XT_MIN_TILES restores a tile floor)
     if ((w.shape[1] + 255) // 256) * ((w.shape[0] + 255) // 256) < _XT_MIN_TILES:
         return False
     x0 = xs[0]
