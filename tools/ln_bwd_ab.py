@@ -17,6 +17,10 @@ CASES = [  # rows, cols, dtype, addend, p
     (8192, 4096, torch.bfloat16, False, 0.0),
     (8192, 1024, torch.bfloat16, True, 0.1),
     (4096, 4096, torch.float32, True, 0.1),
+    # the wave-per-row kernel (<= 2048 columns): GPT-2-XL's 1600, ref_main's fp32 2048
+    (18432, 1600, torch.bfloat16, True, 0.0),
+    (18432, 1600, torch.bfloat16, False, 0.1),
+    (8192, 2048, torch.float32, True, 0.1),
 ]
 
 

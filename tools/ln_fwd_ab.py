@@ -1,4 +1,4 @@
-"""LayerNorm forward (rows wider than 2048: the one-row-per-block kernel) at training shapes, for a same-box
+"""LayerNorm forward (both kernels: one row per block above 2048 columns, one per wave up to 2048) at training shapes, for a same-box
 A/B of two builds: per-call time and the outputs.
 
     python tools/ln_fwd_ab.py ROOT TAG                # ROOT: repo root whose mipipe/_C.so to load
@@ -17,6 +17,9 @@ CASES = [  # rows, cols, dtype, residual, p
     (8192, 4096, torch.bfloat16, True, 0.0),
     (8192, 4096, torch.float32, True, 0.1),
     (4096, 8192, torch.bfloat16, True, 0.1),
+    # the wave-per-row kernel (<= 2048 columns): GPT-2-XL's pre-norm 1600, ref_main's fp32 2048
+    (18432, 1600, torch.bfloat16, False, 0.0),
+    (8192, 2048, torch.float32, True, 0.1),
 ]
 
 
