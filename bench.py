@@ -278,6 +278,7 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     sync()
+    tele = _telemetry(device) if on_gpu else None
     t0 = time.perf_counter()
     for k in range(args.steps):
         mark(f"timed step {k}")
@@ -288,6 +289,7 @@ def main() -> int:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    tele = tele.stop() if tele is not None else None
     ms = elapsed / max(args.steps, 1) * 1e3
     ms_t = torch.tensor([ms], device=device)
     if world > 1:
@@ -328,6 +330,10 @@ def main() -> int:
         loss_val = float(lt.item())
 
     comm = _comm_report(engine, device, world, local, on_gpu)
+    teles = [tele]
+    if world > 1:
+        teles = [None] * world
+        dist.all_gather_object(teles, tele)
     armed.__exit__(None, None, None)
     if wd is not None:
         wd.close()
@@ -388,12 +394,21 @@ def main() -> int:
             "peak_hbm_gib_per_gpu": [round(x, 2) for x in peaks] if on_gpu else None,
             "baseline_note": _baseline_note(ref_match, args.checkpoint),
             "comm": comm,
+            "telemetry": teles[0] if world == 1 else teles,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _telemetry(device):
+    """GPU clock / power / temperature over the timed region (mipipe.utils.telemetry;
+    firmware counters read on a side thread, no GPU work)."""
+    from mipipe.utils.telemetry import GpuTelemetry
+
+    return GpuTelemetry(device.index if device.index is not None else 0).start()
 
 
 def _comm_report(engine, device, world, local, on_gpu):
