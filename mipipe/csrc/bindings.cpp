@@ -1157,6 +1157,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("seq"), py::arg("consumer_stream"))
       .def("done", &ipc::Link::done)
       .def("abort", &ipc::Link::abort)
+      .def("drain", &ipc::Link::drain, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("message_bytes", &ipc::Link::message_bytes)
       .def("unlink", &ipc::Link::unlink)
       .def("describe", &ipc::Link::describe)
       .def_property_readonly("copy_stream", [](const ipc::Link& L) { return reinterpret_cast<int64_t>(L.copy_stream()); })

@@ -219,10 +219,18 @@ Link::~Link() {
   try {
     if (!host_mode() && sh_ != nullptr) {
       DeviceGuard g(device_);
-      // Everything this side queued on the link has run before a mapping goes:
-      // the sender's copy stream, the receiver's releases (on its streams).
-      if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
-      else (void)hipDeviceSynchronize();
+      // Everything this side queued on the link has run before a mapping goes.
+      // Each slot's event is recorded right after the flag write of the last
+      // send (on the stream the copy used: the copy stream, or the producer's
+      // for the inline engines) or the last release (the consumer's stream),
+      // so those events cover every write into the peer's memory.  Bounded:
+      // after a peer failure a send may wait forever for a slot the dead
+      // receiver never frees -- then the mappings are left to process teardown
+      // instead of hanging here (abort() releases this side's own waits).
+      if (!drain(30.0)) {
+        IPC_TRACE("  %s: queued work did not drain in 30 s; mappings left to teardown", name_.c_str());
+        throw std::runtime_error("undrained");
+      }
       if (sender_) {
         if (ring_) (void)hipIpcCloseMemHandle(ring_);
         sh_->sender_detached.store(1, std::memory_order_release);
@@ -254,7 +262,63 @@ Link::~Link() {
 int64_t Link::nslots() const { return sh_->nslots; }
 int64_t Link::slot_bytes() const { return sh_->slot_bytes; }
 
-void Link::abort() { sh_->aborted.store(1, std::memory_order_release); }
+bool Link::drain(double timeout_s) const {
+  if (host_mode()) return true;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  auto quiet = [&](auto query) {
+    for (;;) {
+      const hipError_t e = query();
+      if (e != hipErrorNotReady) return true;  // done (or an error: nothing left to wait for)
+      if (std::chrono::steady_clock::now() > deadline) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  };
+  if (events_)
+    for (int64_t k = 0; k < sh_->nslots; ++k)
+      if (!quiet([&] { return hipEventQuery(events_[k]); })) return false;
+  if (copy_stream_ && !quiet([&] { return hipStreamQuery(copy_stream_); })) return false;
+  return true;
+}
+
+void Link::abort() {
+  sh_->aborted.store(1, std::memory_order_release);
+  if (host_mode() || aborted_local_) return;
+  aborted_local_ = true;
+  // Device mode: every wait on this side is a hipStreamWaitValue64 on a flag
+  // this side OWNS (receiver: the full flags at the head of its ring; sender:
+  // its freed flags).  Saturating them lets every pending and future wait
+  // pass, so the streams drain instead of blocking forever on a dead peer
+  // (the step is being torn down with an error anyway; the slots' contents
+  // no longer matter).  Written from a stream of our own, never the
+  // compute stream that may be the one stuck in the wait.
+  char* flags = sender_ ? freed_ : ring_;
+  if (flags == nullptr || (sender_ && !owns_freed_)) return;
+  try {
+    DeviceGuard g(device_);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+    for (int64_t k = 0; k < sh_->nslots; ++k)
+      (void)hipStreamWriteValue64(s, flags + k * kFlagStride, ~0ull, 0);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(5);
+    while (hipStreamQuery(s) == hipErrorNotReady && std::chrono::steady_clock::now() < deadline)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    IPC_TRACE("abort %s: %lld flags saturated", name_.c_str(), (long long)sh_->nslots);
+    // the stream is leaked if its writes are still queued (destroying it would block)
+    if (hipStreamQuery(s) != hipErrorNotReady) (void)hipStreamDestroy(s);
+  } catch (...) {
+  }
+}
+
+int64_t Link::message_bytes(uint64_t seq) const {
+  // the sender records each message's byte count in the shared block when it
+  // enqueues the send; -1 while message seq has not been enqueued yet (or the
+  // slot already holds a later one)
+  const int k = int(seq % uint64_t(sh_->nslots));
+  const uint64_t sent = sh_->sent.load(std::memory_order_acquire);
+  if (sent < seq + 1) return -1;
+  if (sent > seq + uint64_t(sh_->nslots)) return -2;
+  return (int64_t)sh_->slots[k].bytes;
+}
 void Link::unlink() { shm_unlink(name_.c_str()); }
 
 char* Link::slot(uint64_t seq) const {

@@ -85,8 +85,17 @@ class Link {
   // released (device mode: an event query, never blocks).
   bool done(uint64_t seq) const;
 
-  // Unblocks host-mode waits with an error (a failed peer, a watchdog).
+  // A failed peer, a watchdog: unblocks host-mode waits with an error, and
+  // (device mode) saturates the flags this side owns so its pending
+  // hipStreamWaitValue64s pass instead of blocking the streams forever.
   void abort();
+  // Waits (bounded) until everything this side queued on the link has run:
+  // every slot's last send / release event and the copy stream.  False on
+  // timeout.
+  bool drain(double timeout_s) const;
+  // Byte count of message seq as the sender enqueued it; -1 while the sender
+  // has not enqueued it yet, -2 once its slot holds a later message.
+  int64_t message_bytes(uint64_t seq) const;
   // Removes the shm name (after both sides are attached; the mapping stays).
   void unlink();
   std::string describe() const;
@@ -112,6 +121,7 @@ class Link {
   hipStream_t copy_stream_ = nullptr;
   hipEvent_t* events_ = nullptr;  // one per slot: sender after the copy, receiver after the release
   uint64_t next_seq_ = 0;
+  bool aborted_local_ = false;     // abort() already saturated this side's flags
   uint64_t last_done_seq_ = 0;    // receiver: 1 + last released sequence (host bookkeeping)
 };
 

@@ -111,9 +111,11 @@ class _ViewWork:
         return True
 
     def is_completed(self) -> bool:
-        # arrival is a GPU-side event the host does not poll; a receive counts as
-        # complete once its wait is on the stream (the watchdog reports the rest)
-        return self.waited
+        # arrival is a GPU-side event the host does not poll: a receive counts as
+        # complete once its wait is on the stream AND the sender has enqueued the
+        # message (the shared block's send count), so a stalled peer shows up in
+        # the watchdog's pending-transfer report
+        return self.waited and self.link.message_bytes(self.seq) != -1
 
 
 class IpcChannels:
@@ -169,7 +171,7 @@ class IpcChannels:
         self._act_in = self._act_out = self._grad_in = self._grad_out = None
         self._links: list = []
         self._copy_streams: Dict[int, torch.cuda.ExternalStream] = {}
-        self._held: List[Tuple[object, int]] = []  # (link, seq) read in place, released at end_step
+        self._held: List[Tuple[object, int, int]] = []  # (link, seq, bytes) read in place, released at end_step
         if self.rank < 0 or n < 2:
             dist.barrier()
             dist.barrier()
@@ -221,7 +223,9 @@ class IpcChannels:
         return out
 
     def abort(self) -> None:
-        """Unblocks every host-mode wait on this rank's links with an error."""
+        """A failed step: unblocks every host-mode wait on this rank's links with
+        an error, and lets every pending GPU-side wait on a flag this rank owns
+        pass (``IpcLink.abort``), so the streams drain instead of hanging."""
         for link in self._links:
             link.abort()
 
@@ -266,7 +270,7 @@ class IpcChannels:
             return t, self._recv(link, t)
         seq = link.post()
         t = link.slot_tensor(seq, list(shape), dtype, self.device.index)  # the GPU wait comes with work.wait()
-        self._held.append((link, seq))
+        self._held.append((link, seq, t.numel() * t.element_size()))
         return t, _ViewWork(self, link, seq, self.device)
 
     def send_act(self, t: Tensor):
@@ -293,9 +297,18 @@ class IpcChannels:
         if not self._held:
             return
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        for link, seq in self._held:
+        bad = []
+        for link, seq, nbytes in self._held:
             link.release(seq, stream)
+            # the device-side wait cannot compare sizes: check the sender's byte
+            # count here, once it has enqueued the message (-1: not yet, -2: gone)
+            sent = link.message_bytes(seq)
+            if sent >= 0 and sent != nbytes:
+                bad.append(f"message {seq} on {link.describe()}: sender wrote {sent} B, the receive read {nbytes} B")
         self._held = []
+        if bad:
+            raise RuntimeError("mipipe ipc: message size mismatch (the ranks disagree on a boundary shape): "
+                               + "; ".join(bad))
 
     def close(self) -> None:
         """Tears the links down: every sender unmaps its peer's ring, then (after
@@ -303,6 +316,11 @@ class IpcChannels:
         Collective when ``dist`` is initialised."""
         if self.device.type == "cuda":
             self.end_step()
+            # bounded: a link whose peer died would otherwise block the
+            # synchronize forever (abort() saturates this side's flags first)
+            stuck = [link.describe() for link in self._links if not link.drain(60.0)]
+            if stuck:
+                raise RuntimeError("mipipe ipc: links did not drain in 60 s: " + "; ".join(stuck))
             torch.cuda.synchronize(self.device)
         # the ExternalStream wrappers go before the links destroy their streams
         self._copy_streams = {}
