@@ -1227,6 +1227,10 @@ PYBIND11_MODULE(_C, m) {
         "multi-round GEMM grids whose last round is at most half full: 0 one launch, 1 (default) one launch per round "
         "of tiles when K >= 4096, 2 one launch per round at any K");
   m.def("gemm_set_splitk", &gemm_set_splitk, "split-K factor of under-filled long-K GEMMs: 0 off, 1 auto (default), n >= 2 forced");
+  m.def("gemm_set_waves", &gemm_set_waves,
+        "256x256 GEMM blocks: 4 = one wave per SIMD with a 128x128 tile each (gemm4w_kernel), 8 = the ping-pong kernel, "
+        "0 = default");
+  m.def("gemm_get_waves", &gemm_get_waves);
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none(),

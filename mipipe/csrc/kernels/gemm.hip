@@ -448,13 +448,15 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
 // per store (+ the bf16 addend `res`, read as 16-byte row chunks), fp32
 // read-modify-write (kEpiAccumF32) or fp32 stores.  Starts with the LDS free,
 // ends with a barrier (so it can run twice: aux, then the output).
-template <int EPI, int W>
-__device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W / 64], int wm, int wn, int lane,
+// NJ: 16-wide accumulator tiles per wave (W / 64 for the 8-wave kernel, whose
+// wave tile is 128 x W/4; 8 for the 4-wave kernel's 128 x 128), kT: threads.
+template <int EPI, int W, int NJ = W / 64, int kT = 512>
+__device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][NJ], int wm, int wn, int lane,
                                              int tid, int m0, int n0, int M, int N, int64_t ldc, void* out,
                                              const bf16_t* res, int64_t ldr = 0, const bf16_t* dact_in = nullptr,
                                              int64_t ldd = 0, int dact = 0, float dact_scale = 1.f,
                                              bool trans = false, bool dgelu = false) {
-  constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512;
+  constexpr int WN = 16 * NJ, kStride = W + 4;
   const int quad = lane >> 4, col_in = lane & 15;
   float* stg = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -554,10 +556,10 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][W
 // (18432 x 6400 x 1600, GELU, p 0.1, pre saved) cost 542 us against 358 plain
 // (tools/epilogue_cost_probe.py).  Also the activation backward of a dgrad
 // whose forward had dropout (dact_in with the mask regenerated).
-template <int ACT, int W>
-__device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[8][W / 64], int wm, int wn,
+template <int ACT, int W, int NJ = W / 64, int kT = 512>
+__device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[8][NJ], int wm, int wn,
                                                  int lane, int tid, int m0, int n0, const GemmArgs& g) {
-  constexpr int NJ = W / 64, WN = W / 4, kStride = W + 4, kT = 512, CB = W / 8;
+  constexpr int WN = 16 * NJ, kStride = W + 4, CB = W / 8;
   const int quad = lane >> 4, col_in = lane & 15;
   float* stg = reinterpret_cast<float*>(smem);
   bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
@@ -1253,6 +1255,265 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
                          EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
 }
 
+// ============================================================================
+// 4-wave variant: the same 256x256x64 block tile, LDS
+// images, staging offsets and epilogues, computed by 4 waves instead of 8 --
+// 2 M x 2 N, a 128x128 tile per wave (8x8 v_mfma_f32_16x16x32_bf16
+// accumulators: 256 registers, AGPRs), ONE wave per SIMD.  Per k32-step a
+// wave reads 16 fragments (8 A + 8 B) for 64 MFMAs, 256 B of LDS per MFMA
+// against the 8-wave kernel's 384 (128x64 wave tile): a third less LDS
+// traffic and issue.  With no partner wave on the SIMD, the LDS latency is
+// hidden inside the wave: the fragments of the next k32-step are read
+// between the MFMAs of this one (one read after every 4th MFMA), and the
+// K-tile two ahead is staged by LDS-DMA in the same stream (one 1 KiB piece
+// after every 4th MFMA of the second k-step).  One barrier per K-tile,
+// between its two k-steps:
+//   k-step 0 of tile u:  MFMAs on fragments (u, 0); reads of (u, 1) from cur
+//   wait: this wave's DMAs of tile u+1 landed, its reads of cur retired
+//   barrier            -> cur is free for restaging, tile u+1 readable
+//   k-step 1 of tile u:  MFMAs on (u, 1); reads of (u+1, 0) from nxt; DMA of
+//                        tile u+2 into cur
+// Past the last tiles the DMA restages the last tile and the reads read the
+// other buffer (both harmless: nothing reads them), so the stream has no
+// branches.  Compiler scheduling is pinned by sched_barriers between the
+// MFMA groups.  A^T emission is not supported (launch_big_w keeps those on
+// the 8-wave kernel).
+template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA, int X = 0>
+__global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
+  constexpr int W = 256, NJ = 8, WN = 128;
+  constexpr int kBuf = 2 * kTileBytes;  // A + B tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  tile_coords((g.M + BM - 1) / BM, (g.N + W - 1) / W, tm, tn, g.group_m);
+  tm = __builtin_amdgcn_readfirstlane(tm);
+  tn = __builtin_amdgcn_readfirstlane(tn);
+  const int m0 = tm * BM, n0 = tn * W;
+  f32x4 acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fused bias gradient, A side (GemmArgs::rowsum): as the 8-wave kernel's
+  // group 0, with all 256 threads
+  const bool rsum = g.rowsum != nullptr && tn < 16 && !A_KC;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto rowsum_step = [&](const char* tile) {
+    if (rsum) {
+      const int r = tid >> 2, c8 = 4 * tn + (tid & 3);
+      const s16x4 v = *reinterpret_cast<const s16x4*>(tile + ic_off_w<256>(r, c8));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rs[e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+    }
+  };
+  // fused bias gradient, B side (GemmArgs::colsum): the 8-wave kernel's two
+  // group slices, both summed by these 256 threads
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int cm_log = __builtin_amdgcn_readfirstlane(2 * tiles_m * 16 >= W ? 0 : 2 * tiles_m * 32 >= W ? 1
+                                                    : 2 * tiles_m * 64 >= W ? 2 : 3);
+  const bool csum0 = X == kXColsum && !B_KC && g.colsum != nullptr && tm < (W / 16 >> cm_log);
+  const bool csum1 = X == kXColsum && !B_KC && g.colsum != nullptr && tm + tiles_m < (W / 16 >> cm_log);
+  float cs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  auto colsum_step = [&](const char* btile) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 0 ? csum0 : csum1) {
+        const int csl = tm + tiles_m * q;
+        const int qq = tid & ((4 << cm_log) - 1), r0 = tid >> (2 + cm_log);
+        for (int j = 0; j < (1 << cm_log); ++j) {
+          const s16x4 v = *reinterpret_cast<const s16x4*>(
+              btile + ic_off_w<W>(r0 + (j << (6 - cm_log)), (4 << cm_log) * csl + qq));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[q][e] += __uint_as_float((uint32_t)(uint16_t)v[e] << 16);
+        }
+      }
+    }
+  };
+
+  int kt0 = 0, nk = g.K / BK;
+  if (g.k_splits > 1) {
+    const int total = nk;
+    kt0 = (int)blockIdx.y * total / g.k_splits;
+    nk = ((int)blockIdx.y + 1) * total / g.k_splits - kt0;
+  }
+  // staging: wave w takes the 8-wave shares w and w + 4 of each operand tile
+  uint32_t offA0[4], offA1[4], offB0[4], offB1[4];
+  stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave, lane, offA0);
+  stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave + 4, lane, offA1);
+  stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave, lane, offB0);
+  stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave + 4, lane, offB1);
+  // piece d (0-15) of K-tile kt into buffer buf: A shares (d 0-7), then B
+  auto stage_piece = [&](int kt, char* buf, int d) {
+    int kl;
+    if (d < 8) {
+      const char* b = reinterpret_cast<const char*>(seg_base(g, true, (kt0 + kt) * BK, kl));
+      b += A_KC ? (int64_t)kl * 2 : (int64_t)kl * g.lda * 2;
+      const int sh = d < 4 ? wave : wave + 4;
+      glds16_saddr(b, d < 4 ? offA0[d & 3] : offA1[d & 3], buf + (sh * 4 + (d & 3)) * 1024);
+    } else {
+      const char* b = reinterpret_cast<const char*>(seg_base(g, false, (kt0 + kt) * BK, kl));
+      b += B_KC ? (int64_t)kl * 2 : (int64_t)kl * g.ldb * 2;
+      const int sh = d < 12 ? wave : wave + 4;
+      glds16_saddr(b, d < 12 ? offB0[d & 3] : offB1[d & 3], buf + kTileBytes + (sh * 4 + (d & 3)) * 1024);
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < 16; ++d) stage_piece(0, smem, d);
+  if (nk > 1) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) stage_piece(1, smem + kBuf, d);
+    vmcnt_keep<16>();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  bf16x8 fa[2][8], fb[2][8];  // [k-step][tile]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[0][i] = frag<A_KC, 256>(smem, wm * 128 + 16 * i, 0, lane);
+    fb[0][i] = frag<B_KC, W>(smem + kTileBytes, wn * WN + 16 * i, 0, lane);
+  }
+  for (int u = 0; u < nk; ++u) {
+    char* cur = smem + (u & 1) * kBuf;
+    char* nxt = smem + ((u + 1) & 1) * kBuf;
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- k-step 0: MFMAs on (u, 0), fragment reads of (u, 1) ----
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+        if ((j & 3) == 3) {
+          const int q = 2 * i + (j >> 2);
+          if (q < 8) fa[1][q] = frag<A_KC, 256>(cur, wm * 128 + 16 * q, 1, lane);
+          else fb[1][q - 8] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * (q - 8), 1, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    rowsum_step(cur);
+    colsum_step(cur + kTileBytes);
+    // this wave's DMAs of tile u+1 have landed and its reads of cur retired;
+    // after the barrier cur may be restaged and nxt read
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int ks = u + 2 < nk ? u + 2 : nk - 1;
+    // ---- k-step 1: MFMAs on (u, 1), reads of (u+1, 0), DMA of tile u+2 ----
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+        const int gi = NJ * i + j;
+        if ((gi & 3) == 1) stage_piece(ks, cur, gi >> 2);
+        if ((gi & 3) == 3) {
+          const int q = gi >> 2;
+          if (q < 8) fa[0][q] = frag<A_KC, 256>(nxt, wm * 128 + 16 * q, 0, lane);
+          else fb[0][q - 8] = frag<B_KC, W>(nxt + kTileBytes, wn * WN + 16 * (q - 8), 0, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  if (rsum) {  // K-rows -> one sum per row: lanes (xor over the K-row bits), then the 4 waves through LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) rs[e] += __shfl_xor(rs[e], o, 64);
+    if (lane < 4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave * 16 + 4 * lane + e] = rs[e];
+    __syncthreads();
+    if (tid < 16) {
+      const float v = red[tid] + red[16 + tid] + red[32 + tid] + red[48 + tid];
+      const int row = m0 + 16 * tn + tid;
+      if (row < g.M) g.rowsum[row] += v;
+    }
+  }
+  if (X == kXColsum && g.colsum != nullptr) {  // the 8-wave kernel's reduction, slice q in place of group q
+    __syncthreads();
+    const int sw = 16 << cm_log;
+    float* red = reinterpret_cast<float*>(smem) + 64;  // [2 slices x 4 waves][sw columns]
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        for (int o = 4 << cm_log; o < 64; o <<= 1) cs[q][e] += __shfl_xor(cs[q][e], o, 64);
+      if (lane < (4 << cm_log))
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[(4 * q + wave) * sw + 4 * lane + e] = cs[q][e];
+    }
+    __syncthreads();
+    for (int t = tid; t < 2 * sw; t += 256) {
+      const int gq = t >> (4 + cm_log), c = t & (sw - 1);
+      const int sl = tm + tiles_m * gq;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += red[(4 * gq + w) * sw + c];
+      const int col = n0 + sw * sl + c;
+      if (sl < (W / 16 >> cm_log) && col < g.N) {
+        if (g.k_splits > 1) g.colsum[(int64_t)blockIdx.y * g.N + col] = v;
+        else g.colsum[col] += v;
+      }
+    }
+  }
+  // ---- epilogue (as the 8-wave kernel's, on the 128x128 wave layout) ----
+  const int quad = lane >> 4, col_in = lane & 15;
+  __syncthreads();
+  if (EPI == kEpiStoreBf16 && EXTRA) {
+    const int ncol = n0 + wn * WN + col_in;
+    if (g.bias != nullptr) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float b = ncol + 16 * j < g.N ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[ncol + 16 * j]) : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] += b;
+      }
+    }
+    staged_store_act<ACT, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g);
+    return;
+  }
+  if (EPI == kEpiStoreBf16 && (ACT != kActNone || g.bias != nullptr)) {
+    const int ncol = n0 + wn * WN + col_in, nrow = m0 + wm * 128 + 4 * quad;
+    const float pscale = g.p > 0.f ? 1.f / (1.f - g.p) : 1.f;
+    const EpiParams ep{g.seed, g.offset, g.N, g.p, pscale, g.threshold, g.mask_row0, g.mask_col0,
+                       g.mask_ld > 0 ? g.mask_ld : g.N};
+    float bias[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      bias[j] = (g.bias != nullptr && ncol + 16 * j < g.N) ? bf2f(reinterpret_cast<const bf16_t*>(g.bias)[ncol + 16 * j]) : 0.f;
+    epi_rows<0, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<1, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<2, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<3, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<4, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<5, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<6, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+    epi_rows<7, ACT, NJ, EXTRA>(ep, acc, nrow, ncol, bias);
+  }
+  void* out = EPI == kEpiStoreBf16 ? g.C
+                                   : reinterpret_cast<void*>(reinterpret_cast<float*>(g.C) +
+                                                             (int64_t)blockIdx.y * g.M * g.ldc);
+  if (EPI == kEpiStoreBf16 && g.dact_in != nullptr)
+    staged_store<EPI, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+                                  reinterpret_cast<const bf16_t*>(g.res), g.ldr,
+                                  reinterpret_cast<const bf16_t*>(g.dact_in), g.ldd, g.dact, g.dact_scale);
+  else if (EPI != kEpiStoreBf16 && g.trans_c && g.k_splits <= 1)
+    staged_store<EPI, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out, nullptr, 0, nullptr, 0,
+                                  0, 1.f, true);
+  else
+    staged_store<EPI, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+                                  EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
+}
+
 }  // namespace big
 
 int big_tiles(const GemmArgs& g, int w) { return ((g.M + big::BM - 1) / big::BM) * ((g.N + w - 1) / w); }
@@ -1307,9 +1568,43 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
 // whole-tile ping-pong).  The A/B schedules 0-6 are compiled in only with
 // -DMIPIPE_GEMM_AB (python -m mipipe.build --gemm-ab), for tools/gemm_sched_ab.py
 // and the like; without it gemm_set_schedule() accepts 7 alone.
+// 256-wide blocks: the 4-wave kernel (gemm4w_kernel) or the 8-wave one.
+// gemm_set_waves(4 / 8) or MIPIPE_GEMM_WAVES picks; 0 = default (8).
+int g_gemm_waves = -1;
+int gemm_waves() {
+  if (g_gemm_waves < 0) {
+    const char* e = getenv("MIPIPE_GEMM_WAVES");
+    g_gemm_waves = e ? atoi(e) : 0;
+  }
+  return g_gemm_waves == 4 ? 4 : 8;
+}
+
+template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA, int X = 0>
+void launch_4w(const GemmArgs& g, hipStream_t s) {
+  constexpr int smem = big::kSmemBytes;  // the epilogue's staging image (130 KiB); the main loop uses 128 KiB
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&big::gemm4w_kernel<A_KC, B_KC, EPI, ACT, EXTRA, X>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((big::gemm4w_kernel<A_KC, B_KC, EPI, ACT, EXTRA, X>), dim3(big_tiles(g, 256), g.k_splits),
+                     dim3(256), smem, s, g);
+}
+
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
   const bool narrow = big_width(g) == 128;
+  if (!narrow && g.at == nullptr && gemm_waves() == 4) {
+    if constexpr (A_KC && !B_KC && EPI != kEpiStoreBf16 && !EXTRA) {
+      if (g.colsum != nullptr) {
+        launch_4w<A_KC, B_KC, EPI, ACT, EXTRA, big::kXColsum>(g, s);
+        return;
+      }
+    }
+    launch_4w<A_KC, B_KC, EPI, ACT, EXTRA>(g, s);
+    return;
+  }
   if constexpr (A_KC && B_KC && EPI == kEpiStoreBf16 && !(ACT == kActGelu && EXTRA)) {
     if (g.at != nullptr) {  // forward GEMM that also writes A^T (gemm_emit_ok)
       if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA, big::kXEmit>(g, s);
@@ -1472,6 +1767,8 @@ bool gemm_ab_build() {
 }
 void gemm_set_width(int w) { g_gemm_width = w; }
 void gemm_set_rounds(int on) { g_gemm_rounds = on; }
+void gemm_set_waves(int w) { g_gemm_waves = w; }
+int gemm_get_waves() { return gemm_waves(); }
 void gemm_set_splitk(int n) { g_gemm_splitk = n; }
 int gemm_get_schedule() { return big::gemm_sched(); }
 

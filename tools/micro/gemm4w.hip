@@ -73,17 +73,43 @@ __device__ __forceinline__ uint32_t piece_off(int64_t ld, int i0, int lim, int p
   return (uint32_t)(((int64_t)gi * ld + 8 * c) * 2);
 }
 
+// I-contiguous image [64 rows (k)][256 i]: 512-byte rows, 8-byte chunk c of row
+// r at chunk c ^ (4 rk(r)), rk(r) = (r & 3) | (((r >> 3) & 1) << 2).
+__device__ __forceinline__ int ic_rk(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int ic_off(int r, int c8) { return r * 512 + ((c8 ^ (ic_rk(r) << 2)) << 3); }
+
+// Per-lane source offsets of piece p of an I-contiguous tile (2 k-rows of 256).
+__device__ __forceinline__ uint32_t piece_off_ic(int64_t ld, int i0, int lim, int p, int lane) {
+  const int row = 2 * p + (lane >> 5);
+  const int c16 = (lane & 31) ^ (ic_rk(row) << 1);
+  const int gi = min(i0 + 8 * c16, lim - 8);
+  return (uint32_t)(((int64_t)row * ld + gi) * 2);
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <bool KC>
 __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane) {
-  const int r = ib + (lane & 15);
-  const int c = 4 * s + (lane >> 4);
-  return *reinterpret_cast<const bf16x8*>(tile + kc_off(r, c));
+  if (KC) {
+    const int r = ib + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(tile + kc_off(r, c));
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int r0 = 32 * s + 8 * g + q;
+    const int c8 = (ib >> 2) + p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0, c8)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + ic_off(r0 + 4, c8)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
 }
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
 
 // ---------------------------------------------------------------------------
 // 4 waves, 128x128 per wave.  SCHED selects the interleave pattern.
-template <int SCHED>
+template <int SCHED, bool B_KC>
 __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                  bf16_t* __restrict__ C, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -100,13 +126,13 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     offA[u] = piece_off(K, m0, M, 8 * wave + u, lane);
-    offB[u] = piece_off(K, n0, N, 8 * wave + u, lane);
+    offB[u] = B_KC ? piece_off(K, n0, N, 8 * wave + u, lane) : piece_off_ic(N, n0, N, 8 * wave + u, lane);
   }
   const char* Ab = reinterpret_cast<const char*>(A);
   const char* Bb = reinterpret_cast<const char*>(B);
   auto stageA = [&](int kt, char* buf, int u) { glds16(Ab + (int64_t)kt * BK * 2, offA[u], buf + (8 * wave + u) * 1024); };
   auto stageB = [&](int kt, char* buf, int u) {
-    glds16(Bb + (int64_t)kt * BK * 2, offB[u], buf + kTile + (8 * wave + u) * 1024);
+    glds16(Bb + (B_KC ? (int64_t)kt * BK * 2 : (int64_t)kt * BK * N * 2), offB[u], buf + kTile + (8 * wave + u) * 1024);
   };
   f32x4 acc[8][8];
 #pragma unroll
@@ -128,8 +154,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
   bf16x8 fa[2][8], fb[2][8];  // [k-step parity][tile]
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    fa[0][i] = frag(smem, wm * 128 + 16 * i, 0, lane);
-    fb[0][i] = frag(smem + kTile, wn * 128 + 16 * i, 0, lane);
+    fa[0][i] = frag<true>(smem, wm * 128 + 16 * i, 0, lane);
+    fb[0][i] = frag<B_KC>(smem + kTile, wn * 128 + 16 * i, 0, lane);
   }
   for (int u = 0; u < nk; ++u) {
     char* cur = smem + (u & 1) * kBuf;
@@ -145,8 +171,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
           // one fragment read after every 4th MFMA
           if ((j & 3) == 3) {
             const int q = 2 * i + (j >> 2);  // 0..15
-            if (q < 8) fa[1][q] = frag(cur, wm * 128 + 16 * q, 1, lane);
-            else fb[1][q - 8] = frag(cur + kTile, wn * 128 + 16 * (q - 8), 1, lane);
+            if (q < 8) fa[1][q] = frag<true>(cur, wm * 128 + 16 * q, 1, lane);
+            else fb[1][q - 8] = frag<B_KC>(cur + kTile, wn * 128 + 16 * (q - 8), 1, lane);
           }
           SB();
         }
@@ -155,8 +181,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
     if (SCHED == 1) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        fa[1][q] = frag(cur, wm * 128 + 16 * q, 1, lane);
-        fb[1][q] = frag(cur + kTile, wn * 128 + 16 * q, 1, lane);
+        fa[1][q] = frag<true>(cur, wm * 128 + 16 * q, 1, lane);
+        fb[1][q] = frag<B_KC>(cur + kTile, wn * 128 + 16 * q, 1, lane);
       }
     }
     // all reads of `cur` retired and this wave's DMAs of tile u+1 landed, then
@@ -182,8 +208,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
           }
           if ((g & 3) == 3) {  // 16 reads (past the last tile: harmless reads of the other buffer)
             const int q = g >> 2;
-            if (q < 8) fa[0][q] = frag(nxt, wm * 128 + 16 * q, 0, lane);
-            else fb[0][q - 8] = frag(nxt + kTile, wn * 128 + 16 * (q - 8), 0, lane);
+            if (q < 8) fa[0][q] = frag<true>(nxt, wm * 128 + 16 * q, 0, lane);
+            else fb[0][q - 8] = frag<B_KC>(nxt + kTile, wn * 128 + 16 * (q - 8), 0, lane);
           }
           SB();
         }
@@ -197,8 +223,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
       if (more) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          fa[0][q] = frag(nxt, wm * 128 + 16 * q, 0, lane);
-          fb[0][q] = frag(nxt + kTile, wn * 128 + 16 * q, 0, lane);
+          fa[0][q] = frag<true>(nxt, wm * 128 + 16 * q, 0, lane);
+          fb[0][q] = frag<B_KC>(nxt + kTile, wn * 128 + 16 * q, 0, lane);
         }
       }
     }
@@ -243,9 +269,9 @@ static bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
-template <int SCHED>
+template <int SCHED, bool B_KC>
 static float run(const bf16_t* dA, const bf16_t* dB, bf16_t* dC, int M, int N, int K, int iters) {
-  auto kern = gemm4w<SCHED>;
+  auto kern = gemm4w<SCHED, B_KC>;
   CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBuf));
   dim3 grid((M / BM) * (N / BN)), block(256);
   for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(kern, grid, block, 2 * kBuf, 0, dA, dB, dC, M, N, K);
@@ -262,10 +288,10 @@ static float run(const bf16_t* dA, const bf16_t* dB, bf16_t* dC, int M, int N, i
   return ms * 1e3f / iters;
 }
 
-template <int SCHED>
+template <int SCHED, bool B_KC>
 static bool check(const std::vector<bf16_t>& hA, const std::vector<bf16_t>& hB, const bf16_t* dA, const bf16_t* dB,
                   bf16_t* dC, int M, int N, int K) {
-  run<SCHED>(dA, dB, dC, M, N, K, 1);
+  run<SCHED, B_KC>(dA, dB, dC, M, N, K, 1);
   CK(hipDeviceSynchronize());
   std::vector<bf16_t> hC((size_t)M * N);
   CK(hipMemcpy(hC.data(), dC, hC.size() * 2, hipMemcpyDeviceToHost));
@@ -275,7 +301,8 @@ static bool check(const std::vector<bf16_t>& hA, const std::vector<bf16_t>& hB, 
   for (int t = 0; t < 4000; ++t) {
     const int i = (t < 16) ? (t * 97) % M : rand() % M, j = (t < 16) ? (t * 131) % N : rand() % N;
     double ref = 0;
-    for (int k = 0; k < K; ++k) ref += (double)bf2f(hA[(size_t)i * K + k]) * bf2f(hB[(size_t)j * K + k]);
+    for (int k = 0; k < K; ++k)
+      ref += (double)bf2f(hA[(size_t)i * K + k]) * bf2f(B_KC ? hB[(size_t)j * K + k] : hB[(size_t)k * N + j]);
     const double got = bf2f(hC[(size_t)i * N + j]);
     const double err = fabs(got - ref) / (fabs(ref) + 1.0);
     if (err > worst) worst = err;
@@ -284,7 +311,8 @@ static bool check(const std::vector<bf16_t>& hA, const std::vector<bf16_t>& hB, 
       ++bad;
     }
   }
-  printf("check sched %d %dx%dx%d: %s (worst rel err %.2e)\n", SCHED, M, N, K, bad ? "FAIL" : "ok", worst);
+  printf("check sched %d B_%s %dx%dx%d: %s (worst rel err %.2e)\n", SCHED, B_KC ? "KC" : "IC", M, N, K,
+         bad ? "FAIL" : "ok", worst);
   return bad == 0;
 }
 
@@ -301,47 +329,44 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dC, (size_t)M * N * 2));
   CK(hipMemcpy(dA, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(dB, hB.data(), hB.size() * 2, hipMemcpyHostToDevice));
-  // correctness at K = 4096 (the operands are laid out with ld = K, so re-pack for smaller K)
+  // correctness at K = 4096: A [M][K]; B [N][K] (KC) or [K][N] (IC) -- the first N*K elements either way
   bool ok = true;
   {
     const int K = 4096;
     std::vector<bf16_t> a((size_t)M * K), b((size_t)N * K);
-    for (int i = 0; i < M; ++i) memcpy(&a[(size_t)i * K], &hA[(size_t)i * Kmax], K * 2);
-    for (int i = 0; i < N; ++i) memcpy(&b[(size_t)i * K], &hB[(size_t)i * Kmax], K * 2);
-    bf16_t *tA, *tB;
-    CK(hipMalloc(&tA, a.size() * 2));
-    CK(hipMalloc(&tB, b.size() * 2));
-    CK(hipMemcpy(tA, a.data(), a.size() * 2, hipMemcpyHostToDevice));
-    CK(hipMemcpy(tB, b.data(), b.size() * 2, hipMemcpyHostToDevice));
-    ok &= check<0>(a, b, tA, tB, dC, M, N, K);
-    ok &= check<1>(a, b, tA, tB, dC, M, N, K);
-    CK(hipFree(tA));
-    CK(hipFree(tB));
+    for (size_t i = 0; i < a.size(); ++i) a[i] = hA[i];
+    for (size_t i = 0; i < b.size(); ++i) b[i] = hB[i];
+    ok &= check<0, true>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<1, true>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<0, false>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<1, false>(a, b, dA, dB, dC, M, N, K);
   }
   if (!ok) return 1;
   const int rounds = (M / BM) * (N / BN) / 256;
   printf("%dx%d (%d tiles, %d rounds of 256): us per launch (TF/s)\n", M, N, (M / BM) * (N / BN), rounds);
-  printf("   K     sched0            sched1\n");
-  float t[2][4];
+  printf("   K   fwd sched0        fwd sched1        dgrad sched0      dgrad sched1\n");
+  float t[4][4];
   int ks[4] = {1024, 2048, 4096, 8192};
   for (int r = 0; r < 4; ++r) {
     const int K = ks[r];
-    // operands with ld = K: reuse the Kmax buffers' first M*K elements (values irrelevant for timing)
-    t[0][r] = run<0>(dA, dB, dC, M, N, K, 20);
-    t[1][r] = run<1>(dA, dB, dC, M, N, K, 20);
-    printf("%5d  %8.1f (%5.0f)  %8.1f (%5.0f)\n", K, t[0][r], 2.0 * M * N * K / t[0][r] / 1e6, t[1][r],
-           2.0 * M * N * K / t[1][r] / 1e6);
+    t[0][r] = run<0, true>(dA, dB, dC, M, N, K, 20);
+    t[1][r] = run<1, true>(dA, dB, dC, M, N, K, 20);
+    t[2][r] = run<0, false>(dA, dB, dC, M, N, K, 20);
+    t[3][r] = run<1, false>(dA, dB, dC, M, N, K, 20);
+    printf("%5d", K);
+    for (int v = 0; v < 4; ++v) printf("  %8.1f (%5.0f)", t[v][r], 2.0 * M * N * K / t[v][r] / 1e6);
+    printf("\n");
   }
-  for (int s = 0; s < 2; ++s) {
-    // least squares over K = 1024..8192
+  const char* names[4] = {"fwd sched0", "fwd sched1", "dgrad sched0", "dgrad sched1"};
+  for (int s = 0; s < 4; ++s) {
     double sx = 0, sy = 0, sxx = 0, sxy = 0;
     for (int r = 0; r < 4; ++r) {
       const double x = ks[r] / 1024.0, y = t[s][r];
       sx += x; sy += y; sxx += x * x; sxy += x * y;
     }
     const double slope = (4 * sxy - sx * sy) / (4 * sxx - sx * sx), icpt = (sy - slope * sx) / 4;
-    printf("sched%d fit: fixed %.1f us + %.2f us per 1k K  (main loop %.0f TF/s)\n", s, icpt, slope,
-           2.0 * M * N * 1024 / slope / 1e6);
+    printf("%-13s fit: fixed %.1f us + %.2f us per 1k K (%.2f per round)  main loop %.0f TF/s\n", names[s], icpt,
+           slope, slope / (rounds > 0 ? rounds : 1), 2.0 * M * N * 1024 / slope / 1e6);
   }
   return 0;
 }
