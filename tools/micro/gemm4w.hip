@@ -170,9 +170,10 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
         if (SCHED == 0) {
           // one fragment read after every 4th MFMA
           if ((j & 3) == 3) {
-            const int q = 2 * i + (j >> 2);  // 0..15
-            if (q < 8) fa[1][q] = frag<true>(cur, wm * 128 + 16 * q, 1, lane);
-            else fb[1][q - 8] = frag<B_KC>(cur + kTile, wn * 128 + 16 * (q - 8), 1, lane);
+            const int q = 2 * i + (j >> 2);  // 0..15: A0, B0-B7, A1-A7
+            const int ia = q == 0 ? 0 : q - 8;
+            if (q == 0 || q > 8) fa[1][ia] = frag<true>(cur, wm * 128 + 16 * ia, 1, lane);
+            else fb[1][q - 1] = frag<B_KC>(cur + kTile, wn * 128 + 16 * (q - 1), 1, lane);
           }
           SB();
         }
@@ -207,9 +208,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
             else stageB(kl2, cur, d - 8);
           }
           if ((g & 3) == 3) {  // 16 reads (past the last tile: harmless reads of the other buffer)
-            const int q = g >> 2;
-            if (q < 8) fa[0][q] = frag<true>(nxt, wm * 128 + 16 * q, 0, lane);
-            else fb[0][q - 8] = frag<B_KC>(nxt + kTile, wn * 128 + 16 * (q - 8), 0, lane);
+            const int q = g >> 2, ia = q == 0 ? 0 : q - 8;
+            if (q == 0 || q > 8) fa[0][ia] = frag<true>(nxt, wm * 128 + 16 * ia, 0, lane);
+            else fb[0][q - 1] = frag<B_KC>(nxt + kTile, wn * 128 + 16 * (q - 1), 0, lane);
           }
           SB();
         }
