@@ -80,3 +80,17 @@ def test_example_driver_runs_on_cpu(tmp_path):
     assert out.returncode == 0, out.stderr[-2000:]
     assert "Total parameters in model" in out.stdout
     assert out.stdout.count("| batch") == 3
+
+
+def test_gpu_telemetry_degrades_without_a_gpu():
+    """bench.py brackets its timed steps with GpuTelemetry; with no driver (or no
+    amdsmi) it must report itself unavailable instead of raising."""
+    from mipipe.utils.telemetry import GpuTelemetry
+
+    t = GpuTelemetry(0, period=0.01).start()
+    out = t.stop()
+    assert isinstance(out, dict) and "available" in out
+    if out["available"]:  # a GPU host: the fields the bench JSON documents
+        assert "gfxclk_mhz" in out and "samples" in out
+    else:
+        assert out.get("error")
