@@ -1388,9 +1388,10 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
       for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
         if ((j & 3) == 3) {
-          const int q = 2 * i + (j >> 2);
-          if (q < 8) fa[1][q] = frag<A_KC, 256>(cur, wm * 128 + 16 * q, 1, lane);
-          else fb[1][q - 8] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * (q - 8), 1, lane);
+          const int q = 2 * i + (j >> 2);  // read order A0, B0-B7, A1-A7: the order the MFMAs use them
+          const int ia = q == 0 ? 0 : q - 8;
+          if (q == 0 || q > 8) fa[1][ia] = frag<A_KC, 256>(cur, wm * 128 + 16 * ia, 1, lane);
+          else fb[1][q - 1] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * (q - 1), 1, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1412,9 +1413,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
         const int gi = NJ * i + j;
         if ((gi & 3) == 1) stage_piece(ks, cur, gi >> 2);
         if ((gi & 3) == 3) {
-          const int q = gi >> 2;
-          if (q < 8) fa[0][q] = frag<A_KC, 256>(nxt, wm * 128 + 16 * q, 0, lane);
-          else fb[0][q - 8] = frag<B_KC, W>(nxt + kTileBytes, wn * WN + 16 * (q - 8), 0, lane);
+          const int q = gi >> 2, ia = q == 0 ? 0 : q - 8;
+          if (q == 0 || q > 8) fa[0][ia] = frag<A_KC, 256>(nxt, wm * 128 + 16 * ia, 0, lane);
+          else fb[0][q - 1] = frag<B_KC, W>(nxt + kTileBytes, wn * WN + 16 * (q - 1), 0, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
       }

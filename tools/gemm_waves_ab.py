@@ -56,7 +56,7 @@ def main(T=int(sys.argv[1]) if len(sys.argv) > 1 else 8192):
     # numerics first (the 4-wave kernel on every layout it serves)
     ok = True
     k.gemm_set_width(256)  # small grids would otherwise take the 256x128 block (8-wave only)
-    for (M, N, K) in [(1000, 776, 1088), (1280, 520, 512)]:
+    for (M, N, K) in [(1088, 768, 1088), (1280, 576, 512)]:
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = torch.randn(N, K, device=dev).to(torch.bfloat16)
         dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
