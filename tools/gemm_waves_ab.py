@@ -62,7 +62,7 @@ def main(T=int(sys.argv[1]) if len(sys.argv) > 1 else 8192):
         dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
         b = torch.randn(N, device=dev).to(torch.bfloat16)
         k.gemm_set_waves(4)
-        y = k.linear_fwd(x, w, b, 1, 0.0, False)
+        y = k.linear_fwd(x, w, b, 1, 0.0, False)[0]
         dx = k.linear_dgrad(dy, w)
         mg = torch.zeros(N, K, device=dev)
         k.linear_wgrad(dy, x, mg)

@@ -319,6 +319,7 @@ static bool check(const std::vector<bf16_t>& hA, const std::vector<bf16_t>& hB, 
 
 int main(int argc, char** argv) {
   const int M = argc > 2 ? atoi(argv[1]) : 8192, N = argc > 2 ? atoi(argv[2]) : 4096;
+
   const int Kmax = 8192;
   std::vector<bf16_t> hA((size_t)M * Kmax), hB((size_t)N * Kmax);
   srand(1);
@@ -330,6 +331,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dC, (size_t)M * N * 2));
   CK(hipMemcpy(dA, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(dB, hB.data(), hB.size() * 2, hipMemcpyHostToDevice));
+  if (argc > 4) {  // gemm4w M N <variant 0-3> <K> [iters]: one arm only (PMC runs)
+    const int v = atoi(argv[3]), K = atoi(argv[4]), it = argc > 5 ? atoi(argv[5]) : 50;
+    const float t = v == 0 ? run<0, true>(dA, dB, dC, M, N, K, it) : v == 1 ? run<1, true>(dA, dB, dC, M, N, K, it)
+                  : v == 2 ? run<0, false>(dA, dB, dC, M, N, K, it) : run<1, false>(dA, dB, dC, M, N, K, it);
+    printf("variant %d %dx%dx%d: %.1f us (%.0f TF/s)\n", v, M, N, K, t, 2.0 * M * N * K / t / 1e6);
+    return 0;
+  }
   // correctness at K = 4096: A [M][K]; B [N][K] (KC) or [K][N] (IC) -- the first N*K elements either way
   bool ok = true;
   {
