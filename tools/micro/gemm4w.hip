@@ -107,6 +107,14 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, int ib, int s, int lane
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
 
+// Interleave pattern of the interleaved schedules (all but 1): k-step 0 issues
+// fragment read q after MFMA R0 q + O0; k-step 1 issues DMA d after MFMA D1 d + OD
+// and read q after MFMA R1 q + O1 (MFMAs numbered 0-63 per k-step).
+template <int S> struct Sch { static constexpr int R0 = 4, O0 = 3, R1 = 4, O1 = 3, D1 = 4, OD = 1; };
+template <> struct Sch<2> { static constexpr int R0 = 3, O0 = 0, R1 = 4, O1 = 3, D1 = 4, OD = 1; };
+template <> struct Sch<3> { static constexpr int R0 = 3, O0 = 0, R1 = 3, O1 = 1, D1 = 4, OD = 0; };
+template <> struct Sch<4> { static constexpr int R0 = 2, O0 = 0, R1 = 4, O1 = 2, D1 = 4, OD = 0; };
+
 // ---------------------------------------------------------------------------
 // 4 waves, 128x128 per wave.  SCHED selects the interleave pattern.
 template <int SCHED, bool B_KC>
@@ -167,10 +175,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-        if (SCHED == 0) {
-          // one fragment read after every 4th MFMA
-          if ((j & 3) == 3) {
-            const int q = 2 * i + (j >> 2);  // 0..15: A0, B0-B7, A1-A7
+        if (SCHED != 1) {
+          // fragment read q after MFMA R0 q + O0 (Sch<SCHED>)
+          const int g = 8 * i + j;
+          if (g % Sch<SCHED>::R0 == Sch<SCHED>::O0 && g / Sch<SCHED>::R0 < 16) {
+            const int q = g / Sch<SCHED>::R0;  // 0..15: A0, B0-B7, A1-A7
             const int ia = q == 0 ? 0 : q - 8;
             if (q == 0 || q > 8) fa[1][ia] = frag<true>(cur, wm * 128 + 16 * ia, 1, lane);
             else fb[1][q - 1] = frag<B_KC>(cur + kTile, wn * 128 + 16 * (q - 1), 1, lane);
@@ -200,15 +209,15 @@ __global__ void __launch_bounds__(256, 1) gemm4w(const bf16_t* __restrict__ A, c
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
-        if (SCHED == 0) {
+        if (SCHED != 1) {
           const int g = 8 * i + j;  // 0..63
-          if ((g & 3) == 1) {  // 16 DMAs (past the last tile: a harmless restage of the last one)
-            const int d = g >> 2;
+          if (g % Sch<SCHED>::D1 == Sch<SCHED>::OD && g / Sch<SCHED>::D1 < 16) {  // 16 DMAs (past the last tile: a harmless restage)
+            const int d = g / Sch<SCHED>::D1;
             if (d < 8) stageA(kl2, cur, d);
             else stageB(kl2, cur, d - 8);
           }
-          if ((g & 3) == 3) {  // 16 reads (past the last tile: harmless reads of the other buffer)
-            const int q = g >> 2, ia = q == 0 ? 0 : q - 8;
+          if (g % Sch<SCHED>::R1 == Sch<SCHED>::O1 && g / Sch<SCHED>::R1 < 16) {  // 16 reads (past the last tile: harmless)
+            const int q = g / Sch<SCHED>::R1, ia = q == 0 ? 0 : q - 8;
             if (q == 0 || q > 8) fa[0][ia] = frag<true>(nxt, wm * 128 + 16 * ia, 0, lane);
             else fb[0][q - 1] = frag<B_KC>(nxt + kTile, wn * 128 + 16 * (q - 1), 0, lane);
           }
@@ -317,6 +326,21 @@ static bool check(const std::vector<bf16_t>& hA, const std::vector<bf16_t>& hB, 
   return bad == 0;
 }
 
+// arm v: schedule {0, 2, 3, 4}[v % 4], B K-contiguous for v < 4 (forward layout) else I-contiguous (dgrad)
+static const int kSched[4] = {0, 2, 3, 4};
+static float run_arm(int v, const bf16_t* dA, const bf16_t* dB, bf16_t* dC, int M, int N, int K, int it) {
+  switch (v) {
+    case 0: return run<0, true>(dA, dB, dC, M, N, K, it);
+    case 1: return run<2, true>(dA, dB, dC, M, N, K, it);
+    case 2: return run<3, true>(dA, dB, dC, M, N, K, it);
+    case 3: return run<4, true>(dA, dB, dC, M, N, K, it);
+    case 4: return run<0, false>(dA, dB, dC, M, N, K, it);
+    case 5: return run<2, false>(dA, dB, dC, M, N, K, it);
+    case 6: return run<3, false>(dA, dB, dC, M, N, K, it);
+    default: return run<4, false>(dA, dB, dC, M, N, K, it);
+  }
+}
+
 int main(int argc, char** argv) {
   const int M = argc > 2 ? atoi(argv[1]) : 8192, N = argc > 2 ? atoi(argv[2]) : 4096;
 
@@ -333,8 +357,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dB, hB.data(), hB.size() * 2, hipMemcpyHostToDevice));
   if (argc > 4) {  // gemm4w M N <variant 0-3> <K> [iters]: one arm only (PMC runs)
     const int v = atoi(argv[3]), K = atoi(argv[4]), it = argc > 5 ? atoi(argv[5]) : 50;
-    const float t = v == 0 ? run<0, true>(dA, dB, dC, M, N, K, it) : v == 1 ? run<1, true>(dA, dB, dC, M, N, K, it)
-                  : v == 2 ? run<0, false>(dA, dB, dC, M, N, K, it) : run<1, false>(dA, dB, dC, M, N, K, it);
+    const float t = run_arm(v, dA, dB, dC, M, N, K, it);
     printf("variant %d %dx%dx%d: %.1f us (%.0f TF/s)\n", v, M, N, K, t, 2.0 * M * N * K / t / 1e6);
     return 0;
   }
@@ -346,36 +369,39 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < a.size(); ++i) a[i] = hA[i];
     for (size_t i = 0; i < b.size(); ++i) b[i] = hB[i];
     ok &= check<0, true>(a, b, dA, dB, dC, M, N, K);
-    ok &= check<1, true>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<2, true>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<3, true>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<4, true>(a, b, dA, dB, dC, M, N, K);
     ok &= check<0, false>(a, b, dA, dB, dC, M, N, K);
-    ok &= check<1, false>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<2, false>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<3, false>(a, b, dA, dB, dC, M, N, K);
+    ok &= check<4, false>(a, b, dA, dB, dC, M, N, K);
   }
   if (!ok) return 1;
   const int rounds = (M / BM) * (N / BN) / 256;
   printf("%dx%d (%d tiles, %d rounds of 256): us per launch (TF/s)\n", M, N, (M / BM) * (N / BN), rounds);
-  printf("   K   fwd sched0        fwd sched1        dgrad sched0      dgrad sched1\n");
-  float t[4][4];
+  printf("   K");
+  for (int v = 0; v < 8; ++v) printf("   %s s%d", v < 4 ? "fwd" : "dgr", kSched[v % 4]);
+  printf("   (us per launch)\n");
+  float t[8][4];
   int ks[4] = {1024, 2048, 4096, 8192};
   for (int r = 0; r < 4; ++r) {
     const int K = ks[r];
-    t[0][r] = run<0, true>(dA, dB, dC, M, N, K, 20);
-    t[1][r] = run<1, true>(dA, dB, dC, M, N, K, 20);
-    t[2][r] = run<0, false>(dA, dB, dC, M, N, K, 20);
-    t[3][r] = run<1, false>(dA, dB, dC, M, N, K, 20);
+    for (int v = 0; v < 8; ++v) t[v][r] = run_arm(v, dA, dB, dC, M, N, K, 20);
     printf("%5d", K);
-    for (int v = 0; v < 4; ++v) printf("  %8.1f (%5.0f)", t[v][r], 2.0 * M * N * K / t[v][r] / 1e6);
+    for (int v = 0; v < 8; ++v) printf("  %8.1f", t[v][r]);
     printf("\n");
   }
-  const char* names[4] = {"fwd sched0", "fwd sched1", "dgrad sched0", "dgrad sched1"};
-  for (int s = 0; s < 4; ++s) {
+  for (int v = 0; v < 8; ++v) {
     double sx = 0, sy = 0, sxx = 0, sxy = 0;
     for (int r = 0; r < 4; ++r) {
-      const double x = ks[r] / 1024.0, y = t[s][r];
+      const double x = ks[r] / 1024.0, y = t[v][r];
       sx += x; sy += y; sxx += x * x; sxy += x * y;
     }
     const double slope = (4 * sxy - sx * sy) / (4 * sxx - sx * sx), icpt = (sy - slope * sx) / 4;
-    printf("%-13s fit: fixed %.1f us + %.2f us per 1k K (%.2f per round)  main loop %.0f TF/s\n", names[s], icpt,
-           slope, slope / (rounds > 0 ? rounds : 1), 2.0 * M * N * 1024 / slope / 1e6);
+    printf("%s sched%d fit: fixed %.1f us + %.2f us per 1k K (%.2f per round)  main loop %.0f TF/s\n",
+           v < 4 ? "fwd  " : "dgrad", kSched[v % 4], icpt, slope, slope / (rounds > 0 ? rounds : 1),
+           2.0 * M * N * 1024 / slope / 1e6);
   }
   return 0;
 }
