@@ -1346,26 +1346,47 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
   stage_offsets<A_KC, 256>(g.lda, m0, g.M, wave + 4, lane, offA1);
   stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave, lane, offB0);
   stage_offsets<B_KC, W>(g.ldb, n0, g.N, wave + 4, lane, offB1);
-  // piece d (0-15) of K-tile kt into buffer buf: A shares (d 0-7), then B
-  auto stage_piece = [&](int kt, char* buf, int d) {
-    int kl;
+  // Operand bases of K-tile kt (scalar).  Every GemmArgs field the loop needs
+  // is read into a local first: the DMA asm clobbers "memory", and a field
+  // read after it is re-loaded from the kernel arguments -- an s_load whose
+  // s_waitcnt lgkmcnt(0) also drains every LDS read in flight (that cost the
+  // first version of this kernel 20 %).  The bases of the tile staged in k-step
+  // 1 are computed at the top of the iteration, before any DMA of it.
+  const int64_t lda = g.lda, ldb = g.ldb;
+  const int seg_k = g.seg_k;
+  const char* const gA = reinterpret_cast<const char*>(g.A);
+  const char* const gB = reinterpret_cast<const char*>(g.B);
+  auto tile_bases = [&](int kt, const char*& bA, const char*& bB) {
+    int kl = (kt0 + kt) * BK;
+    const char *a = gA, *b = gB;
+    if (seg_k > 0) {  // segmented operands: the segment's pointers (the only scalar loads in the loop)
+      const int sg = kl / seg_k;
+      kl -= sg * seg_k;
+      a = reinterpret_cast<const char*>(g.a_seg[sg]);
+      b = reinterpret_cast<const char*>(g.b_seg[sg]);
+    }
+    bA = a + (A_KC ? (int64_t)kl * 2 : (int64_t)kl * lda * 2);
+    bB = b + (B_KC ? (int64_t)kl * 2 : (int64_t)kl * ldb * 2);
+  };
+  // piece d (0-15) of a K-tile into buffer buf: A shares (d 0-7), then B
+  auto stage_piece = [&](const char* bA, const char* bB, char* buf, int d) {
     if (d < 8) {
-      const char* b = reinterpret_cast<const char*>(seg_base(g, true, (kt0 + kt) * BK, kl));
-      b += A_KC ? (int64_t)kl * 2 : (int64_t)kl * g.lda * 2;
       const int sh = d < 4 ? wave : wave + 4;
-      glds16_saddr(b, d < 4 ? offA0[d & 3] : offA1[d & 3], buf + (sh * 4 + (d & 3)) * 1024);
+      glds16_saddr(bA, d < 4 ? offA0[d & 3] : offA1[d & 3], buf + (sh * 4 + (d & 3)) * 1024);
     } else {
-      const char* b = reinterpret_cast<const char*>(seg_base(g, false, (kt0 + kt) * BK, kl));
-      b += B_KC ? (int64_t)kl * 2 : (int64_t)kl * g.ldb * 2;
       const int sh = d < 12 ? wave : wave + 4;
-      glds16_saddr(b, d < 12 ? offB0[d & 3] : offB1[d & 3], buf + kTileBytes + (sh * 4 + (d & 3)) * 1024);
+      glds16_saddr(bB, d < 12 ? offB0[d & 3] : offB1[d & 3], buf + kTileBytes + (sh * 4 + (d & 3)) * 1024);
     }
   };
+  const char *bA, *bB;
+  tile_bases(0, bA, bB);
+  const char *bA1 = bA, *bB1 = bB;
+  if (nk > 1) tile_bases(1, bA1, bB1);
 #pragma unroll
-  for (int d = 0; d < 16; ++d) stage_piece(0, smem, d);
+  for (int d = 0; d < 16; ++d) stage_piece(bA, bB, smem, d);
   if (nk > 1) {
 #pragma unroll
-    for (int d = 0; d < 16; ++d) stage_piece(1, smem + kBuf, d);
+    for (int d = 0; d < 16; ++d) stage_piece(bA1, bB1, smem + kBuf, d);
     vmcnt_keep<16>();
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1387,8 +1408,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-        if ((j & 3) == 3) {
-          const int q = 2 * i + (j >> 2);  // read order A0, B0-B7, A1-A7: the order the MFMAs use them
+        // read q after MFMA 3 q: all 16 issued by MFMA 45, so they have landed by
+        // the k-step's end (the wait before the barrier, and the compiler's wait
+        // at the top of the next k-step, find them retired)
+        const int gi = NJ * i + j;
+        if (gi % 3 == 0 && gi / 3 < 16) {
+          const int q = gi / 3;  // read order A0, B0-B7, A1-A7: the order the MFMAs use them
           const int ia = q == 0 ? 0 : q - 8;
           if (q == 0 || q > 8) fa[1][ia] = frag<A_KC, 256>(cur, wm * 128 + 16 * ia, 1, lane);
           else fb[1][q - 1] = frag<B_KC, W>(cur + kTileBytes, wn * WN + 16 * (q - 1), 1, lane);
@@ -1397,13 +1422,19 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
       }
     rowsum_step(cur);
     colsum_step(cur + kTileBytes);
+    // Bases of tile u+2 (past the end: the last tile again), whose scalar
+    // loads (segmented operands) the wait below drains with the LDS reads: no
+    // scalar load is ever pending where the compiler counts LDS reads, so its
+    // own waits stay counted (lgkmcnt(N)) rather than lgkmcnt(0).
+    __builtin_amdgcn_sched_barrier(0);
+    const char *sA, *sB;
+    tile_bases(u + 2 < nk ? u + 2 : nk - 1, sA, sB);
     // this wave's DMAs of tile u+1 have landed and its reads of cur retired;
     // after the barrier cur may be restaged and nxt read
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const int ks = u + 2 < nk ? u + 2 : nk - 1;
     // ---- k-step 1: MFMAs on (u, 1), reads of (u+1, 0), DMA of tile u+2 ----
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1411,9 +1442,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
       for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
         const int gi = NJ * i + j;
-        if ((gi & 3) == 1) stage_piece(ks, cur, gi >> 2);
-        if ((gi & 3) == 3) {
-          const int q = gi >> 2, ia = q == 0 ? 0 : q - 8;
+        if ((gi & 3) == 1) stage_piece(sA, sB, cur, gi >> 2);
+        if (gi % 3 == 0 && gi / 3 < 16) {
+          const int q = gi / 3, ia = q == 0 ? 0 : q - 8;
           if (q == 0 || q > 8) fa[0][ia] = frag<A_KC, 256>(nxt, wm * 128 + 16 * ia, 0, lane);
           else fb[0][q - 1] = frag<B_KC, W>(nxt + kTileBytes, wn * WN + 16 * (q - 1), 0, lane);
         }
