@@ -42,6 +42,7 @@ compute.  Per-stage busy time is measured with HIP events (bubble %).
 from __future__ import annotations
 
 import os
+import warnings
 import time
 from contextlib import contextmanager
 from dataclasses import dataclass, field
@@ -230,7 +231,10 @@ class PipelineEngine:
         elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
             dev = device or next(mods[0].parameters()).device
-            if transport == "ipc":
+            self.transport_note = None
+            if transport == "auto":
+                transport = self._auto_transport(ranks, dev, transport_options, watchdog)
+            elif transport == "ipc":
                 from .ipc import IpcChannels
 
                 opts = dict(transport_options or {})
@@ -246,7 +250,8 @@ class PipelineEngine:
                 with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
                     self.chan.warmup(dev)
             else:
-                raise ValueError(f"transport must be 'rccl' or 'ipc', got {transport!r}")
+                raise ValueError(f"transport must be 'auto', 'rccl' or 'ipc', got {transport!r}")
+            self.transport = transport
         else:
             self.chan = None
         if self.chan is not None:
@@ -266,6 +271,53 @@ class PipelineEngine:
         if self.watchdog is not None and self.watchdog.describe is None:
             self.watchdog.describe = self.describe
         self._setup_skips(group, skip_shapes, skip_routes)
+
+    def _auto_transport(self, ranks, dev, transport_options, watchdog) -> str:
+        """``transport="auto"``: stage boundaries that take no CU from compute.
+
+        An RCCL receive is a kernel that spins on its CUs until the data lands
+        (footprint of torch's ``rcclGenericKernel``: 256 threads, 19.7 KiB LDS,
+        ~270 registers -- it can never share a CU with a 256x256 GEMM block),
+        and the engine posts its receives ahead, so one stays resident through
+        most of a phase.  ``profiles/cu_hold_r5.txt`` measures what k such
+        blocks cost the PP=1 step.  The IPC links move data with the DMA engines
+        (the link's copy stream, ``sdma``) and order it with command-processor
+        stream waits: no CU at all -- the reference's own design (copies on
+        dedicated copy streams, event waits: /root/reference/README.md:193-237,
+        332-369).  Ranks sharing one GPU (rehearsals) copy on the producer's
+        stream (``inline``).  The links are self-tested first
+        (:meth:`IpcChannels.self_test`); if any rank fails, every rank falls
+        back to RCCL and :attr:`transport_note` says why.  CPU: RCCL-style
+        channels over gloo.  Collective."""
+        if dev.type != "cuda":
+            self.chan = Channels(ranks, wrap=self.virtual > 1)
+            self.chan.warmup(dev)
+            return "rccl"
+        from .ipc import IpcChannels, ranks_share_a_device, verified_ipc
+
+        shared = ranks_share_a_device(dev)
+        opts = dict(transport_options or {})
+        opts.setdefault("slots", self.chunks * self.virtual)
+        opts.setdefault("engine", "inline" if shared else "sdma")
+
+        def make_rccl():
+            if shared:
+                raise RuntimeError("IPC links failed their self-test and RCCL refuses two ranks on one GPU: "
+                                   + str(self.transport_note))
+            ch = Channels(ranks, wrap=self.virtual > 1)
+            with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
+                ch.warmup(dev)
+            return ch
+
+        with (watchdog.watch("IPC link self-test") if watchdog is not None else _null()):
+            self.chan, why = verified_ipc(
+                lambda: IpcChannels(ranks, wrap=self.virtual > 1, device=dev, recv_bytes=self.recv_bytes(), **opts),
+                make_rccl, dev)
+        if why is not None:
+            self.transport_note = f"IPC self-test failed, fell back to RCCL: {why}"
+            warnings.warn(self.transport_note)
+            return "rccl"
+        return f"ipc-{opts['engine']}"
 
     def close(self) -> None:
         """Releases the transport (IPC links: senders unmap, then receivers

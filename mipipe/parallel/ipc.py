@@ -39,6 +39,7 @@ rank's incoming-message size and shares a job-unique name prefix).
 from __future__ import annotations
 
 import os
+import time
 import uuid
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -49,7 +50,7 @@ from torch import Tensor
 from .. import _native_loader
 from ..stream import record_stream
 
-__all__ = ["IpcChannels", "ENGINES"]
+__all__ = ["IpcChannels", "ENGINES", "ranks_share_a_device", "verified_ipc"]
 
 # sdma / blit: the sender's copy on the link's own copy stream (overlaps the
 # producer's next kernels; two cross-stream dependencies per message);
@@ -203,6 +204,67 @@ class IpcChannels:
             if not link.is_sender:
                 link.unlink()  # everyone is attached: no name left behind in /dev/shm
 
+    # ------------------------------------------------------------------ self-test
+    def self_test(self, rounds: int = 2, timeout: float = 30.0) -> Optional[str]:
+        """Exercises every link of this rank exactly as the engine will: whole-slot
+        messages through the sender's engine into the peer's ring, the GPU-side
+        flag wait, a kernel reading the slot in place, the release -- and checks
+        every word (a pattern unique to link, direction and message).
+
+        Returns ``None`` on success or the reason it failed.  Bounded: the GPU
+        work runs on a side stream polled for ``timeout`` seconds; on a timeout
+        the links are aborted (this rank's flags saturated), so nothing stays
+        blocked.  Every rank of the pipeline must call it (each receives what
+        its neighbours send).  A cross-GPU link that never ran on hardware gets
+        checked before it carries a step (the cross-GPU path had
+        only ever been exercised with the ranks sharing one GPU).
+        """
+        if self.rank < 0 or self.world < 2:
+            return None
+        dev = self.device
+        if dev.type != "cuda":
+            return None
+        side = torch.cuda.Stream(dev)
+        ok = torch.ones((), dtype=torch.int32, device=dev)
+
+        def pattern(n: int, kind: str, src: int, dst: int, seq: int, device) -> Tensor:
+            # the same on both sides of a link (no per-process hash seeds)
+            base = (((1 if kind == "act" else 2) * 131 + src) * 131 + dst) * 65536 + seq * 7919
+            return (torch.arange(n, dtype=torch.int64, device=device) * 3 + base).remainder(2**31).to(torch.int32)
+
+        me = self.ranks[self.rank]
+        n = self.world
+        r = self.rank
+        prev_g, next_g = self.ranks[(r - 1) % n], self.ranks[(r + 1) % n]
+        t0 = time.perf_counter()
+        with torch.cuda.stream(side):
+            for rd in range(rounds):
+                for kind, link, dst in (("act", self._act_out, next_g), ("grad", self._grad_out, prev_g)):
+                    if link is None:
+                        continue
+                    peer_slot = int(link.slot_bytes) // 4
+                    msg = pattern(peer_slot, kind, me, dst, rd, dev)
+                    self._send(link, msg)
+                for kind, link, src in (("act", self._act_in, prev_g), ("grad", self._grad_in, next_g)):
+                    if link is None:
+                        continue
+                    words = int(link.slot_bytes) // 4
+                    t, work = self._recv_view(link, (words,), torch.int32)
+                    work.wait()
+                    ok &= (t == pattern(words, kind, src, me, rd, dev)).all().to(torch.int32)
+            self.end_step()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        while not ev.query():
+            if time.perf_counter() - t0 > timeout:
+                self.abort()
+                return f"self-test timed out after {timeout:.0f} s ({'; '.join(self.describe())})"
+            time.sleep(0.001)
+        if int(ok.item()) != 1:
+            return "self-test read wrong data through a link (" + "; ".join(self.describe()) + ")"
+        torch.cuda.current_stream(dev).wait_stream(side)
+        return None
+
     # ------------------------------------------------------------------ API
     def warmup(self, device: torch.device) -> None:
         """Nothing to do: the links are connected at construction."""
@@ -331,3 +393,31 @@ class IpcChannels:
         self._links = []
         self._act_in = self._grad_in = None
 
+
+
+def ranks_share_a_device(device: torch.device) -> bool:
+    """True if two ranks of the default process group run on one GPU (the
+    one-GPU rehearsals).  Collective."""
+    me = str(torch.cuda.get_device_properties(device).uuid) if device.type == "cuda" else f"cpu-{os.getpid()}"
+    ids: List[Optional[str]] = [None] * dist.get_world_size()
+    dist.all_gather_object(ids, me)
+    return len(set(ids)) < len(ids)
+
+
+def verified_ipc(make_ipc, make_fallback, device: torch.device):
+    """Builds IPC channels (``make_ipc()``), runs :meth:`IpcChannels.self_test`
+    on every rank and agrees over the default process group: all ranks keep
+    the IPC channels, or all switch to ``make_fallback()`` (RCCL).  Returns
+    ``(channels, reason)`` -- ``reason`` is ``None`` when IPC passed, else what
+    failed on which rank (for the bench JSON).  Collective."""
+    chan = make_ipc()
+    reason = chan.self_test()
+    flag = torch.tensor([0 if reason else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return chan, None
+    reasons: List[Optional[str]] = [None] * dist.get_world_size()
+    dist.all_gather_object(reasons, reason)
+    chan.abort()  # not closed: a link that failed may never drain; process teardown unmaps it
+    why = "; ".join(f"rank {i}: {r}" for i, r in enumerate(reasons) if r)
+    return make_fallback(), why
