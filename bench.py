@@ -92,10 +92,13 @@ def parse():
     ap.add_argument("--dp", type=int, default=1,
                     help="data-parallel replicas of the pipeline (world = PP x DP; gradients averaged by bucketed "
                          "RCCL all-reduces overlapped with the deferred weight gradients). Default 1: PP = world")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
-                    help="stage-boundary transport of the engine: rccl = send/recv of the process group; ipc = "
-                         "device-memory IPC links (DMA copies into the receiver's slots, no RCCL kernels; "
-                         "mipipe.parallel.ipc)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="stage-boundary transport of the engine: auto (default) = self-tested device-memory IPC "
+                         "links (SDMA copies on the links' copy streams into the receiver's slots, command-processor "
+                         "stream waits: no CU taken from compute; profiles/cu_hold_r5.txt), every rank falling back "
+                         "to RCCL together if a link fails its self-test; rccl = send/recv of the process group "
+                         "(each receive a resident kernel on CUs); ipc = the IPC links without the self-test "
+                         "(mipipe.parallel.ipc)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="every rank on cuda:0 (gloo for the small collectives, --transport ipc for the stage "
                          "boundaries): a one-GPU rehearsal of the multi-rank step for timelines "
@@ -218,7 +221,8 @@ def main() -> int:
             item = torch.empty((), dtype=dtype).element_size()
             ipc_opts = {"device": device, "slots": m * virtual,
                         "recv_bytes": max(torch.Size(s_).numel() for s_ in act_shapes) * item}
-        groups = make_pp_dp_groups(pp, dp, wrap=virtual > 1, transport=args.transport, ipc_options=ipc_opts)
+        groups = make_pp_dp_groups(pp, dp, wrap=virtual > 1, transport="ipc" if args.transport == "ipc" else "rccl",
+                                   ipc_options=ipc_opts)
         dpg = DataParallelGrads(opt, groups.dp_group)
 
     def loss_fn(y, t):
@@ -330,6 +334,8 @@ def main() -> int:
         loss_val = float(lt.item())
 
     comm = _comm_report(engine, device, world, local, on_gpu)
+    # what the stage boundaries actually ran on ('auto' resolves in the engine; one rank: none)
+    transport_used = getattr(engine, "transport", None) or "none (one stage)"
     teles = [tele]
     if world > 1:
         teles = [None] * world
@@ -373,9 +379,11 @@ def main() -> int:
                 "skips": args.skips if not skip_pairs else f"{args.skips}: {len(skip_pairs)} long residuals, "
                                                            f"{len(engine.skip_routes)} cross-stage",
                 "parallelism": f"pp{pp}" + (f"dp{dp}" if dp > 1 else ""),
-                "impl": ("engine (one process per GPU, RCCL send/recv)" if args.transport == "rccl" else
-                         "engine (one process per GPU, device-memory IPC links: DMA into the receiver's slots)"),
-                "transport": args.transport,
+                "impl": ("engine (one process per GPU, RCCL send/recv)" if transport_used == "rccl" else
+                         "engine (one process per GPU, device-memory IPC links: DMA into the receiver's slots)"
+                         if transport_used.startswith("ipc") else "engine (one process per GPU)"),
+                "transport": transport_used,
+                "transport_note": getattr(engine, "transport_note", None),
                 "shared_gpu": bool(args.shared_gpu),
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),

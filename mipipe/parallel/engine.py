@@ -223,15 +223,17 @@ class PipelineEngine:
         # step run this way with a scheduled one
         self.sync_debug = (os.environ.get("MIPIPE_SYNC_DEBUG") == "1") if sync_debug is None else bool(sync_debug)
         self._action = "construction"
+        self.transport: Optional[str] = None  # what the stage boundaries run on (None: one rank)
+        self.transport_note: Optional[str] = None
         if isinstance(group, Channels) or hasattr(group, "send_act"):  # ready channels (RCCL or IPC)
             self.chan: Optional[Channels] = group
+            self.transport = "ipc" if type(group).__name__ == "IpcChannels" else "rccl"
             if group.world > 1:
                 with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
                     group.warmup(device or next(mods[0].parameters()).device)
         elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
             dev = device or next(mods[0].parameters()).device
-            self.transport_note = None
             if transport == "auto":
                 transport = self._auto_transport(ranks, dev, transport_options, watchdog)
             elif transport == "ipc":
