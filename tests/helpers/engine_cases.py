@@ -33,7 +33,7 @@ SKIP_PAIRS = [(0, 3), (1, 2)]
 # Modes: "cpu" (gloo, fp32), "nccl" (RCCL, one rank per GPU), "ipc_cpu" (gloo for
 # collectives, activations over shared-memory IPC links), "ipc_gpu" (every rank
 # on cuda:0, activations over device-memory IPC links -- mipipe.parallel.ipc).
-GPU_MODES = ("nccl", "ipc_gpu")
+GPU_MODES = ("nccl", "ipc_gpu", "auto_gpu", "auto_sdma_gpu")
 
 
 def case_cfg(mode):
@@ -72,7 +72,7 @@ def _port():
 def _device(mode, rank):
     if mode == "nccl":
         return torch.device("cuda", rank)
-    return torch.device("cuda", 0) if mode == "ipc_gpu" else torch.device("cpu")
+    return torch.device("cuda", 0) if mode in ("ipc_gpu", "auto_gpu", "auto_sdma_gpu") else torch.device("cpu")
 
 
 def _grads(params, names):
@@ -81,6 +81,15 @@ def _grads(params, names):
         g = p.main_grad if hasattr(p, "main_grad") else p.grad
         out[names[id(p)]] = g.float().cpu().numpy().copy()
     return out
+
+
+def _transport_options(mode, steps, virtual):
+    opts = {}
+    if (mode.startswith("ipc") or mode.startswith("auto")) and steps > 1 and virtual == 1:
+        opts["slots"] = 2
+    if mode == "auto_sdma_gpu":  # the cross-GPU engine (copies on the links' copy streams), on one GPU
+        opts["engine"] = "sdma"
+    return opts or None
 
 
 def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropout=0.0, seed=0, steps=1):
@@ -118,13 +127,16 @@ def worker(rank, world, port, mode, checkpoint, virtual, split, skips, q, dropou
                              act_dtype=dtype, loss_fn=_loss_fn(cfg) if rank == world - 1 else None,
                              device=dev, watchdog=120.0,
                              skip_shapes={"skip": ((mb, cfg.seq_len, cfg.d_model), dtype)},
-                             transport="ipc" if mode.startswith("ipc") else "rccl",
+                             transport=("ipc" if mode.startswith("ipc") else
+                                        "auto" if mode.startswith("auto") else "rccl"),
                              # several steps of a plain chain: a 2-slot ring is reused many times over
                              # (a looping placement keeps one slot per message of the step)
-                             transport_options={"slots": 2} if (mode.startswith("ipc") and steps > 1
-                                                                and virtual == 1) else None)
-        if mode.startswith("ipc"):
+                             transport_options=_transport_options(mode, steps, virtual))
+        if mode.startswith("ipc") or mode.startswith("auto"):
             assert type(eng.chan).__name__ == "IpcChannels"
+        if mode.startswith("auto"):  # the self-test passed: no fallback
+            assert eng.transport == ("ipc-sdma" if mode == "auto_sdma_gpu" else "ipc-inline"), eng.transport
+            assert eng.transport_note is None
         inputs, targets = _data(cfg, m, mb)
         for _ in range(steps):  # no optimizer step: every step computes the same gradients
             torch.manual_seed(1000 + seed * 97 + rank)  # dropout streams: per rank, same in every mode

@@ -317,3 +317,21 @@ def test_engine_ipc_links_slot_reuse_over_steps(world, virtual):
     single-rank engine."""
     run_engine_case("ipc_gpu", world, "except_last", virtual, virtual > 1, False, steps=3)
 
+
+
+# ------------------------------------------------------------------ transport 'auto' (the bench's default at PP > 1)
+@pytest.mark.parametrize("world,virtual", [(2, 1), (4, 2)])
+def test_engine_auto_transport_self_tested_ipc(world, virtual):
+    """transport='auto': the IPC links pass their self-test (every word of a
+    whole-slot message per link and direction checked) and carry the step;
+    ranks sharing one GPU copy on the producer's stream ('ipc-inline')."""
+    run_engine_case("auto_gpu", world, "except_last", virtual, virtual > 1, False)
+
+
+@pytest.mark.parametrize("world,virtual", [(2, 1), (4, 2)])
+def test_engine_auto_transport_sdma_engine(world, virtual):
+    """The cross-GPU engine of transport='auto' -- copies on each link's own copy
+    stream (SDMA), ordered after the producer by an event and before the
+    consumer by the flag wait -- self-tested and then carrying two steps, on
+    ranks sharing one GPU (the only way to run it on a one-GPU box)."""
+    run_engine_case("auto_sdma_gpu", world, "except_last", virtual, virtual > 1, False, steps=2)
