@@ -173,6 +173,19 @@ def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
         if layout != opt_meta["layout"]:
             raise ValueError(f"{path}: the optimizer's parameter layout differs from the saved one "
                              f"(a different partition or model)")
+        for gi, g in enumerate(optimizer.groups):  # the flat buffers: present and of the group's size
+            for part in ("master", "exp_avg", "exp_avg_sq"):
+                key = f"flat.{gi}.{part}"
+                if key not in tensors:
+                    raise KeyError(f"{path}: no {key} (a truncated or foreign file)")
+                if tuple(tensors[key].shape) != tuple(g.master.shape):
+                    raise ValueError(f"{path}: {key} is {tuple(tensors[key].shape)}, the optimizer's is "
+                                     f"{tuple(g.master.shape)}")
+    elif isinstance(optimizer, torch.optim.Optimizer):
+        owned = {id(v) for v in params.values()}
+        stray = sum(1 for grp in optimizer.param_groups for q in grp["params"] if id(q) not in owned)
+        if stray:
+            raise ValueError(f"{path}: {stray} optimizer parameter(s) are not among the model's parameters")
     for n, p in params.items():
         key = f"param.{n}"
         if key not in tensors:

@@ -154,3 +154,29 @@ def test_refused_load_leaves_state_untouched(tmp_path, monkeypatch):
         load_training_state(path, other.named_parameters(), None)
     assert all(torch.equal(a, b) for a, b in zip(lin.parameters(), other.parameters()))
     assert not restored
+
+
+def test_truncated_optimizer_state_leaves_the_model_untouched(tmp_path):
+    """A file whose FlatAdam buffers are missing is refused BEFORE any parameter
+    is overwritten (the parameters used to be copied first)."""
+    from safetensors.torch import load_file, save_file
+
+    pipe = _pipe(0)
+    opt = FlatAdam(pipe.parameters(), lr=1e-2)
+    path = str(tmp_path / "ck.safetensors")
+    save_training_state(path, pipe.named_parameters(), opt)
+    t = load_file(path)
+    from safetensors import safe_open
+
+    with safe_open(path, "pt") as f:
+        meta = f.metadata()
+    del t["flat.0.exp_avg"]
+    cut = str(tmp_path / "cut.safetensors")
+    save_file(t, cut, metadata=meta)
+    other = _pipe(1)
+    before = [p.detach().clone() for p in other.parameters()]
+    opt2 = FlatAdam(other.parameters(), lr=1e-2)
+    with pytest.raises(KeyError, match="flat.0.exp_avg"):
+        load_training_state(cut, other.named_parameters(), opt2)
+    for a, b in zip(before, other.parameters()):
+        assert torch.equal(a, b)
