@@ -450,7 +450,10 @@ __device__ __forceinline__ void epi_rows(const EpiParams ep, f32x4 (&acc)[8][NJ]
 // ends with a barrier (so it can run twice: aux, then the output).
 // NJ: 16-wide accumulator tiles per wave (W / 64 for the 8-wave kernel, whose
 // wave tile is 128 x W/4; 8 for the 4-wave kernel's 128 x 128), kT: threads.
-template <int EPI, int W, int NJ = W / 64, int kT = 512>
+// ROWSPLIT (the 4-wave kernel): pass p stages accumulator rows i = 4p..4p+3 of
+// EVERY wave (all waves share the LDS writes) instead of all rows of the waves
+// with wm == p; image row R is then tile row 128 (R >> 6) + 64 p + (R & 63).
+template <int EPI, int W, int NJ = W / 64, int kT = 512, bool ROWSPLIT = false>
 __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][NJ], int wm, int wn, int lane,
                                              int tid, int m0, int n0, int M, int N, int64_t ldc, void* out,
                                              const bf16_t* res, int64_t ldr = 0, const bf16_t* dact_in = nullptr,
@@ -461,7 +464,15 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
   float* stg = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) {
+    if (ROWSPLIT) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(64 * wm + 16 * ii + 4 * quad + r) * kStride + wn * WN + 16 * j + col_in] = acc[4 * pass + ii][j][r];
+    } else if (wm == pass) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -472,6 +483,8 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
     }
     __syncthreads();
     const int rbase = m0 + pass * 128;
+    // tile row of image row R (R's 4-row quads never straddle a 64-row block)
+    auto grow = [&](int R) { return ROWSPLIT ? m0 + ((R >> 6) << 7) + 64 * pass + (R & 63) : rbase + R; };
     if (EPI == kEpiStoreBf16) {
       bf16_t* C = reinterpret_cast<bf16_t*>(out);
       constexpr int CPR = W / 8;  // 128 rows x W/8 chunks of 8 columns
@@ -479,22 +492,22 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
       for (int u = 0; u < 128 * CPR / kT; ++u) {
         const int idx = tid + u * kT;
         const int row = idx / CPR, c8 = idx % CPR;
-        if (rbase + row >= M || n0 + 8 * c8 >= N) continue;
+        if (grow(row) >= M || n0 + 8 * c8 >= N) continue;
         const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8);
         const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + row * kStride + 8 * c8 + 4);
-        const int64_t at = (int64_t)(rbase + row) * ldc + n0 + 8 * c8;
+        const int64_t at = (int64_t)grow(row) * ldc + n0 + 8 * c8;
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         if (dgelu) {  // GELU'(pre) for the backward instead of pre (GemmArgs::aux_grad)
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_grad_f(v[e]);
         }
         if (dact_in != nullptr) {  // activation backward: x act'(saved)
-          const bf16x8 sv = *reinterpret_cast<const bf16x8*>(dact_in + (int64_t)(rbase + row) * ldd + n0 + 8 * c8);
+          const bf16x8 sv = *reinterpret_cast<const bf16x8*>(dact_in + (int64_t)grow(row) * ldd + n0 + 8 * c8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= dact_scale * dact_f(dact, (float)sv[e]);
         }
         if (res != nullptr) {
-          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (int64_t)(rbase + row) * ldr + n0 + 8 * c8);
+          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + (int64_t)grow(row) * ldr + n0 + 8 * c8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
         }
@@ -512,10 +525,10 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
       for (int u = 0; u < 32 * W / kT; ++u) {
         const int idx = tid + u * kT;
         const int mq = (idx & 7) + 8 * (idx / (8 * W)), n = (idx >> 3) % W;
-        if (rbase + 4 * mq >= M || n0 + n >= N) continue;
+        if (grow(4 * mq) >= M || n0 + n >= N) continue;
         const float* sp = stg + 4 * mq * kStride + n;
         const float4 v = make_float4(sp[0], sp[kStride], sp[2 * kStride], sp[3 * kStride]);
-        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(n0 + n) * ldc + rbase + 4 * mq);
+        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(n0 + n) * ldc + grow(4 * mq));
         if (EPI == kEpiAccumF32) {
           const float4 o = *dst;
           *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
@@ -530,9 +543,9 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
       for (int u = 0; u < 128 * CPR / kT; ++u) {
         const int idx = tid + u * kT;
         const int row = idx / CPR, c4 = idx % CPR;
-        if (rbase + row >= M || n0 + 4 * c4 >= N) continue;
+        if (grow(row) >= M || n0 + 4 * c4 >= N) continue;
         const float4 v = *reinterpret_cast<const float4*>(stg + row * kStride + 4 * c4);
-        float4* dst = reinterpret_cast<float4*>(C + (int64_t)(rbase + row) * ldc + n0 + 4 * c4);
+        float4* dst = reinterpret_cast<float4*>(C + (int64_t)grow(row) * ldc + n0 + 4 * c4);
         if (EPI == kEpiAccumF32) {
           const float4 o = *dst;
           *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
@@ -556,7 +569,7 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
 // (18432 x 6400 x 1600, GELU, p 0.1, pre saved) cost 542 us against 358 plain
 // (tools/epilogue_cost_probe.py).  Also the activation backward of a dgrad
 // whose forward had dropout (dact_in with the mask regenerated).
-template <int ACT, int W, int NJ = W / 64, int kT = 512>
+template <int ACT, int W, int NJ = W / 64, int kT = 512, bool ROWSPLIT = false>
 __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[8][NJ], int wm, int wn,
                                                  int lane, int tid, int m0, int n0, const GemmArgs& g) {
   constexpr int WN = 16 * NJ, kStride = W + 4, CB = W / 8;
@@ -573,7 +586,15 @@ __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[
   const uint32_t thr16 = g.threshold >> 16;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) {
+    if (ROWSPLIT) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(64 * wm + 16 * ii + 4 * quad + r) * kStride + wn * WN + 16 * j + col_in] = acc[4 * pass + ii][j][r];
+    } else if (wm == pass) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -588,7 +609,8 @@ __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[
     for (int u = 0; u < 32 * CB / kT; ++u) {
       const int idx = tid + u * kT;
       const int rq = idx / CB, c8 = idx % CB;  // consecutive lanes on consecutive 8-column chunks
-      const int col = n0 + 8 * c8, row0 = rbase + 4 * rq;
+      const int col = n0 + 8 * c8;
+      const int row0 = ROWSPLIT ? m0 + (((4 * rq) >> 6) << 7) + 64 * pass + ((4 * rq) & 63) : rbase + 4 * rq;
       if (col >= g.N || row0 >= g.M) continue;
       uint32_t wd[4][4];  // [column pair][row]: two 16-bit uniforms per word
       if (drop) {
@@ -1442,9 +1464,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
       for (int j = 0; j < NJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
         const int gi = NJ * i + j;
+        // DMA piece after every 4th MFMA from 1, fragment read after every 4th from 3
+        // (harness schedule 2: tools/micro/gemm4w.hip, profiles/gemm4w_r5.txt)
         if ((gi & 3) == 1) stage_piece(sA, sB, cur, gi >> 2);
-        if (gi % 3 == 0 && gi / 3 < 16) {
-          const int q = gi / 3, ia = q == 0 ? 0 : q - 8;
+        if ((gi & 3) == 3) {
+          const int q = gi >> 2, ia = q == 0 ? 0 : q - 8;
           if (q == 0 || q > 8) fa[0][ia] = frag<A_KC, 256>(nxt, wm * 128 + 16 * ia, 0, lane);
           else fb[0][q - 1] = frag<B_KC, W>(nxt + kTileBytes, wn * WN + 16 * (q - 1), 0, lane);
         }
@@ -1510,7 +1534,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
         for (int i = 0; i < 8; ++i) acc[i][j] += b;
       }
     }
-    staged_store_act<ACT, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g);
+    staged_store_act<ACT, W, NJ, 256, true>(smem, acc, wm, wn, lane, tid, m0, n0, g);
     return;
   }
   if (EPI == kEpiStoreBf16 && (ACT != kActNone || g.bias != nullptr)) {
@@ -1535,14 +1559,14 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
                                    : reinterpret_cast<void*>(reinterpret_cast<float*>(g.C) +
                                                              (int64_t)blockIdx.y * g.M * g.ldc);
   if (EPI == kEpiStoreBf16 && g.dact_in != nullptr)
-    staged_store<EPI, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+    staged_store<EPI, W, NJ, 256, true>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
                                   reinterpret_cast<const bf16_t*>(g.res), g.ldr,
                                   reinterpret_cast<const bf16_t*>(g.dact_in), g.ldd, g.dact, g.dact_scale);
   else if (EPI != kEpiStoreBf16 && g.trans_c && g.k_splits <= 1)
-    staged_store<EPI, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out, nullptr, 0, nullptr, 0,
+    staged_store<EPI, W, NJ, 256, true>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out, nullptr, 0, nullptr, 0,
                                   0, 1.f, true);
   else
-    staged_store<EPI, W, NJ, 256>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
+    staged_store<EPI, W, NJ, 256, true>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
                                   EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
 }
 

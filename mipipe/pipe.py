@@ -255,8 +255,19 @@ class Pipe(nn.Module):
             queues anyway; see ``profiles/copy_streams_ab.txt``.
         balance: explicit partition sizes (number of top-level children per
             partition, torchgpipe style).  Lets several partitions share a
-            GPU; each later partition on a device computes on a dedicated
-            stream so neighbouring stages overlap.
+            GPU (see ``stage_streams``).
+        stage_streams: how partitions that share a GPU compute.  ``"shared"``
+            (default): all of them on the device's current stream, the
+            reference's choice (``streams = [current_stream(d) for d in
+            devices]``, ``/root/reference/pipeline.py:158``: one stream per
+            device, whatever the partition count).  ``"dedicated"``: every
+            later partition on a device gets its own stream, so neighbouring
+            stages' kernels run concurrently.  Concurrency does not pay with
+            real compute: on one MI355X the reference's structure (ref_main
+            fp32, ``balance`` 8,8 layers) runs at 26.7k tok/s with dedicated
+            stage streams against 36.0k shared -- two stages' GEMMs split the
+            CUs and every kernel stretches 1.3-2.7x (``profiles/pipe_gap_r5.txt``);
+            with one partition it is 36.0k, the engine's 36.2k.
         copy_same_device: make a boundary between two partitions of the same
             GPU a real device-to-device copy on the copy streams (the native
             ``peer_copy`` path a multi-GPU boundary takes) instead of handing
@@ -278,6 +289,7 @@ class Pipe(nn.Module):
         balance: Optional[List[int]] = None,
         copy_same_device: bool = False,
         copy_engine: Optional[str] = None,
+        stage_streams: str = "shared",
     ) -> None:
         super().__init__()
         chunks = int(chunks)
@@ -306,6 +318,9 @@ class Pipe(nn.Module):
             raise ValueError(f"copy_engine must be one of {sorted(COPY_ENGINES)}, got {copy_engine!r}")
         self.copy_same_device = bool(copy_same_device)
         self.copy_engine = copy_engine
+        if stage_streams not in ("shared", "dedicated"):
+            raise ValueError(f"stage_streams must be 'shared' or 'dedicated', got {stage_streams!r}")
+        self.stage_streams = stage_streams
 
         self.partitions, self.devices = _split_module(module, balance)
         _verify_splitting(module, self.partitions, self.devices)
@@ -371,15 +386,15 @@ class Pipe(nn.Module):
     def _ensure_compute_streams(self) -> List[Optional[AbstractStream]]:
         """Compute stream per partition: ``None`` (= the device's current
         stream, the reference's choice, ``/root/reference/pipeline.py:158``)
-        for the first partition on each device, a dedicated stream for every
-        later partition on the same GPU -- two stages of one GPU must not
-        share an in-order stream, or micro-batch i+1 of stage j-1 could never
-        overlap micro-batch i of stage j."""
+        for every partition with ``stage_streams="shared"``; with
+        ``"dedicated"``, for the first partition on each device only, and a
+        stream of its own for every later partition on the same GPU (then
+        micro-batch i+1 of stage j-1 can overlap micro-batch i of stage j)."""
         seen = set()
         out: List[Optional[AbstractStream]] = []
         for device in self.devices:
             key = (device.type, device.index if device.index is not None else -1)
-            if device.type == "cuda" and key in seen:
+            if device.type == "cuda" and key in seen and self.stage_streams == "dedicated":
                 out.append(new_stream(device))
             else:
                 out.append(None)

@@ -7,9 +7,11 @@ device-to-device copy fenced by pooled events, i.e. ``peer_copy``),
 ``Wait`` events between copy and compute streams, ``record_stream`` on the
 streams that consume, portals for cross-partition skips, and recompute on the
 stage streams (``/root/reference/pipeline.py:119-142,186-192,253-254``;
-``README.md:193-237,332-369``).  Every later partition on the GPU computes on
-a dedicated stream, so stage j's micro-batch i really overlaps stage j-1's
-micro-batch i+1 (sleep-kernel test).
+``README.md:193-237,332-369``).  With ``stage_streams="dedicated"`` every later
+partition on the GPU computes on a stream of its own, so stage j's micro-batch i
+really overlaps stage j-1's micro-batch i+1 (sleep-kernel test); the default,
+``"shared"``, computes every partition of a GPU on its current stream, as the
+reference does (one stream per device).
 """
 import copy
 import dataclasses
@@ -47,19 +49,20 @@ def _loss(cfg, y, t):
 _BALANCE = {2: [3, 3], 4: [2, 1, 1, 2]}  # 6 LM blocks: encoder, 2 x (attention, FFN), decoder
 
 
-def _pipe_step(nparts, checkpoint, dropout, copy_same_device, seed=99, engine=None):
+def _pipe_step(nparts, checkpoint, dropout, copy_same_device, seed=99, engine=None, stage_streams="dedicated"):
     cfg = _cfg(dropout)
     torch.manual_seed(0)
     model = torch.nn.Sequential(*build_lm_blocks(cfg, dtype=torch.bfloat16)).to(DEV).train()
     opt = FlatAdam(model.parameters(), lr=1e-3)
     pipe = Pipe(model, chunks=4, checkpoint=checkpoint, balance=_BALANCE[nparts],
-                copy_same_device=copy_same_device, copy_engine=engine, return_rref=False)
+                copy_same_device=copy_same_device, copy_engine=engine, return_rref=False, stage_streams=stage_streams)
     x, t = _data(cfg, 4, 2)
     try:
         assert len(pipe.partitions) == nparts and all(d == DEV for d in pipe.devices)
-        # later partitions of the GPU compute on streams of their own
+        # dedicated: later partitions of the GPU compute on streams of their own;
+        # shared: all on the device's current stream (the reference's one per device)
         streams = pipe.pipeline.compute_streams()
-        assert len({s.cuda_stream for s in streams}) == nparts
+        assert len({s.cuda_stream for s in streams}) == (nparts if stage_streams == "dedicated" else 1)
         opt.zero_grad()
         torch.manual_seed(seed)
         out = pipe(x)
@@ -121,7 +124,8 @@ def test_check_pipe_four_partitions_one_gpu():
     torch.manual_seed(0)
     model = torch.nn.Sequential(*build_lm_blocks(cfg, dtype=torch.bfloat16)).to(DEV).train()
     FlatAdam(model.parameters(), lr=1e-3)
-    pipe = Pipe(model, chunks=4, checkpoint="except_last", balance=_BALANCE[4], copy_same_device=True)
+    pipe = Pipe(model, chunks=4, checkpoint="except_last", balance=_BALANCE[4], copy_same_device=True,
+                stage_streams="dedicated")
     x, t = _data(cfg, 4, 2)
     try:
         assert len(pipe.partitions) == 4
@@ -157,7 +161,7 @@ def test_skippable_portals_across_partitions_one_gpu(checkpoint):
     loss_ref.backward()
     ref_opt.fold_grads()
     pipe = Pipe(model, chunks=4, checkpoint=checkpoint, balance=[2, 2, 2, 2], copy_same_device=True,
-                return_rref=False)
+                return_rref=False, stage_streams="dedicated")
     try:
         assert len(pipe.partitions) == 4
         layout = pipe._skip_layout
@@ -220,7 +224,8 @@ def test_stage_overlap_on_one_gpu():
     backward (autograd, phony ordering) must overlap the same way."""
     us = 20000
     model = torch.nn.Sequential(_SleepLayer(us), _SleepLayer(us)).to(DEV)
-    pipe = Pipe(model, chunks=4, checkpoint="never", balance=[1, 1], copy_same_device=True, return_rref=False)
+    pipe = Pipe(model, chunks=4, checkpoint="never", balance=[1, 1], copy_same_device=True, return_rref=False,
+                stage_streams="dedicated")
     x = torch.randn(8, 1024, device=DEV, requires_grad=True)
     out = {}
     try:
@@ -235,3 +240,25 @@ def test_stage_overlap_on_one_gpu():
     assert fwd > 0.95 * 5 * us * 1e-6, fwd  # sanity: 5 ticks is the floor
     assert bwd < 0.85 * serial, f"backward {bwd * 1e3:.1f} ms: stages did not overlap"
     assert torch.allclose(x.grad, torch.ones_like(x))
+
+
+def test_shared_stage_streams_default_matches_sequential():
+    """The default (stage_streams='shared', the reference's one stream per
+    device): the partitions of cuda:0 all compute on its current stream, the
+    boundaries still copy on the copy streams -- same loss and gradients as
+    the plain model."""
+    cfg = _cfg(0.0)
+    torch.manual_seed(0)
+    blocks = build_lm_blocks(cfg, dtype=torch.bfloat16)
+    ref = torch.nn.Sequential(*copy.deepcopy(blocks)).to(DEV).train()
+    ref_opt = FlatAdam(ref.parameters(), lr=1e-3)
+    x, t = _data(cfg, 4, 2)
+    ref_opt.zero_grad()
+    loss_ref = _loss(cfg, ref(x), t)
+    loss_ref.backward()
+    ref_opt.fold_grads()
+    loss, grads = _pipe_step(4, "never", 0.0, True, stage_streams="shared")
+    assert abs(loss - float(loss_ref)) < 2e-3 * abs(float(loss_ref))
+    for n, q in ref.named_parameters():
+        g, gr = grads[n].float(), q.main_grad.float()
+        assert (g - gr).abs().max().item() < 2e-2 * (gr.abs().max().item() + 1e-6), n

@@ -48,7 +48,7 @@ def step(pipe):
 arms = {"per (partition, micro-batch)": None, "pool k=1": 1, "pool k=2": 2, "pool k=4": 4}
 # balance=[1]*P: one partition per part even though they share cuda:0 (without it the
 # reference's split rule merges same-device children into ONE partition: no boundaries)
-pipes = {name: Pipe(model, chunks=M, checkpoint="never", copy_streams=k, balance=[1] * len(parts),
+pipes = {name: Pipe(model, chunks=M, checkpoint="never", copy_streams=k, balance=[1] * len(parts), stage_streams="dedicated",
                     copy_same_device=True) for name, k in arms.items()}
 assert all(len(p.partitions) == len(parts) for p in pipes.values())
 times = {name: [] for name in arms}

@@ -144,6 +144,7 @@ def run(parts: int, chunks: int, steps: int = 3) -> None:
     model = torch.nn.Sequential(*blocks).to(dev).train()
     opt = FlatAdam(model.parameters(), lr=1e-4)
     pipe = Pipe(model, chunks=chunks, checkpoint="except_last", balance=balance, copy_same_device=True,
+                stage_streams="dedicated",
                 return_rref=False)
     mb = 8
     tok = torch.randint(0, cfg.vocab, (chunks * mb, cfg.seq_len + 1))
