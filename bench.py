@@ -108,6 +108,9 @@ def parse():
                          "embedding + layers 0-7 | layers 8-15 + decoder); with --gpus 1 every partition sits on "
                          "cuda:0 and each boundary is a native device-to-device copy on the copy streams "
                          "(Pipe(balance=..., copy_same_device=True)), else partition j on cuda:j")
+    ap.add_argument("--pipe-stage-streams", default="shared", choices=["shared", "dedicated"],
+                    help="--impl pipe with several partitions on one GPU: compute them all on the device's stream "
+                         "(shared, the reference's one stream per device) or each later one on its own stream")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -514,7 +517,7 @@ def run_pipe(args) -> int:
         params = [p for b in blocks for p in b.parameters()]
         opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
         pipe = mipipe.Pipe(torch.nn.Sequential(*blocks), chunks=m, checkpoint=args.checkpoint, balance=balance,
-                           copy_same_device=(n == 1 and len(balance) > 1))
+                           copy_same_device=(n == 1 and len(balance) > 1), stage_streams=args.pipe_stage_streams)
         plan = None
     else:
         plan = plan_stages(cfg, n, 1, m, split_decoder=False)
