@@ -108,15 +108,15 @@ def parse():
                          "embedding + layers 0-7 | layers 8-15 + decoder); with --gpus 1 every partition sits on "
                          "cuda:0 and each boundary is a native device-to-device copy on the copy streams "
                          "(Pipe(balance=..., copy_same_device=True)), else partition j on cuda:j")
-    ap.add_argument("--pipe-stage-streams", default="shared", choices=["shared", "dedicated"],
+    ap.add_argument("--pipe-stage-streams", default="dedicated", choices=["shared", "dedicated"],
                     help="--impl pipe with several partitions on one GPU: compute them all on the device's stream "
                          "(shared, the reference's one stream per device) or each later one on its own stream")
     ap.add_argument("--pipe-boundary", default="copy", choices=["copy", "inplace"],
                     help="--impl pipe, several partitions on ONE GPU: a native device-to-device copy on the copy "
                          "streams at each boundary (copy, the multi-GPU path) or the tensor handed over in place "
                          "(inplace: what the reference's Copy does on one device -- .to(same device) is a no-op)")
-    ap.add_argument("--pipe-copy-streams", type=int, default=None,
-                    help="--impl pipe: copy streams per partition (default: one per micro-batch, the reference's)")
+    ap.add_argument("--pipe-copy-streams", type=int, default=1,
+                    help="--impl pipe: copy streams per partition (default 1; 0 = the reference's one per micro-batch)")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -524,7 +524,8 @@ def run_pipe(args) -> int:
         opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip, defer_wgrad=True)
         pipe = mipipe.Pipe(torch.nn.Sequential(*blocks), chunks=m, checkpoint=args.checkpoint, balance=balance,
                            copy_same_device=(n == 1 and len(balance) > 1 and args.pipe_boundary == "copy"),
-                           stage_streams=args.pipe_stage_streams, copy_streams=args.pipe_copy_streams)
+                           stage_streams=args.pipe_stage_streams,
+                           copy_streams=args.pipe_copy_streams if args.pipe_copy_streams != 0 else None)
         plan = None
     else:
         plan = plan_stages(cfg, n, 1, m, split_decoder=False)

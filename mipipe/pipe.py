@@ -246,28 +246,28 @@ class Pipe(nn.Module):
         checkpoint: ``"always"``, ``"except_last"`` or ``"never"``.
         deferred_batch_norm: track BatchNorm statistics over the whole mini-batch.
         return_rref: return an RRef (upstream behaviour, default) or the output.
-        copy_streams: copy streams per partition.  ``None`` (default) keeps the
+        copy_streams: copy streams per partition, shared round-robin by the
+            micro-batches.  ``1`` (default): one per partition.  ``None``: the
             reference's one stream per (partition, micro-batch)
-            (``/root/reference/pipe.py:417-429``); an integer ``k`` gives each
-            partition ``k`` streams shared round-robin by the micro-batches.
-            A HIP process has few hardware queues (``GPU_MAX_HW_QUEUES``, 4 by
-            default), so ``chunks x partitions`` streams alias onto the same
-            queues anyway; see ``profiles/copy_streams_ab.txt``.
+            (``/root/reference/pipe.py:417-429``).  Every stream a HIP process
+            drives gets a hardware queue of its own (up to
+            ``GPU_MAX_HW_QUEUES``), and with chunks x partitions queues busy at
+            once the GPU time-slices them: on one MI355X the reference's
+            structure (ref_main fp32, 2 partitions, chunks 4 -> 8 copy streams)
+            ran 27.5k tok/s with per-micro-batch copy streams against 36.8k
+            with one per partition, the engine's 36.1k
+            (``profiles/pipe_gap_r5.txt``).
         balance: explicit partition sizes (number of top-level children per
             partition, torchgpipe style).  Lets several partitions share a
             GPU (see ``stage_streams``).
-        stage_streams: how partitions that share a GPU compute.  ``"shared"``
-            (default): all of them on the device's current stream, the
+        stage_streams: how partitions that share a GPU compute.
+            ``"dedicated"`` (default): every later partition on a device gets a
+            stream of its own, so neighbouring stages' kernels overlap.
+            ``"shared"``: all of them on the device's current stream, the
             reference's choice (``streams = [current_stream(d) for d in
-            devices]``, ``/root/reference/pipeline.py:158``: one stream per
-            device, whatever the partition count).  ``"dedicated"``: every
-            later partition on a device gets its own stream, so neighbouring
-            stages' kernels run concurrently.  Concurrency does not pay with
-            real compute: on one MI355X the reference's structure (ref_main
-            fp32, ``balance`` 8,8 layers) runs at 26.7k tok/s with dedicated
-            stage streams against 36.0k shared -- two stages' GEMMs split the
-            CUs and every kernel stretches 1.3-2.7x (``profiles/pipe_gap_r5.txt``);
-            with one partition it is 36.0k, the engine's 36.2k.
+            devices]``, ``/root/reference/pipeline.py:158``).  Measured on one
+            MI355X (ref_main fp32, 2 partitions, one copy stream each): 36.8k
+            tok/s dedicated, 35.5k shared (``profiles/pipe_gap_r5.txt``).
         copy_same_device: make a boundary between two partitions of the same
             GPU a real device-to-device copy on the copy streams (the native
             ``peer_copy`` path a multi-GPU boundary takes) instead of handing
@@ -285,11 +285,11 @@ class Pipe(nn.Module):
         deferred_batch_norm: bool = False,
         *,
         return_rref: bool = True,
-        copy_streams: Optional[int] = None,
+        copy_streams: Optional[int] = 1,
         balance: Optional[List[int]] = None,
         copy_same_device: bool = False,
         copy_engine: Optional[str] = None,
-        stage_streams: str = "shared",
+        stage_streams: str = "dedicated",
     ) -> None:
         super().__init__()
         chunks = int(chunks)

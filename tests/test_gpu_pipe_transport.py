@@ -242,7 +242,7 @@ def test_stage_overlap_on_one_gpu():
     assert torch.allclose(x.grad, torch.ones_like(x))
 
 
-def test_shared_stage_streams_default_matches_sequential():
+def test_shared_stage_streams_match_sequential():
     """The default (stage_streams='shared', the reference's one stream per
     device): the partitions of cuda:0 all compute on its current stream, the
     boundaries still copy on the copy streams -- same loss and gradients as
