@@ -145,7 +145,10 @@ def test_pipe_copy_stream_pool():
     (row,) = pipe._copy_streams
     assert len(row) == 5 and len({id(s) for s in row}) == 2 and row[0] is row[2] is row[4]
     pipe.close()
-    pipe = Pipe(torch.nn.Sequential(lin), chunks=5)
+    pipe = Pipe(torch.nn.Sequential(lin), chunks=5)  # default: one copy stream per partition
+    assert len({id(s) for s in pipe._copy_streams[0]}) == 1
+    pipe.close()
+    pipe = Pipe(torch.nn.Sequential(lin), chunks=5, copy_streams=None)  # the reference's: one per micro-batch
     assert len({id(s) for s in pipe._copy_streams[0]}) == 5
     pipe.close()
     with pytest.raises(ValueError):
