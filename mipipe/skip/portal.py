@@ -16,6 +16,12 @@ engine runs their backwards in the order Orange -> Copy -> Blue.
 Tensor life: a portal drops its tensor as soon as the last forward user has
 taken it, to keep activation memory at the reference's level.  The number of
 forward users depends on checkpointing (see ``SkipTrackerThroughPortals.save``).
+
+Attribution: the portal design (three autograd functions on the phony chain,
+the 3-vs-2 forward-user tensor life, PortalCopy reusing Copy's forward /
+backward) follows upstream PyTorch's torch.distributed.pipeline.sync.skip
+(BSD-3-Clause, originally from torchgpipe); this file re-implements that
+behaviour, which SURVEY.md C14 requires bit-for-bit.
 """
 from __future__ import annotations
 

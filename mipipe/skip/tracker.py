@@ -10,6 +10,12 @@
 
 The tracker for the running task is found through a thread-local set by
 :func:`use_skip_tracker` (``/root/reference/pipeline.py:208,228``).
+
+Attribution: the portal design (three autograd functions on the phony chain,
+the 3-vs-2 forward-user tensor life, PortalCopy reusing Copy's forward /
+backward) follows upstream PyTorch's torch.distributed.pipeline.sync.skip
+(BSD-3-Clause, originally from torchgpipe); this file re-implements that
+behaviour, which SURVEY.md C14 requires bit-for-bit.
 """
 from __future__ import annotations
 
