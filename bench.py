@@ -117,6 +117,10 @@ def parse():
                          "(inplace: what the reference's Copy does on one device -- .to(same device) is a no-op)")
     ap.add_argument("--pipe-copy-streams", type=int, default=1,
                     help="--impl pipe: copy streams per partition (default 1; 0 = the reference's one per micro-batch)")
+    ap.add_argument("--opt-overlap", default="off", choices=["on", "off"],
+                    help="on = the Adam step runs on a side stream in forward-order chunks and the next step's "
+                         "forward waits per module (FlatAdam(overlap_modules=...)): the memory-bound update fills "
+                         "CUs the GEMMs leave idle")
     ap.add_argument("--skips", default="none", choices=["none", "unet"],
                     help="unet = @skippable long residuals layer i -> layer L-1-i across stages "
                          "(BASELINE config #5; stash rank -> pop rank over their own xGMI link)")
@@ -217,7 +221,8 @@ def main() -> int:
     params = [p for st_ in stages for p in st_.parameters()]
     n_params_local = sum(p.numel() for p in params)
 
-    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip)
+    opt = FlatAdam(params, lr=args.lr, max_grad_norm=args.clip,
+                   overlap_modules=stages if args.opt_overlap == "on" else None)
 
     is_last = prank == pp - 1
     groups = dpg = None
@@ -393,6 +398,8 @@ def main() -> int:
                          if transport_used.startswith("ipc") else "engine (one process per GPU)"),
                 "transport": transport_used,
                 "transport_note": getattr(engine, "transport_note", None),
+                "optimizer": "FlatAdam, " + ("overlapped with the next forward (side stream, forward-order chunks)"
+                                             if opt._overlap is not None else "serial at the end of the step"),
                 "shared_gpu": bool(args.shared_gpu),
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),

@@ -16,6 +16,18 @@ out identically.  Consequences:
 
 Semantics match ``torch.optim.Adam`` (L2 weight decay) or ``AdamW``
 (``adamw=True``) with ``clip_grad_norm_(max_norm)`` applied first.
+
+``overlap_modules`` (optional): the step runs on a side stream of its own, in
+chunks laid out in forward order (the non-GEMM parameters -- embedding,
+LayerNorm, biases -- first, then the GEMM weights in the order given), with an
+event after each chunk; a forward pre-hook on every module that owns
+parameters makes the compute stream wait for the chunk holding that module's
+last parameter, once per step.  The next step's forward then starts while the
+update of later layers is still streaming through HBM: the memory-bound update
+fills the CUs the GEMMs leave idle instead of running alone at the end of the
+step.  The step also zero-fills the non-GEMM gradients on that stream (the
+GEMM weights' gradients are overwritten by their first write), so under
+``overlap_modules`` ``step()`` consumes the gradients.
 """
 from __future__ import annotations
 
@@ -76,6 +88,7 @@ class FlatAdam:
         adamw: bool = False,
         max_grad_norm: Optional[float] = None,
         defer_wgrad: bool = False,
+        overlap_modules: Optional[Iterable[nn.Module]] = None,
     ) -> None:
         self.lr = lr
         self.betas = betas
@@ -102,6 +115,11 @@ class FlatAdam:
             seen.add(id(p))
             buckets.setdefault((p.device, p.dtype), []).append(p)
         self.groups = [_Group(ps, d, t) for (d, t), ps in buckets.items()]
+        self._overlap = None
+        # chunk starts must keep the kernel's 16-byte vectors aligned: the non-GEMM range starts at n_lazy
+        if (overlap_modules is not None and all(g.device.type == "cuda" for g in self.groups)
+                and all(g.n_lazy % 64 == 0 for g in self.groups)):
+            self._overlap = _Overlap(self, list(overlap_modules))
 
     @property
     def params(self) -> List[nn.Parameter]:
@@ -121,6 +139,19 @@ class FlatAdam:
         mine = self._param_ids()
         if mine & deferred_param_ids():
             drop_deferred_wgrad(mine)
+        if self._overlap is not None and self._overlap.zeroed:
+            # the overlapped step zero-filled the non-GEMM gradients on its stream
+            # and marked the GEMM weights fresh; nothing to queue here
+            self._overlap.zeroed = False
+            for g in self.groups:
+                for p in g.params:
+                    p.grad = None
+            if self.defer_wgrad and not self._deferring:
+                from .ops.linear import begin_deferred_wgrad
+
+                self._deferring = begin_deferred_wgrad()
+            return
+        self.wait_step()
         for g in self.groups:
             if lazy and g.n_lazy:
                 g.main_grad[g.n_lazy:].zero_()
@@ -152,6 +183,8 @@ class FlatAdam:
         (running every queued GEMM) and leaves the deferral open."""
         from .ops.linear import deferred_param_ids, end_deferred_wgrad, flush_wgrad
 
+        if self._overlap is not None:
+            self._overlap.wait_pending()  # modules that never ran forward this step
         if self._deferring:
             self._deferring = False
             end_deferred_wgrad()
@@ -196,6 +229,9 @@ class FlatAdam:
         bc1 = 1 - b1 ** self.step_count
         bc2 = 1 - b2 ** self.step_count
         max_norm = float(self.max_grad_norm) if self.max_grad_norm is not None else 0.0
+        if self._overlap is not None:
+            self._overlap.step(grad_sumsq, b1, b2, bc1, bc2, max_norm)
+            return
         for g in self.groups:
             sq = grad_sumsq.to(g.device) if grad_sumsq is not None else None
             if g.device.type == "cuda":
@@ -224,7 +260,15 @@ class FlatAdam:
         if g.master is not g.model:
             g.model.copy_(p)
 
+    def wait_step(self) -> None:
+        """Makes the current stream wait for an overlapped step still in flight
+        (no-op otherwise).  Needed only by code that reads the parameters or the
+        optimizer state outside the hooked modules' forwards."""
+        if self._overlap is not None:
+            self._overlap.wait_all()
+
     def state_dict(self) -> dict:
+        self.wait_step()
         return {
             "step": self.step_count,
             "groups": [
@@ -233,6 +277,7 @@ class FlatAdam:
         }
 
     def load_state_dict(self, state: dict) -> None:
+        self.wait_step()
         self.step_count = int(state["step"])
         with torch.no_grad():
             for g, s in zip(self.groups, state["groups"]):
@@ -241,3 +286,119 @@ class FlatAdam:
                 g.exp_avg_sq.copy_(s["exp_avg_sq"])
                 if g.master is not g.model:
                     g.model.copy_(g.master)
+
+
+def overlap_chunks(sizes: List[int], n_lazy_params: int, min_chunk: int) -> Tuple[List[Tuple[int, int]], List[int]]:
+    """Chunks of a group's flat buffer for the overlapped step, in issue order,
+    and each parameter's chunk (the one that updates its LAST element).
+
+    ``sizes``: parameter numels in buffer order, the first ``n_lazy_params``
+    being the GEMM weights.  Chunk 0 is the non-GEMM range ``[n_lazy, n)`` (if
+    any); the GEMM range follows, cut at parameter ends rounded down to 64
+    elements once a chunk holds ``min_chunk`` elements."""
+    n_lazy = sum(sizes[:n_lazy_params])
+    n = sum(sizes)
+    chunks: List[Tuple[int, int]] = [(n_lazy, n)] if n > n_lazy else []
+    owner = [0] * len(sizes)
+    start = off = 0
+    pending: List[Tuple[int, int]] = []  # (parameter index, its end offset) not yet in a closed chunk
+    for i in range(n_lazy_params):
+        off += sizes[i]
+        pending.append((i, off))
+        end = off if off == n_lazy else (off // 64) * 64
+        if end - start >= min_chunk or off == n_lazy:
+            chunks.append((start, end))
+            for j, j_end in pending:
+                if j_end <= end:
+                    owner[j] = len(chunks) - 1
+            pending = [(j, j_end) for j, j_end in pending if j_end > end]
+            start = end
+    return chunks, owner
+
+
+class _Overlap:
+    """The side-stream step of :class:`FlatAdam` (``overlap_modules``).
+
+    Chunks per group, in forward order: ``[n_lazy, n)`` (every non-GEMM
+    parameter: embedding, LayerNorm, biases; its zero-fill rides with it), then
+    the GEMM weights ``[0, n_lazy)`` cut at parameter ends into chunks of at
+    least ``MIN_CHUNK`` elements.  Boundaries stay multiples of 64 elements (the
+    Adam kernel's 16-byte vectors)."""
+
+    MIN_CHUNK = 1 << 23
+
+    def __init__(self, opt: "FlatAdam", modules: List[nn.Module]) -> None:
+        self.opt = opt
+        self.zeroed = False
+        self.streams = {}
+        self.chunks: List[List[Tuple[int, int]]] = []  # per group: [(start, end)] in issue order
+        chunk_of: Dict[int, Tuple[int, int]] = {}  # id(param) -> (group, chunk index)
+        for gi, g in enumerate(opt.groups):
+            if g.device not in self.streams:
+                # the least priority HIP offers: when a CU frees, the compute queue's next block goes first
+                least = torch.cuda.Stream.priority_range()[0]
+                prio = int(os.environ.get("MIPIPE_OPT_STREAM_PRIORITY", least))
+                self.streams[g.device] = torch.cuda.Stream(device=g.device, priority=prio)
+            chunks, owner = overlap_chunks([p.numel() for p in g.params], len(g.lazy), self.MIN_CHUNK)
+            for p, ci in zip(g.params, owner):
+                chunk_of[id(p)] = (gi, ci)
+            self.chunks.append(chunks)
+        # module -> the (group, chunk) its forward must wait for: the latest chunk of its direct parameters
+        self.need: Dict[int, Dict[int, int]] = {}
+        self.hooks = []
+        for top in modules:
+            for mod in top.modules():
+                direct = [p for p in mod.parameters(recurse=False) if id(p) in chunk_of]
+                if not direct or id(mod) in self.need:
+                    continue
+                need: Dict[int, int] = {}
+                for p in direct:
+                    gi, ci = chunk_of[id(p)]
+                    need[gi] = max(need.get(gi, -1), ci)
+                self.need[id(mod)] = need
+                self.hooks.append(mod.register_forward_pre_hook(self._hook))
+        # one event per chunk, re-recorded every step (a wait binds to the record before it)
+        self.events = [[torch.cuda.Event() for _ in chunks] for chunks in self.chunks]
+        self.pending: Dict[int, Dict[int, int]] = {}  # modules still to wait this step
+
+    def _hook(self, mod: nn.Module, args) -> None:
+        need = self.pending.pop(id(mod), None)
+        if need:
+            for gi, ci in need.items():
+                g = self.opt.groups[gi]
+                torch.cuda.current_stream(g.device).wait_event(self.events[gi][ci])
+
+    def step(self, grad_sumsq: Optional[Tensor], b1, b2, bc1, bc2, max_norm) -> None:
+        self.wait_pending()  # a step without a forward in between
+        k = _native_loader.kernels()
+        opt = self.opt
+        for gi, g in enumerate(opt.groups):
+            cur = torch.cuda.current_stream(g.device)
+            side = self.streams[g.device]
+            sq = grad_sumsq.to(g.device) if grad_sumsq is not None else None
+            side.wait_stream(cur)  # gradients, the global norm
+            if sq is not None:
+                sq.record_stream(side)
+            with torch.cuda.stream(side):
+                for ci, (a, b) in enumerate(self.chunks[gi]):
+                    model = g.model[a:b] if g.dtype != torch.float32 else None
+                    k.adam_step(g.master[a:b], model, g.main_grad[a:b], g.exp_avg[a:b], g.exp_avg_sq[a:b],
+                                opt.lr, b1, b2, opt.eps, opt.weight_decay, bc1, bc2, sq, max_norm, opt.adamw)
+                    if ci == 0 and a == g.n_lazy:
+                        g.main_grad[a:b].zero_()  # the non-GEMM gradients of the next step
+                    self.events[gi][ci].record(side)
+            for p in g.lazy:
+                p._mg_fresh = True  # type: ignore[attr-defined]  # the next backward's first write overwrites
+        self.zeroed = True
+        self.pending = {mid: dict(need) for mid, need in self.need.items()}
+
+    def wait_pending(self) -> None:
+        """The current streams wait for every chunk a module has not waited for yet."""
+        if self.pending:
+            self.pending = {}
+            self.wait_all()
+
+    def wait_all(self) -> None:
+        for g in self.opt.groups:
+            torch.cuda.current_stream(g.device).wait_stream(self.streams[g.device])
+        self.pending = {}

@@ -75,6 +75,8 @@ def save_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
 
     params = _named(named_params)
     by_id = {id(p): n for n, p in params.items()}
+    if isinstance(optimizer, FlatAdam):
+        optimizer.wait_step()  # an overlapped step may still be writing the weights and the moments
     tensors: Dict[str, Tensor] = {f"param.{n}": _host(p) for n, p in params.items()}
     meta = {"format": FORMAT, "step": int(step), "extra": extra or {}}
     if isinstance(optimizer, FlatAdam):
@@ -192,6 +194,8 @@ def load_training_state(path: str, named_params: Iterable[Tuple[str, nn.Paramete
             raise KeyError(f"{path}: no weights for {n!r}")
         if tuple(tensors[key].shape) != tuple(p.shape):
             raise ValueError(f"{path}: {n!r} is {tuple(tensors[key].shape)}, the model has {tuple(p.shape)}")
+    if isinstance(optimizer, FlatAdam):
+        optimizer.wait_step()
     for n, p in params.items():
         p.copy_(tensors[f"param.{n}"])
     if isinstance(optimizer, FlatAdam):
