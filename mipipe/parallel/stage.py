@@ -266,7 +266,7 @@ def _makespan_refined(costs: List[float], ranks: int, virtual: int, chunks: int,
 
 def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, split_decoder: bool = False,
                 bwd_ratio: float = 2.0, costs: Optional[List[float]] = None,
-                objective: str = "makespan") -> StagePlan:
+                objective: str = "makespan", seeds: Sequence[Sequence[int]] = ()) -> StagePlan:
     """Plan for ``stages`` ranks with ``virtual`` chunks each (looping placement).
 
     With ``virtual > 1`` the split starts from the rank-total-balanced one and
@@ -279,7 +279,12 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, s
     ``objective="balance"``: the split with the most even RANK totals
     (``balance_by_time``'s goal), without the makespan refinement -- which
     may load ranks unevenly when that shortens the simulated fill / drain
-    (profiles/pp_planning_r4.txt compares the two)."""
+    (profiles/pp_planning_r4.txt compares the two).
+
+    ``seeds``: further starting splits for the makespan refinement (e.g. the
+    analytic-cost plan when planning with measured costs: coordinate descent
+    from the cost-balanced starts can stall in a worse local optimum,
+    profiles/plan_table_r5.txt); invalid ones are ignored."""
     if costs is None:
         costs = block_costs(cfg, split_decoder)
     elif len(costs) != len(block_costs(cfg, split_decoder)):
@@ -288,13 +293,25 @@ def plan_stages(cfg: LMConfig, stages: int, virtual: int = 1, chunks: int = 0, s
         raise ValueError(f"{stages} x {virtual} virtual stages exceed the {len(costs)} pipeline units")
     if objective not in ("makespan", "balance"):
         raise ValueError(f"objective must be 'makespan' or 'balance', got {objective!r}")
+    groups = stages * virtual
+    seeds = [list(b) for b in seeds
+             if len(b) == groups and sum(b) == len(costs) and all(k >= 1 for k in b)]
+    m = chunks or 4 * stages
     if virtual == 1:
-        return StagePlan(balance_cost(costs, stages), costs, 1, split_decoder)
+        plan = StagePlan(balance_cost(costs, stages), costs, 1, split_decoder)
+        if objective == "makespan" and seeds:
+            def sim1(p: StagePlan) -> float:
+                return simulate_step([p.stage_cost(g) for g in range(stages)], stages, 1, m, bwd_ratio,
+                                     deferred_w=1.0 / bwd_ratio)[0]
+            for b in seeds:
+                cand = StagePlan(b, costs, 1, split_decoder)
+                if sim1(cand) < sim1(plan):
+                    plan = cand
+        return plan
     if objective == "balance":
         return StagePlan(_rank_balanced(costs, stages, virtual), costs, virtual, split_decoder)
-    m = chunks or 4 * stages
     best = None
-    for start in (balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)):
+    for start in [balance_cost(costs, stages * virtual), _rank_balanced(costs, stages, virtual)] + seeds:
         bal = _makespan_refined(costs, stages, virtual, m, start, bwd_ratio)
         plan = StagePlan(bal, costs, virtual, split_decoder)
         t = simulate_step([plan.stage_cost(g) for g in range(stages * virtual)], stages, virtual, m, bwd_ratio,
@@ -471,8 +488,15 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
     screened.sort()
     best = None
     for _, v, split in screened[:6]:
+        seeds = ()
+        if cost_fn is not None and objective == "makespan":
+            # the analytic plan as a further start: with measured costs the refinement alone can stall
+            # in a worse split (profiles/plan_table_r5.txt: config #3's analytic v=2 plan simulates 6 %
+            # faster under the MEASURED costs than the split refined from them)
+            seeds = (plan_stages(cfg, stages, v, chunks, split, bwd_ratio, objective="makespan").balance,)
         plan = plan_stages(cfg, stages, v, chunks, split, bwd_ratio,
-                           costs=cost_fn(split) if cost_fn is not None else None, objective=objective)
+                           costs=cost_fn(split) if cost_fn is not None else None, objective=objective,
+                           seeds=seeds)
         t = sim(plan, v)
         # ties (within 0.5 %) keep the simpler plan: fewer chunks, no split
         key = (v, split)

@@ -11,7 +11,13 @@ for arm in off on on off on off; do
   timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --opt-overlap $arm > gpurun_out/ov_$arm.log 2>&1 || { tail -20 gpurun_out/ov_$arm.log; exit 1; }
   echo "opt-overlap $arm: $(grep -o '"value": [0-9.]*' gpurun_out/ov_$arm.log) $(grep -o '"gfxclk_mhz": {[^}]*}' gpurun_out/ov_$arm.log) $(grep -o '"power_limited_pct": [0-9.]*' gpurun_out/ov_$arm.log)"
 done
+for arm in off on; do
+  timeout -k 10 300 python -u bench.py --config gpt2_xl --steps 10 --warmup 3 --no-bubble --opt-overlap $arm > gpurun_out/ovg_$arm.log 2>&1 || { tail -20 gpurun_out/ovg_$arm.log; exit 1; }
+  echo "gpt2_xl opt-overlap $arm: $(grep -o '"value": [0-9.]*' gpurun_out/ovg_$arm.log)"
+done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ov -o run -- python3 bench.py --steps 4 --warmup 2 --no-bubble --opt-overlap on > gpurun_out/prof_ov.log 2>&1 || { tail -5 gpurun_out/prof_ov.log; exit 1; }
 python3 tools/prof_summary.py gpurun_out/prof_ov/run_results.db 30 --by-grid > gpurun_out/prof_ov.txt 2>&1
+python3 tools/overlap_share.py gpurun_out/prof_ov/run_results.db adam >> gpurun_out/prof_ov.txt 2>&1
+tail -2 gpurun_out/prof_ov.txt
 rm -rf gpurun_out/prof_ov
 head -20 gpurun_out/prof_ov.txt
