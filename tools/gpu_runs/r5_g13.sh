@@ -21,3 +21,7 @@ python3 tools/overlap_share.py gpurun_out/prof_ov/run_results.db adam >> gpurun_
 tail -2 gpurun_out/prof_ov.txt
 rm -rf gpurun_out/prof_ov
 head -20 gpurun_out/prof_ov.txt
+# GPT-2-XL PP=8: the default plan vs the best alternative, 3 alternating repeats (noise of the plan table)
+export MIPIPE_CALIB_DIR="$GRAFT_REPO_ROOT/gpurun_out/calib"
+timeout -k 10 420 python -u tools/plan_table.py --config gpt2_xl --labels DEFAULT,analytic/makespan/v=4 --repeats 3 > gpurun_out/plan_repeat_gpt2_xl.txt 2>&1 || { tail -30 gpurun_out/plan_repeat_gpt2_xl.txt; exit 1; }
+grep "^   walls\|^## plan" gpurun_out/plan_repeat_gpt2_xl.txt | cut -c1-200

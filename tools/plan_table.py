@@ -68,6 +68,10 @@ def main() -> int:
     ap.add_argument("--pp", type=int, default=8)
     ap.add_argument("--v", default="1,2,3,4", help="chunks per rank to try")
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--labels", default=None,
+                    help="comma list of plan labels (e.g. DEFAULT,analytic/makespan/v=4): emulate only those plans, "
+                         "--repeats times each, alternating (run-to-run noise of the comparison)")
+    ap.add_argument("--repeats", type=int, default=1)
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     m, mb, ckpt = CONFIG[args.config]
@@ -107,8 +111,12 @@ def main() -> int:
                     continue
                 add(f"{kind}/{obj}/v={v}", vv, pv)
     print(f"# {len(plans)} distinct plans", flush=True)
+    todo = list(plans.items())
+    if args.labels:
+        want = set(args.labels.split(","))
+        todo = [kv for kv in todo if want & set(kv[1][1])] * args.repeats
     rows = []
-    for (v, split, bal), (plan, labels) in plans.items():
+    for (v, split, bal), (plan, labels) in todo:
         print(f"## plan v={v} split={split} balance={list(bal)}: {', '.join(labels)}", flush=True)
         walls = []
         for r in range(pp):
@@ -127,6 +135,8 @@ def main() -> int:
         print(f"  {tps:10,.0f} {t:8.1f} {100 * bub:6.1f}% {v:2d} {str(split):>5s} {lo:7.1f}-{hi:7.1f}  "
               f"{', '.join(labels)}")
     best = rows[0]
+    if args.labels:
+        return 0
     default = next(r for r in rows if "DEFAULT" in r[7])
     print(f"# default plan: {default[0]:,.0f} tok/s = {100 * default[0] / best[0]:.1f} % of the best "
           f"({', '.join(best[7])})")
