@@ -2,7 +2,8 @@
 each rank emulated on ONE MI355X.
 
 For a BASELINE config (#3: enc12_d4096, chunks 32, micro-batch 64 -- the
-bench's --- 'except_last'; #4: GPT-2-XL, chunks 8, micro-batch 18, 'always'),
+bench's default -- 'except_last'; #4: GPT-2-XL, chunks 8, micro-batch 18,
+'always'),
 the plans are: unit costs {analytic FLOPs, measured engine-context costs} x
 objective {makespan, balance} x chunks per rank v (the decoder split chosen per
 v by the same simulation the planner uses), plus the plan ``bench.py``
