@@ -343,20 +343,29 @@ class _Overlap:
             for p, ci in zip(g.params, owner):
                 chunk_of[id(p)] = (gi, ci)
             self.chunks.append(chunks)
-        # module -> the (group, chunk) its forward must wait for: the latest chunk of its direct parameters
+        # module -> the (group, chunk) its forward must wait for: the latest chunk holding a parameter of its
+        # SUBTREE (a block may run a child through another method than __call__ -- e.g. forward_fanout -- so
+        # the child's own hook would not fire); for the given root modules only their direct parameters (a
+        # root's subtree is the whole stage: its children's hooks give the per-unit granularity)
         self.need: Dict[int, Dict[int, int]] = {}
         self.hooks = []
-        for top in modules:
-            for mod in top.modules():
-                direct = [p for p in mod.parameters(recurse=False) if id(p) in chunk_of]
-                if not direct or id(mod) in self.need:
-                    continue
-                need: Dict[int, int] = {}
-                for p in direct:
+
+        def need_of(params) -> Dict[int, int]:
+            need: Dict[int, int] = {}
+            for p in params:
+                if id(p) in chunk_of:
                     gi, ci = chunk_of[id(p)]
                     need[gi] = max(need.get(gi, -1), ci)
-                self.need[id(mod)] = need
-                self.hooks.append(mod.register_forward_pre_hook(self._hook))
+            return need
+
+        for top in modules:
+            for mod in top.modules():
+                if id(mod) in self.need:
+                    continue
+                need = need_of(mod.parameters(recurse=mod is not top))
+                if need:
+                    self.need[id(mod)] = need
+                    self.hooks.append(mod.register_forward_pre_hook(self._hook))
         # one event per chunk, re-recorded every step (a wait binds to the record before it)
         self.events = [[torch.cuda.Event() for _ in chunks] for chunks in self.chunks]
         self.pending: Dict[int, Dict[int, int]] = {}  # modules still to wait this step

@@ -50,17 +50,37 @@ def _train(overlap: bool, checkpoint: str, steps: int = 4):
             [t.clone() for grp in state["groups"] for t in grp.values()], opt, model)
 
 
+def _embedding_range(opt, model):
+    """Flat-buffer range of the embedding table: its gradient is summed with float atomics (embed_bwd_kernel),
+    so its last bits depend on the order the atomics land in -- between two SERIAL runs too."""
+    emb = next(m for m in model.modules() if type(m).__name__ == "Encoder")
+    off = 0
+    for p in opt.groups[0].params:
+        if p is emb.weight:
+            return off, off + p.numel()
+        off += p.numel()
+    raise AssertionError("no embedding parameter")
+
+
+def _same(a, b, rng):
+    lo, hi = rng
+    ok = torch.equal(a[:lo], b[:lo]) and torch.equal(a[hi:], b[hi:])
+    return ok and torch.allclose(a[lo:hi], b[lo:hi], rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize("checkpoint", ["never", "except_last"])
 def test_overlapped_step_bit_identical(monkeypatch, checkpoint):
+    """Bit-identical everywhere but the embedding table (atomics), which matches to rounding."""
     monkeypatch.setattr(_Overlap, "MIN_CHUNK", 4096)  # many chunks at this size
     l0, p0, s0, *_ = _train(False, checkpoint)
-    l1, p1, s1, opt, _ = _train(True, checkpoint)
+    l1, p1, s1, opt, model = _train(True, checkpoint)
     assert len(opt._overlap.chunks[0]) > 8, opt._overlap.chunks
     assert l0 == l1
     for a, b in zip(p0, p1):
         assert torch.equal(a, b)
-    for a, b in zip(s0, s1):
-        assert torch.equal(a, b)
+    rng = _embedding_range(opt, model)
+    for a, b in zip(s0, s1):  # master, exp_avg, exp_avg_sq: flat buffers
+        assert _same(a, b, rng)
 
 
 def test_overlap_chunks_cover_the_buffer_in_forward_order(monkeypatch):
@@ -83,7 +103,7 @@ def test_overlap_chunks_cover_the_buffer_in_forward_order(monkeypatch):
         if id(mod) not in opt._overlap.need:
             continue
         need = opt._overlap.need[id(mod)][0]
-        for p in mod.parameters(recurse=False):
+        for p in mod.parameters(recurse=mod is not model):  # a block's hook covers its whole subtree
             a, b = off[id(p)]
             if a >= g.n_lazy:
                 assert need >= 0

@@ -39,8 +39,15 @@ from mipipe.parallel.stage import choose_virtual, simulate_step  # noqa: E402
 from mipipe.pipeline import checkpoint_stop_for  # noqa: E402
 from pp_rank_emulation import run_rank  # noqa: E402
 
-# BASELINE.json's PP=8 configs at the bench's defaults (bench.py: chunks, _default_micro_batch, checkpoint auto)
+# the bench's defaults per model and PP (bench.py: chunks, _default_micro_batch, checkpoint 'auto'): BASELINE
+# config #2 (enc12, chunks 4 x PP, 'never'), #3 (its PP=8 run: 'except_last'), #4 (GPT-2-XL, chunks 8 at PP=8)
 CONFIG = {"enc12_d4096": (32, 64, "except_last"), "gpt2_xl": (8, 18, "always")}
+
+
+def bench_defaults(name: str, pp: int):
+    if name == "gpt2_xl":
+        return (8 if pp == 8 else 4 * pp), 18, "always"
+    return 4 * pp, 64, ("except_last" if pp == 8 else "never")
 HOP_MS = 0.15
 XGMI_BYTES_PER_S = 100e9
 
@@ -75,9 +82,9 @@ def main() -> int:
     ap.add_argument("--repeats", type=int, default=1)
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
-    m, mb, ckpt = CONFIG[args.config]
-    args.chunks, args.micro_batch, args.checkpoint = m, mb, ckpt
     pp = args.pp
+    m, mb, ckpt = bench_defaults(args.config, pp)
+    args.chunks, args.micro_batch, args.checkpoint = m, mb, ckpt
     dev = torch.device("cuda", 0)
     bwd_ratio = 2.0 + {"never": 0.0, "except_last": (m - 1) / m, "always": 1.0}[ckpt]
     t0 = time.perf_counter()
