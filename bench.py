@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--plan-objective", default="makespan", choices=["makespan", "balance"],
                     help="stage plan: shortest simulated step (may load ranks unevenly to shorten fill / drain) "
                          "or the most even per-rank work")
+    ap.add_argument("--plan-select", default="auto", choices=["auto", "emulate", "model"],
+                    help="final pick of the stage plan: emulate = the few best plans of the cost model are each run "
+                         "on every rank alone (loop-back engine, a few steps) and the fastest by measured walls "
+                         "wins (mipipe.parallel.calibrate.select_plan_by_emulation; profiles/plan_table_r5.txt); "
+                         "model = the cost model's choice.  auto = emulate with measured costs on GPUs at PP > 1")
     ap.add_argument("--split-decoder", default="auto", choices=["auto", "on", "off"],
                     help="cut the LM head along the vocabulary into two pipeline units")
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
@@ -195,6 +200,8 @@ def main() -> int:
     plan_mode = args.plan if args.plan != "auto" else ("measured" if on_gpu and pp > 1 and not args.shared_gpu
                                                        else "analytic")
     cost_fn = None
+    unit_ms = None
+    plan_report = None
     if plan_mode == "measured" and pp > 1:
         from mipipe.parallel.calibrate import CalibrationError, calibrated_costs, engine_unit_costs
 
@@ -211,6 +218,26 @@ def main() -> int:
         split = splits[-1] and pp > 1
         plan = plan_stages(cfg, pp, virtual, m, split_decoder=split, bwd_ratio=bwd_ratio,
                            costs=cost_fn(split) if cost_fn is not None else None, objective=args.plan_objective)
+    select = args.plan_select
+    if select == "auto":
+        select = "emulate" if (cost_fn is not None and args.virtual == "auto" and args.skips == "none"
+                               and args.plan_objective == "makespan") else "model"
+    if select == "emulate" and pp > 1:
+        if cost_fn is None:
+            raise SystemExit("--plan-select emulate needs measured costs (--plan measured, on GPUs)")
+        from mipipe.parallel.calibrate import select_plan_by_emulation
+        from mipipe.parallel.stage import candidate_plans
+
+        cands = candidate_plans(cfg, pp, m, bwd_ratio, mb, cost_fn, split_options=splits)
+        if len(cands) > 1:
+            plan, plan_report = select_plan_by_emulation(cfg, cands, prank, m, mb, args.checkpoint, unit_ms,
+                                                         device=device, dtype=dtype, replica=replica)
+            virtual = plan.virtual
+        else:
+            plan, virtual = cands[0], cands[0].virtual
+            plan_report = {"method": "one candidate within 6 % of the model's best: no emulation needed",
+                           "candidates": [{"v": plan.virtual, "split_decoder": plan.split_decoder,
+                                           "balance": list(plan.balance)}], "chosen": 0}
     torch.manual_seed(1234 + prank)  # same initial weights in every data-parallel replica
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     from mipipe.models.long_skip import unet_pairs
@@ -404,6 +431,7 @@ def main() -> int:
                 "balance": plan.balance,
                 "stage_imbalance": round(plan.imbalance(), 3),
                 "plan_costs": "measured (engine-context unit costs)" if cost_fn is not None else "analytic FLOPs",
+                "plan_selection": plan_report,
             },
             "bubble_pct": None if bubble is None else round(bubble, 2),
             "work_note": (f"checkpoint={args.checkpoint!r} re-runs the forward of {stop_n} of {m} micro-batches: "

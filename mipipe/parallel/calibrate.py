@@ -392,3 +392,113 @@ def calibrated_costs(cfg: LMConfig, micro_batch: int, chunks: int, checkpoint: s
         except OSError:
             pass
     return costs
+
+
+def emulate_rank_ms(cfg: LMConfig, plan, rank: int, chunks: int, micro_batch: int, checkpoint: str, *,
+                    device: torch.device, dtype: torch.dtype = torch.bfloat16, steps: int = 2) -> float:
+    """Median wall (ms) of one training step of pipeline rank ``rank`` of
+    ``plan`` run alone: its virtual stages through the real PipelineEngine over
+    :class:`Loopback` channels, deferred weight gradients, grad-norm and Adam
+    included -- the GPU runs exactly that rank's kernels in its schedule."""
+    from .. import ops
+    from ..optim import FlatAdam
+    from .engine import PipelineEngine
+    from .stage import build_stage, stage_input_shape
+
+    device = torch.device(device)
+    pp = plan.ranks
+    vss = plan.vstages(rank)
+    stages = [build_stage(cfg, plan, vs, device=device, dtype=dtype).train() for vs in vss]
+    opt = FlatAdam([p for s in stages for p in s.parameters()], lr=1e-6, max_grad_norm=1.0)
+    last = any(vs == pp * plan.virtual - 1 for vs in vss)
+    S, V = cfg.seq_len, cfg.vocab
+
+    def loss_fn(y, t):
+        return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
+
+    engine = PipelineEngine(stages, chunks=chunks, checkpoint=checkpoint,
+                            act_shape=[stage_input_shape(cfg, plan, vs, micro_batch) for vs in vss], act_dtype=dtype,
+                            loss_fn=loss_fn if last else None, group=Loopback(rank, pp), device=device,
+                            skip_routes={})
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    tokens = torch.randint(0, V, (chunks, micro_batch, S + 1), generator=g)
+    inputs = [tokens[i, :, :S].to(device) for i in range(chunks)] if rank == 0 else None
+    targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(chunks)]
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    def step():
+        opt.zero_grad()
+        engine.step(inputs, targets)
+        opt.step(opt.grad_sumsq())
+
+    step()
+    walls = []
+    for _ in range(steps):
+        sync()
+        t0 = time.perf_counter()
+        step()
+        sync()
+        walls.append((time.perf_counter() - t0) * 1e3)
+    del engine, opt, stages
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    return sorted(walls)[len(walls) // 2]
+
+
+def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int, micro_batch: int,
+                             checkpoint: str, unit_ms: Dict[str, float], *, device: torch.device,
+                             dtype: torch.dtype = torch.bfloat16, replica: int = 0, group=None,
+                             steps: int = 2, emulate=None):
+    """Picks the fastest of ``candidates`` (:func:`~mipipe.parallel.stage.candidate_plans`)
+    from MEASURED walls: every pipeline rank emulates its own rank of every
+    candidate at once (:func:`emulate_rank_ms`, replica 0 only under data
+    parallelism), ONE all-reduce gathers the [candidate x rank] wall matrix,
+    and each candidate's job step is simulated from its walls
+    (:func:`~mipipe.parallel.stage.simulate_from_walls`, IPC hop).  Identical
+    on every rank.  Returns ``(plan, report)``; if any rank's emulation fails,
+    every rank returns the model's first candidate (report says why).
+    ``emulate(plan, prank) -> ms``: test hook."""
+    from ..pipeline import checkpoint_stop_for
+    from .stage import HOP_BYTES_PER_S, HOP_LATENCY_MS, simulate_from_walls
+
+    device = torch.device(device)
+    k = len(candidates)
+    pp = candidates[0].ranks
+    emulate = emulate or (lambda plan, r: emulate_rank_ms(cfg, plan, r, chunks, micro_batch, checkpoint,
+                                                          device=device, dtype=dtype, steps=steps))
+    walls = torch.zeros(k * pp + 1, dtype=torch.float64)
+    err = None
+    if replica == 0:
+        try:
+            for i, plan in enumerate(candidates):
+                walls[i * pp + prank] = float(emulate(plan, prank))
+        except Exception as exc:  # noqa: BLE001 -- reported on every rank below, identically
+            err = exc
+            walls[-1] = 1.0
+    distributed = dist.is_available() and dist.is_initialized()
+    if distributed:
+        nccl = dist.get_backend(group) == "nccl"
+        w = walls.to(device) if nccl else walls
+        dist.all_reduce(w, group=group)  # ONE collective whatever happened locally
+        walls = w.cpu()
+    report = {"method": "emulated rank walls (loop-back engine), IPC hop", "candidates": []}
+    if walls[-1] > 0:
+        report["method"] = "model (emulation failed" + (f": {err!r}" if err is not None else " on another rank") + ")"
+        return candidates[0], report
+    stop = checkpoint_stop_for(checkpoint, chunks)
+    hop = HOP_LATENCY_MS + micro_batch * cfg.seq_len * cfg.d_model * 2 / HOP_BYTES_PER_S * 1e3
+    best = None
+    for i, plan in enumerate(candidates):
+        w = walls[i * pp:(i + 1) * pp].tolist()
+        costs = engine_unit_costs(cfg, unit_ms, plan.split_decoder)
+        t, bub = simulate_from_walls(plan, w, costs, chunks, stop, hop)
+        report["candidates"].append({"v": plan.virtual, "split_decoder": plan.split_decoder,
+                                     "balance": list(plan.balance), "rank_walls_ms": [round(x, 1) for x in w],
+                                     "step_ms": round(t, 1), "bubble": round(bub, 3)})
+        if best is None or t < best[0]:
+            best = (t, i)
+    report["chosen"] = best[1]
+    return candidates[best[1]], report

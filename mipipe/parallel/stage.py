@@ -503,3 +503,66 @@ def choose_virtual(cfg: LMConfig, stages: int, chunks: int, candidates: Optional
         if best is None or t < best[0] * 0.995 or (t <= best[0] * 1.005 and key < best[3]):
             best = (t, v, plan, key)
     return best[1], best[2]
+
+
+# Stage-transport hop used to rank plans from measured rank walls: the IPC link's cross-stream event latency plus the
+# message at an assumed 100 GB/s of xGMI copy bandwidth (profiles/pp8_transport_prediction_r5.txt).
+HOP_LATENCY_MS = 0.15
+HOP_BYTES_PER_S = 100e9
+
+
+def simulate_from_walls(plan: StagePlan, walls: Sequence[float], costs: Sequence[float], chunks: int,
+                        checkpoint_stop: int, hop_ms: float) -> Tuple[float, float]:
+    """(step ms, mean bubble) of ``plan`` from MEASURED per-rank step walls
+    (e.g. each rank emulated over loop-back channels): each rank's wall is split
+    over its virtual stages in proportion to their unit ``costs``, per
+    micro-batch, recompute stripped (the simulation adds it back explicitly),
+    weight gradients deferred; ``hop_ms`` per stage-boundary message.  Unlike
+    the unit-cost model this carries every cost a rank really pays for its cut
+    positions and chunk count (profiles/plan_table_r5.txt)."""
+    pp, v = plan.ranks, plan.virtual
+    rec = checkpoint_stop / chunks
+    per = []
+    for g in range(pp * v):
+        r = g % pp
+        mine = sum(costs[i] for i in plan.slice(g))
+        total = sum(sum(costs[i] for i in plan.slice(s)) for s in plan.vstages(r)) or 1.0
+        per.append(walls[r] * mine / total / chunks / (3.0 + rec) * 3.0)
+    t, busy = simulate_step(per, pp, v, chunks, 2.0, deferred_w=1.0 / 3.0, checkpoint_stop=checkpoint_stop,
+                            transfer=hop_ms)
+    return t, 1.0 - sum(busy) / len(busy) / t
+
+
+def candidate_plans(cfg: LMConfig, stages: int, chunks: int, bwd_ratio: float, micro_batch: Optional[int],
+                    cost_fn, split_options: Sequence[bool] = (False, True), max_candidates: int = 6,
+                    within: float = 0.06, max_virtual: int = 6) -> List[StagePlan]:
+    """The plans worth measuring: for every v up to ``max_virtual`` the makespan
+    plan from the measured costs (``cost_fn``) and from the analytic ones, kept
+    when the measured-cost simulation puts them within ``within`` of the best,
+    best first, at most ``max_candidates``.  The unit-cost model ranks plans only
+    to ~2-3 % (the cut positions and chunk count cost what it does not see), so
+    the final pick among these is made from emulated rank walls
+    (:func:`mipipe.parallel.calibrate.select_plan_by_emulation`)."""
+    transfer, launch = boundary_terms(cfg, micro_batch, "ms" if cost_fn is not None else "flop")
+    units = len(block_costs(cfg, False))
+    seen, scored = set(), []
+    for v in range(1, max(1, min(max_virtual, units // stages)) + 1):
+        for fn in ((cost_fn, None) if cost_fn is not None else (None,)):
+            try:
+                vv, plan = choose_virtual(cfg, stages, chunks, candidates=[v], split_options=split_options,
+                                          bwd_ratio=bwd_ratio, micro_batch=micro_batch, cost_fn=fn)
+            except (TypeError, ValueError):
+                continue
+            key = (vv, plan.split_decoder, tuple(plan.balance))
+            if key in seen:
+                continue
+            seen.add(key)
+            # score every candidate under the same (measured, when given) costs
+            costs = cost_fn(plan.split_decoder) if cost_fn is not None else block_costs(cfg, plan.split_decoder)
+            p = StagePlan(list(plan.balance), costs, vv, plan.split_decoder)
+            t = simulate_step([p.stage_cost(g) for g in range(stages * vv)], stages, vv, chunks, bwd_ratio,
+                              deferred_w=1.0 / bwd_ratio, transfer=transfer, launch=launch)[0]
+            scored.append((t, len(scored), p))
+    scored.sort(key=lambda x: (x[0], x[1]))
+    best = scored[0][0]
+    return [p for t, _, p in scored if t <= best * (1.0 + within)][:max_candidates]

@@ -105,6 +105,8 @@ class GpuTelemetry:
             "power": _num(m.get("current_socket_power")),
             "hotspot": _num(m.get("temperature_hotspot")),
             "mem": _num(m.get("temperature_mem")),
+            "uclk": _num(m.get("current_uclk")),  # HBM clock
+            "fclk": _num(m.get("current_fclk")),  # data-fabric clock (absent on some firmware tables)
         }
 
     def _loop(self) -> None:
@@ -144,6 +146,10 @@ class GpuTelemetry:
         out["socket_power_w"] = _stats([x["power"] for x in s], 0)
         out["hotspot_c"] = _stats([x["hotspot"] for x in s], 0)
         out["hbm_c"] = _stats([x["mem"] for x in s], 0)
+        for key, name in (("uclk", "uclk_mhz"), ("fclk", "fclk_mhz")):
+            st = _stats([x[key] for x in s], 0)
+            if st is not None:
+                out[name] = st
         try:
             m1 = self._metrics()
             m0 = self._m0 or {}

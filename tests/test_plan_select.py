@@ -1,0 +1,115 @@
+"""Plan selection from emulated rank walls (mipipe.parallel.calibrate.select_plan_by_emulation,
+stage.candidate_plans / simulate_from_walls): the unit-cost model ranks plans only to ~2-3 %, so
+bench.py measures its few best candidates on every rank at once and keeps the fastest
+(profiles/plan_table_r5.txt).  CPU: real emulation of a tiny model, and a 2-rank gloo group
+that must agree on the pick -- or fall back together when one rank's emulation fails."""
+import dataclasses
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mipipe.models import CONFIGS
+from mipipe.parallel.calibrate import engine_unit_costs, emulate_rank_ms, select_plan_by_emulation, unit_kinds
+from mipipe.parallel.stage import (StagePlan, block_costs, candidate_plans, plan_stages, simulate_from_walls,
+                                   simulate_step)
+
+CPU = torch.device("cpu")
+
+
+def _cfg():
+    return dataclasses.replace(CONFIGS["tiny"], num_layers=4)
+
+
+def _unit_ms(cfg):
+    base = {"enc": 0.2, "core": 2.0, "out": 0.8, "mlp_in": 0.8, "mlp_out": 0.8, "norm": 0.1, "dec": 3.0,
+            "dec_head": 1.5, "dec_tail": 1.5}
+    return {k: base[k] for k in set(unit_kinds(cfg, False)) | set(unit_kinds(cfg, True))}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_simulate_from_walls_equal_walls_is_the_cost_simulation():
+    """Walls proportional to the unit costs reproduce the unit-cost simulation."""
+    cfg = _cfg()
+    costs = engine_unit_costs(cfg, _unit_ms(cfg), False)
+    plan = plan_stages(cfg, 2, 2, 8, False, costs=costs)
+    m = 8
+    walls = [plan.rank_cost(r) * m for r in range(2)]  # ms per step = per-micro-batch cost x chunks
+    t, _ = simulate_from_walls(plan, walls, costs, m, 0, 0.0)
+    t_ref, _ = simulate_step([plan.stage_cost(g) for g in range(4)], 2, 2, m, 2.0, deferred_w=1.0 / 3.0,
+                             checkpoint_stop=0)
+    assert abs(t - t_ref) < 1e-6 * t_ref
+
+
+def test_candidate_plans_are_valid_and_ranked():
+    cfg = _cfg()
+    um = _unit_ms(cfg)
+    cands = candidate_plans(cfg, 2, 8, 2.0, 2, lambda s: engine_unit_costs(cfg, um, s))
+    assert 1 <= len(cands) <= 6
+    for p in cands:
+        assert sum(p.balance) == len(block_costs(cfg, p.split_decoder))
+        assert p.ranks == 2 and all(k >= 1 for k in p.balance)
+    assert len({(p.virtual, p.split_decoder, tuple(p.balance)) for p in cands}) == len(cands)
+
+
+def test_emulate_rank_ms_cpu():
+    cfg = _cfg()
+    plan = plan_stages(cfg, 2, 1, 2, False)
+    for r in range(2):
+        assert emulate_rank_ms(cfg, plan, r, 2, 2, "never", device=CPU, dtype=torch.float32, steps=1) > 0
+
+
+def _worker(rank, port, q, fail):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        cfg = _cfg()
+        um = _unit_ms(cfg)
+        costs = engine_unit_costs(cfg, um, False)
+        cands = [StagePlan(b, costs, 1, False) for b in ([9, 9], [8, 10], [10, 8])]
+
+        def emulate(plan, r):  # candidate [8, 10] is the fastest; rank 1 fails when asked to
+            if fail and r == 1:
+                raise RuntimeError("boom")
+            return {(9, 9): 100.0, (8, 10): 80.0, (10, 8): 120.0}[tuple(plan.balance)] + r
+
+        plan, rep = select_plan_by_emulation(cfg, cands, rank, 8, 2, "never", um, device=CPU, emulate=emulate)
+        q.put((rank, list(plan.balance), rep["method"], len(rep["candidates"])))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fail):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q, fail)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, rest) for r, *rest in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_select_plan_by_emulation_agrees_across_ranks():
+    res = _run(False)
+    assert res[0] == res[1]
+    assert res[0][0] == [8, 10] and res[0][1].startswith("emulated") and res[0][2] == 3
+
+
+def test_select_plan_falls_back_together_when_a_rank_fails():
+    res = _run(True)
+    assert res[0][0] == res[1][0] == [9, 9]  # the model's first candidate on both ranks
+    assert all(r[1].startswith("model (emulation failed") and r[2] == 0 for r in res.values())
+    assert "boom" in res[1][1]

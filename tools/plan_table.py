@@ -35,7 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 from mipipe.models import CONFIGS  # noqa: E402
 from mipipe.parallel.calibrate import calibrated_costs, engine_unit_costs  # noqa: E402
-from mipipe.parallel.stage import choose_virtual, simulate_step  # noqa: E402
+from mipipe.parallel.stage import candidate_plans, choose_virtual, simulate_from_walls  # noqa: E402
 from mipipe.pipeline import checkpoint_stop_for  # noqa: E402
 from pp_rank_emulation import run_rank  # noqa: E402
 
@@ -53,21 +53,10 @@ XGMI_BYTES_PER_S = 100e9
 
 
 def job_step_ms(cfg, plan, walls, unit_ms, m, mb, ckpt):
-    """Simulated PP step from measured rank walls (see the module doc)."""
-    pp, v = plan.ranks, plan.virtual
-    costs = engine_unit_costs(cfg, unit_ms, plan.split_decoder)
-    stop = checkpoint_stop_for(ckpt, m)
-    rec = stop / m
-    per = []
-    for g in range(pp * v):
-        r = g % pp
-        mine = sum(costs[i] for i in plan.slice(g))
-        total = sum(sum(costs[i] for i in plan.slice(s)) for s in plan.vstages(r))
-        # this vstage's share of the rank's wall, per micro-batch, recompute stripped (simulate_step adds it)
-        per.append(walls[r] * mine / total / m / (3.0 + rec) * 3.0)
+    """Simulated PP step from measured rank walls (stage.simulate_from_walls, as the bench's pick)."""
     hop = HOP_MS + mb * cfg.seq_len * cfg.d_model * 2 / XGMI_BYTES_PER_S * 1e3
-    t, busy = simulate_step(per, pp, v, m, 2.0, deferred_w=1.0 / 3.0, checkpoint_stop=stop, transfer=hop)
-    return t, 1.0 - sum(busy) / len(busy) / t
+    return simulate_from_walls(plan, walls, engine_unit_costs(cfg, unit_ms, plan.split_decoder), m,
+                               checkpoint_stop_for(ckpt, m), hop)
 
 
 def main() -> int:
@@ -102,10 +91,14 @@ def main() -> int:
         key = (v, plan.split_decoder, tuple(plan.balance))
         plans.setdefault(key, (plan, []))[1].append(label)
 
-    # the bench's default at PP > 1 on GPUs: measured costs, makespan, v and split by simulated step
+    # the bench's default at PP > 1 on GPUs: the cost model's few best plans (stage.candidate_plans), the pick made
+    # from their emulated rank walls (calibrate.select_plan_by_emulation) -- i.e. the best of the "candidate" rows
+    for cp in candidate_plans(cfg, pp, m, bwd_ratio, mb, cost_fn_for("measured")):
+        add("candidate", cp.virtual, cp)
+    # the cost model alone (round 4's default, before the emulated pick)
     v0, p0 = choose_virtual(cfg, pp, m, bwd_ratio=bwd_ratio, micro_batch=mb, cost_fn=cost_fn_for("measured"),
                             objective="makespan")
-    add("DEFAULT", v0, p0)
+    add("model-default", v0, p0)
     for kind in ("analytic", "measured"):
         for obj in ("makespan", "balance"):
             va, pa = choose_virtual(cfg, pp, m, bwd_ratio=bwd_ratio, micro_batch=mb, cost_fn=cost_fn_for(kind),
@@ -145,9 +138,10 @@ def main() -> int:
     best = rows[0]
     if args.labels:
         return 0
-    default = next(r for r in rows if "DEFAULT" in r[7])
-    print(f"# default plan: {default[0]:,.0f} tok/s = {100 * default[0] / best[0]:.1f} % of the best "
-          f"({', '.join(best[7])})")
+    default = next(r for r in rows if "candidate" in r[7])  # rows are sorted: the emulated pick
+    model = next(r for r in rows if "model-default" in r[7])
+    print(f"# bench default (best emulated candidate): {default[0]:,.0f} tok/s = {100 * default[0] / best[0]:.1f} % "
+          f"of the best ({', '.join(best[7])}); the cost model's own pick: {100 * model[0] / best[0]:.1f} %")
     return 0
 
 
