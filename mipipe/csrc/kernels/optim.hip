@@ -156,7 +156,13 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
 // stride vectors of one block-sized tile; 4U loads in flight, then the math
 // and the stores.  The default (adam_set_variant(1)): 7.24 vs 8.01 ms for the
 // 1.44B-parameter enc12 group, 5.99 vs 5.41 TB/s at 30 B/param (tools/adam_ab.py).
-template <typename M, int U>
+__device__ __forceinline__ void nt_store(float4* p, const float4 v) {
+  f32x4 x;
+  x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
+}
+
+template <typename M, int U, bool NTS = false>
 __global__ void __launch_bounds__(256) adam_tile_kernel(float* __restrict__ master, M* __restrict__ model,
                                                         const float* __restrict__ grad, float* __restrict__ m,
                                                         float* __restrict__ v, int64_t n, AdamHyper h,
@@ -192,14 +198,21 @@ __global__ void __launch_bounds__(256) adam_tile_kernel(float* __restrict__ mast
     adam_one(p[u].y, g[u].y, mm[u].y, vv[u].y, h, c);
     adam_one(p[u].z, g[u].z, mm[u].z, vv[u].z, h, c);
     adam_one(p[u].w, g[u].w, mm[u].w, vv[u].w, h, c);
-    P[i] = p[u];
-    Mo[i] = mm[u];
-    V[i] = vv[u];
+    if constexpr (NTS) {
+      nt_store(P + i, p[u]);
+      nt_store(Mo + i, mm[u]);
+      nt_store(V + i, vv[u]);
+    } else {
+      P[i] = p[u];
+      Mo[i] = mm[u];
+      V[i] = vv[u];
+    }
     if (model != nullptr) {
       if constexpr (sizeof(M) == 2) {
         bf16x4 o;
         o[0] = (__bf16)p[u].x; o[1] = (__bf16)p[u].y; o[2] = (__bf16)p[u].z; o[3] = (__bf16)p[u].w;
-        *reinterpret_cast<bf16x4*>(model + 4 * i) = o;
+        if constexpr (NTS) __builtin_nontemporal_store(o, reinterpret_cast<bf16x4*>(model + 4 * i));
+        else *reinterpret_cast<bf16x4*>(model + 4 * i) = o;
       } else {
         reinterpret_cast<float4*>(model)[i] = p[u];
       }
@@ -242,11 +255,15 @@ template <typename M>
 void adam_step(float* master, M* model, const float* grad, float* m, float* v, int64_t n, const AdamHyper& h,
                const float* sumsq_ptr, hipStream_t s) {
   if (n == 0) return;
-  if (g_adam_variant == 1 && n >= 4) {
+  if ((g_adam_variant == 1 || g_adam_variant == 2) && n >= 4) {
     constexpr int U = 4;
     const int64_t tiles = (n / 4 + 256 * U - 1) / (256 * U);
-    hipLaunchKernelGGL((adam_tile_kernel<M, U>), dim3((unsigned)tiles), dim3(256), 0, s, master, model, grad, m, v,
-                       n, h, sumsq_ptr);
+    if (g_adam_variant == 2)  // streaming (nt) stores too: A/B (tools/adam_ab.py)
+      hipLaunchKernelGGL((adam_tile_kernel<M, U, true>), dim3((unsigned)tiles), dim3(256), 0, s, master, model, grad,
+                         m, v, n, h, sumsq_ptr);
+    else
+      hipLaunchKernelGGL((adam_tile_kernel<M, U>), dim3((unsigned)tiles), dim3(256), 0, s, master, model, grad, m, v,
+                         n, h, sumsq_ptr);
     return;
   }
   int64_t blocks = (n / 4 + 255) / 256;

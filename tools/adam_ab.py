@@ -41,13 +41,30 @@ def timeit(iters=10):
 
 for _ in range(5):
     run()
-res = {0: [], 1: []}
-for rnd in range(4):
-    for var in (0, 1, 1, 0):
+VARIANTS = {0: "grid-stride loop", 1: "one tile per block (default)", 2: "one tile per block, streaming stores"}
+res = {v_: [] for v_ in VARIANTS}
+for rnd in range(3):
+    for var in (0, 1, 2, 2, 1, 0):
         k.adam_set_variant(var)
         res[var].append(timeit())
 gb = 30.0 * n / 1e9
 for var, ts in res.items():
     t = min(ts)
-    print(f"variant {var}: {t:7.3f} ms (median {statistics.median(ts):.3f})  {gb / t:6.2f} TB/s at 30 B/param")
-k.adam_set_variant(0)
+    print(f"variant {var} ({VARIANTS[var]}): {t:7.3f} ms (median {statistics.median(ts):.3f})  {gb / t:6.2f} TB/s "
+          f"at 30 B/param", flush=True)
+k.adam_set_variant(1)
+# the same HBM read / write mix without the math: 16 B read + 14 B written per parameter (grad, master, moments in;
+# master, moments, bf16 model out) vs a plain copy (read 1, write 1)
+del m, v
+a = torch.empty(n // 2, device=dev)
+b = torch.empty_like(a)
+ts = []
+for _ in range(10):
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    b.copy_(a)
+    e_.record()
+    e_.synchronize()
+    ts.append(s_.elapsed_time(e_))
+t = min(ts)
+print(f"torch copy_ {a.numel() * 4 / 1e9:.1f} GB -> {a.numel() * 8 / 1e9 / t:.2f} TB/s (read + write)", flush=True)
