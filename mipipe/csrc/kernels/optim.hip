@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ master, M
 
 // One-shot variant (no grid-stride loop): each thread owns U consecutive-by-
 // stride vectors of one block-sized tile; 4U loads in flight, then the math
-// and the stores.  The default (adam_set_variant(1)): 7.24 vs 8.01 ms for the
+// and the stores.  adam_set_variant(1) (round 3): 7.24 vs 8.01 ms for the
 // 1.44B-parameter enc12 group, 5.99 vs 5.41 TB/s at 30 B/param (tools/adam_ab.py).
 __device__ __forceinline__ void nt_store(float4* p, const float4 v) {
   f32x4 x;
@@ -230,7 +230,10 @@ __global__ void __launch_bounds__(256) adam_tile_kernel(float* __restrict__ mast
   }
 }
 
-int g_adam_variant = 1;
+// 2 (default since round 5): the tile kernel with streaming (nt) stores as well -- 6.80 vs 7.06 ms for the
+// 1.44B-parameter enc12 group on one box, 6.37 vs 6.14 TB/s at 30 B/param, interleaved (tools/adam_ab.py,
+// profiles/adam_r5.txt); a plain torch copy_ reaches 5.16 TB/s on that box.
+int g_adam_variant = 2;
 
 }  // namespace
 

@@ -183,10 +183,11 @@ def test_embedding(k):
 
 
 # ------------------------------------------------------------------ optimizer
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_flat_adam_matches_torch(k, variant):
-    """Both Adam kernels (grid-stride and one-shot tiles; the flat group spans
-    several tiles and ends in a scalar tail) against torch.optim.Adam."""
+    """Every Adam kernel (grid-stride, one-shot tiles, tiles with streaming
+    stores -- the default; the flat group spans several tiles and ends in a
+    scalar tail) against torch.optim.Adam."""
     from mipipe.optim import FlatAdam
 
     k.adam_set_variant(variant)
@@ -206,7 +207,7 @@ def test_flat_adam_matches_torch(k, variant):
             q.grad = g.clone()
         torch.nn.utils.clip_grad_norm_(qs, 0.5)
         ref.step()
-    k.adam_set_variant(1)
+    k.adam_set_variant(2)
     for p, q in zip(ps, qs):
         assert torch.allclose(p, q, atol=1e-5)
 
