@@ -4,7 +4,9 @@
 tools/bench_gemm.py and the A/B scripts measure) and sustained for seconds (what
 the step does), with the amdsmi telemetry of each window.
 
-    python tools/gemm_clock_probe.py
+    python tools/gemm_clock_probe.py            # burst vs sustained, the default kernel
+    python tools/gemm_clock_probe.py --waves    # sustained only: 8-wave vs 4-wave block, interleaved (energy per
+                                                # FLOP decides speed at the power cap; bursts cannot show it)
 """
 import statistics
 import sys
@@ -38,6 +40,32 @@ def run_window(fn, seconds=None, iters=None):
     t = tel.stop()
     return statistics.median(ts), t
 
+
+def waves_ab():
+    for name, M, N, K in SHAPES:
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        fl = 2.0 * M * N * K
+        for case, fn in (("fwd", lambda: k.linear_fwd(x, w, None, 0, 0.0, False)),
+                         ("dgrad", lambda: k.linear_dgrad(dy, w))):
+            for waves in (8, 4, 4, 8):
+                k.gemm_set_waves(waves)
+                for _ in range(10):
+                    fn()
+                torch.cuda.synchronize()
+                time.sleep(2.0)
+                ms, t = run_window(fn, seconds=3.0)
+                clk = (t.get("gfxclk_mhz") or {}).get("mean")
+                pw = (t.get("socket_power_w") or {}).get("mean")
+                print(f"{name:26s} {case:5s} {waves}-wave sustained 3 s {ms * 1e3:7.1f} us {fl / ms / 1e9:6.0f} TF/s | "
+                      f"gfxclk {clk} MHz, power {pw} W, power-limited {t.get('power_limited_pct')} %", flush=True)
+        k.gemm_set_waves(0)
+
+
+if "--waves" in sys.argv:
+    waves_ab()
+    sys.exit(0)
 
 for name, M, N, K in SHAPES:
     x = torch.randn(M, K, device=dev).to(torch.bfloat16)
