@@ -209,7 +209,9 @@ class IpcChannels:
         """Exercises every link of this rank exactly as the engine will: whole-slot
         messages through the sender's engine into the peer's ring, the GPU-side
         flag wait, a kernel reading the slot in place, the release -- and checks
-        every word (a pattern unique to link, direction and message).
+        every word (a pattern unique to link, direction and message) -- then
+        once more after the ring has wrapped onto the first slot read, so a
+        receiver reading stale cached lines of a reused slot is caught too.
 
         Returns ``None`` on success or the reason it failed.  Bounded: the GPU
         work runs on a side stream polled for ``timeout`` seconds; on a timeout
@@ -252,6 +254,31 @@ class IpcChannels:
                     t, work = self._recv_view(link, (words,), torch.int32)
                     work.wait()
                     ok &= (t == pattern(words, kind, src, me, rd, dev)).all().to(torch.int32)
+            self.end_step()
+            # Slot reuse: tiny filler messages walk every ring round to the slot the first round used and read
+            # (its lines are in this GPU's caches now), then one more checked whole-slot message lands there --
+            # a receiver that kept reading stale cached lines of its slot would fail here, not in a step.
+            outs = [(kind, link, dst) for kind, link, dst in (("act", self._act_out, next_g),
+                                                              ("grad", self._grad_out, prev_g)) if link is not None]
+            ins = [(kind, link, src) for kind, link, src in (("act", self._act_in, prev_g),
+                                                            ("grad", self._grad_in, next_g)) if link is not None]
+            filler = torch.zeros(64, dtype=torch.int32, device=dev)
+            for i in range(max([(-rounds) % int(link.nslots) for _, link, _ in outs + ins] or [0])):
+                for _, link, _ in outs:
+                    if i < (-rounds) % int(link.nslots):
+                        self._send(link, filler)
+                for _, link, _ in ins:
+                    if i < (-rounds) % int(link.nslots):
+                        _, work = self._recv_view(link, (64,), torch.int32)
+                        work.wait()
+                self.end_step()
+            for kind, link, dst in outs:
+                self._send(link, pattern(int(link.slot_bytes) // 4, kind, me, dst, rounds, dev))
+            for kind, link, src in ins:
+                words = int(link.slot_bytes) // 4
+                t, work = self._recv_view(link, (words,), torch.int32)
+                work.wait()
+                ok &= (t == pattern(words, kind, src, me, rounds, dev)).all().to(torch.int32)
             self.end_step()
             ev = torch.cuda.Event()
             ev.record(side)
