@@ -155,3 +155,27 @@ def test_bench_data_parallel_contract(transport):
     tokens = cfg["global_batch"] * cfg["seq_len"]
     assert abs(rec["value"] - tokens / (rec["ms_per_step"] / 1e3)) / rec["value"] < 0.01
     assert rec["loss"] is not None and rec["loss"] > 0
+
+
+def test_bench_emulated_plan_pick_cpu(tmp_path):
+    """PP > 1 with measured costs: the bench runs its candidate plans on every rank and keeps the fastest
+    (calibrate.select_plan_by_emulation) -- the path the GPU bench takes at N > 1, here over gloo."""
+    args = ["--gpus", "2", "--steps", "1", "--warmup", "1", "--device", "cpu", "--config", "tiny", "--num-layers", "4",
+            "--micro-batch", "2", "--plan", "measured", "--plan-select", "emulate", "--no-bubble"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py")] + args
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd="/tmp",
+                         env={**os.environ, "CUDA_VISIBLE_DEVICES": "", "MIPIPE_CALIB_DIR": str(tmp_path)})
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = _json_lines(out.stdout)[0]
+    cfg = rec["config"]
+    sel = cfg["plan_selection"]
+    assert sel is not None and cfg["plan_costs"].startswith("measured")
+    if len(sel["candidates"]) > 1:
+        assert sel["method"].startswith("emulated"), sel["method"]
+        chosen = sel["candidates"][sel["chosen"]]
+        assert all(len(c["rank_walls_ms"]) == 2 and min(c["rank_walls_ms"]) > 0 for c in sel["candidates"])
+        assert chosen["step_ms"] == min(c["step_ms"] for c in sel["candidates"])
+    else:
+        chosen = sel["candidates"][0]
+    assert chosen["v"] == cfg["virtual_chunks_per_rank"] and chosen["balance"] == cfg["balance"]
