@@ -388,8 +388,10 @@ uint64_t Link::send(const void* src, size_t bytes, hipStream_t producer, double 
                                hipStreamWaitValueGte, ~0ull),
           "hipStreamWaitValue64(freed)");
   if (bytes) {
+    // engines 0 / 3 ("sdma", "inline-sdma"): the copy engines only -- hipMemcpyDeviceToDevice may pick a blit
+    // kernel (CUs taken from compute, profiles/cu_hold_r5.txt); NoCU never does (tools/micro/nocu_copy.hip)
     if (engine_ == 1 || engine_ == 2) rt::blit_copy(dst, src, bytes, cs);
-    else check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync(send)");
+    else check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDeviceNoCU, cs), "hipMemcpyAsync(send, NoCU)");
   }
   check(hipStreamWriteValue64(cs, ring_ + int64_t(k) * kFlagStride, s + 1, 0), "hipStreamWriteValue64(full)");
   check(hipEventRecord(events_[k], cs), "hipEventRecord(sent)");

@@ -135,7 +135,10 @@ class IpcChannels:
         engine: the sender's copy (:data:`ENGINES`); default ``$MIPIPE_IPC_ENGINE``
             or ``"inline"`` (one-way 15.7 us at 1 MiB against ~150 us through a
             copy stream; the 2-rank shared-GPU step +3.2 %:
-            profiles/ipc_stream_ordered.txt).
+            profiles/ipc_stream_ordered.txt).  ``"sdma"`` / ``"inline-sdma"``
+            copy with ``hipMemcpyDeviceToDeviceNoCU``: the copy engines only,
+            never a blit kernel on the CUs (what transport ``auto`` uses across
+            GPUs; profiles/nocu_copy_r5.txt).
         timeout: seconds a host-mode wait may block before it raises (the
             engine's watchdog usually fires first).
     """
