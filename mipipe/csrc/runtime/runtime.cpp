@@ -146,7 +146,12 @@ void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_
     } else if (dst_device == src_device) {
       check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, src_stream), "hipMemcpyAsync");
     } else {
-      check(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, src_stream), "hipMemcpyPeerAsync");
+      // the copy engines only (peer access is on: Pipe enables it): a peer copy must not hold CUs for the
+      // whole xGMI transfer (profiles/nocu_copy_r5.txt); hipMemcpyPeerAsync if the runtime refuses the kind
+      if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDeviceNoCU, src_stream) != hipSuccess) {
+        (void)hipGetLastError();
+        check(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, src_stream), "hipMemcpyPeerAsync");
+      }
     }
   }
   {
