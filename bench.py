@@ -289,9 +289,14 @@ def main() -> int:
     # every rank gets the targets: the vocabulary-split decoder's head stage needs them too
     targets = [tokens[i, :, 1:].contiguous().to(device) for i in range(m)]
 
+    progress = os.environ.get("MIPIPE_BENCH_PROGRESS", "0") != "0" and rank == 0
+    t_start = time.perf_counter()
+
     def mark(label):
         if wd is not None:
             wd.progress(label)
+        if progress:  # a heartbeat for long rehearsals (host issue time, not GPU time)
+            print(f"[bench {time.perf_counter() - t_start:8.1f} s] {label}", file=sys.stderr, flush=True)
 
     def train_step():
         opt.zero_grad()
