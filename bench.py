@@ -134,6 +134,11 @@ def parse():
 
 def main() -> int:
     args = parse()
+    if os.environ.get("MIPIPE_BENCH_PROGRESS", "0") != "0":
+        import faulthandler
+
+        # a rehearsal that stops printing shows where every thread is, every 60 s
+        faulthandler.dump_traceback_later(60, repeat=True, file=sys.stderr)
     if args.impl == "pipe":
         return run_pipe(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
