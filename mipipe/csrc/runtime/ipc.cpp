@@ -82,6 +82,23 @@ static size_t map_size(int64_t nslots, int64_t slot_bytes, bool host) {
   return n;
 }
 
+static bool ipc_debug() {
+  static const bool on = [] {
+    const char* v = getenv("MIPIPE_IPC_DEBUG");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
+}
+
+#define IPC_TRACE(...)                                     \
+  do {                                                     \
+    if (ipc_debug()) {                                     \
+      fprintf(stderr, "[mipipe ipc %d] ", (int)getpid());  \
+      fprintf(stderr, __VA_ARGS__);                        \
+      fprintf(stderr, "\n");                               \
+    }                                                      \
+  } while (0)
+
 std::unique_ptr<Link> Link::create(const std::string& name, int device, int64_t nslots, int64_t slot_bytes) {
   if (nslots < 1 || nslots > kMaxSlots) throw std::runtime_error("mipipe ipc: nslots must be in [1, 1024]");
   if (slot_bytes < 16) throw std::runtime_error("mipipe ipc: slot_bytes too small");
@@ -147,6 +164,7 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
   L->device_ = device;
   L->engine_ = engine;
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  IPC_TRACE("attach %s: waiting for the block", name.c_str());
   for (;;) {
     L->fd_ = shm_open(name.c_str(), O_RDWR, 0600);
     if (L->fd_ >= 0) {
@@ -178,12 +196,15 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
   } else {
     DeviceGuard g(device);
     void* d = nullptr;
+    IPC_TRACE("attach %s: opening the ring handle", name.c_str());
     check(hipIpcOpenMemHandle(&d, sh->ring, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(ring)");
+    IPC_TRACE("attach %s: ring mapped at %p", name.c_str(), d);
     L->ring_ = static_cast<char*>(d);
     void* f = nullptr;
     check(hipMalloc(&f, size_t(flag_bytes(sh->nslots))), "hipMalloc(freed flags)");
     check(hipMemset(f, 0, size_t(flag_bytes(sh->nslots))), "hipMemset(freed flags)");
     check(hipDeviceSynchronize(), "hipDeviceSynchronize(freed flags)");
+    IPC_TRACE("attach %s: freed flags ready", name.c_str());
     L->freed_ = static_cast<char*>(f);
     L->owns_freed_ = true;
     check(hipIpcGetMemHandle(&sh->freed, f), "hipIpcGetMemHandle(freed flags)");
@@ -194,25 +215,10 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
       check(hipEventCreateWithFlags(&L->events_[k], hipEventDisableTiming), "hipEventCreate(slot)");
   }
   sh->sender_ready.store(1, std::memory_order_release);
+  IPC_TRACE("attach %s: done", name.c_str());
   return L;
 }
 
-static bool ipc_debug() {
-  static const bool on = [] {
-    const char* v = getenv("MIPIPE_IPC_DEBUG");
-    return v != nullptr && v[0] == '1';
-  }();
-  return on;
-}
-
-#define IPC_TRACE(...)                                     \
-  do {                                                     \
-    if (ipc_debug()) {                                     \
-      fprintf(stderr, "[mipipe ipc %d] ", (int)getpid());  \
-      fprintf(stderr, __VA_ARGS__);                        \
-      fprintf(stderr, "\n");                               \
-    }                                                      \
-  } while (0)
 
 Link::~Link() {
   IPC_TRACE("destroy %s %s", sender_ ? "sender" : "receiver", name_.c_str());
