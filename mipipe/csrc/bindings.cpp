@@ -1160,6 +1160,7 @@ PYBIND11_MODULE(_C, m) {
       .def("drain", &ipc::Link::drain, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
       .def("message_bytes", &ipc::Link::message_bytes)
       .def("unlink", &ipc::Link::unlink)
+      .def("open_peer_flags", &ipc::Link::open_peer_flags, py::call_guard<py::gil_scoped_release>())
       .def("describe", &ipc::Link::describe)
       .def_property_readonly("copy_stream", [](const ipc::Link& L) { return reinterpret_cast<int64_t>(L.copy_stream()); })
       .def_property_readonly("inline_copy", &ipc::Link::inline_copy)

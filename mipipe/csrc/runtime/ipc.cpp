@@ -422,7 +422,9 @@ void Link::open_peer_flags() {
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   void* f = nullptr;
+  IPC_TRACE("receiver %s: opening the sender's freed flags", name_.c_str());
   check(hipIpcOpenMemHandle(&f, sh_->freed, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(freed flags)");
+  IPC_TRACE("receiver %s: freed flags mapped", name_.c_str());
   freed_ = static_cast<char*>(f);
   peer_open_ = true;
 }

@@ -98,12 +98,15 @@ class Link {
   int64_t message_bytes(uint64_t seq) const;
   // Removes the shm name (after both sides are attached; the mapping stays).
   void unlink();
+  // Receiver: maps the sender's freed flags (exported when it attached).  Done at
+  // construction, one process at a time (mipipe/parallel/ipc.py): importing IPC
+  // handles concurrently in a ring of processes can deadlock in the runtime.
+  void open_peer_flags();
   std::string describe() const;
 
  private:
   Link() = default;
   void wait_for(const char* what, uint64_t seq, int slot, bool full, double timeout_s) const;
-  void open_peer_flags();
   char* slot(uint64_t seq) const;
 
   std::string name_;

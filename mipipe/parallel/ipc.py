@@ -176,9 +176,11 @@ class IpcChannels:
         self._links: list = []
         self._copy_streams: Dict[int, torch.cuda.ExternalStream] = {}
         self._held: List[Tuple[object, int, int]] = []  # (link, seq, bytes) read in place, released at end_step
+        members = sorted(set(self.ranks))
         if self.rank < 0 or n < 2:
-            dist.barrier()
-            dist.barrier()
+            # every process takes part in the same barriers (the attach below runs one member at a time)
+            for _ in range(1 + 2 * len(members) if n >= 2 else 1):
+                dist.barrier()
             return
         r = self.rank
         has_prev = r > 0 or wrap
@@ -195,13 +197,24 @@ class IpcChannels:
             self._grad_in = k.IpcLink.create(name("grad", next_g, me), dev_index, slots,
                                              max(by_rank[next_g], 256))
         dist.barrier()
-        # ... then senders attach to the neighbours' blocks
+        # ... then senders attach to the neighbours' blocks (importing their rings, exporting their own freed
+        # flags), and receivers map the senders' freed flags -- ONE PROCESS AT A TIME: with every rank importing
+        # a neighbour's handle at once (a ring of imports) hipIpcOpenMemHandle deadlocked in the runtime (4 and 8
+        # ranks on one MI355X: every rank blocked inside it; tools/ipc_attach_probe.py, tools/gpu_runs/r5_g25.sh).
         eng = ENGINES[engine]
-        if has_next:
-            self._act_out = k.IpcLink.attach(name("act", me, next_g), dev_index, eng, self.timeout)
-        if has_prev:
-            self._grad_out = k.IpcLink.attach(name("grad", me, prev_g), dev_index, eng, self.timeout)
-        dist.barrier()
+        for turn in members:
+            if turn == me:
+                if has_next:
+                    self._act_out = k.IpcLink.attach(name("act", me, next_g), dev_index, eng, self.timeout)
+                if has_prev:
+                    self._grad_out = k.IpcLink.attach(name("grad", me, prev_g), dev_index, eng, self.timeout)
+            dist.barrier()
+        for turn in members:
+            if turn == me:
+                for link in (self._act_in, self._grad_in):
+                    if link is not None:
+                        link.open_peer_flags()
+            dist.barrier()
         self._links = [x for x in (self._act_in, self._grad_in, self._act_out, self._grad_out) if x is not None]
         for link in self._links:
             if not link.is_sender:
