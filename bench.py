@@ -243,6 +243,20 @@ def main() -> int:
             plan_report = {"method": "one candidate within 6 % of the model's best: no emulation needed",
                            "candidates": [{"v": plan.virtual, "split_decoder": plan.split_decoder,
                                            "balance": list(plan.balance)}], "chosen": 0}
+    from mipipe.parallel.watchdog import Watchdog
+
+    wd = Watchdog(args.watchdog) if args.watchdog > 0 else None
+    act_shapes = [stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(prank)]
+    # The stage transport first, before the stages take their memory: link set-up maps peer memory, and it is
+    # kept out of the way of the big allocations (profiles/ipc_import_stall_r5.txt).
+    early_chan = None
+    if world > 1 and dp == 1 and args.skips == "none":
+        from mipipe.parallel.engine import make_transport
+
+        item = torch.empty((), dtype=dtype).element_size()
+        early_chan, _, _ = make_transport(list(range(world)), device=device, chunks=m, virtual=virtual,
+                                          recv_bytes=max(torch.Size(s_).numel() for s_ in act_shapes) * item,
+                                          transport=args.transport, watchdog=wd)
     torch.manual_seed(1234 + prank)  # same initial weights in every data-parallel replica
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     from mipipe.models.long_skip import unet_pairs
@@ -258,7 +272,6 @@ def main() -> int:
 
     is_last = prank == pp - 1
     groups = dpg = None
-    act_shapes = [stage_input_shape(cfg, plan, vs, mb) for vs in plan.vstages(prank)]
     if dp > 1:
         from mipipe.parallel.data_parallel import DataParallelGrads, make_pp_dp_groups
 
@@ -274,13 +287,10 @@ def main() -> int:
     def loss_fn(y, t):
         return ops.cross_entropy(y.reshape(-1, V), t.reshape(-1))
 
-    from mipipe.parallel.watchdog import Watchdog
-
-    wd = Watchdog(args.watchdog) if args.watchdog > 0 else None
     engine = PipelineEngine(stages, chunks=m, checkpoint=args.checkpoint, act_shape=act_shapes,
                             act_dtype=dtype, loss_fn=loss_fn if is_last else None, device=device,
                             skip_shapes={"skip": ((mb, S, E), dtype)}, watchdog=wd,
-                            group=groups.channels if groups is not None else None,
+                            group=groups.channels if groups is not None else early_chan,
                             grad_divisor=dp, transport=args.transport)
     # explicit recompute (issued before each gradient wait, as the engine does)
     from mipipe.pipeline import checkpoint_stop_for

@@ -227,33 +227,19 @@ class PipelineEngine:
         self.transport_note: Optional[str] = None
         if isinstance(group, Channels) or hasattr(group, "send_act"):  # ready channels (RCCL or IPC)
             self.chan: Optional[Channels] = group
-            self.transport = "ipc" if type(group).__name__ == "IpcChannels" else "rccl"
+            # channels made by make_transport() carry what they are; others are named by type
+            self.transport = getattr(group, "transport_name", None) or (
+                "ipc" if type(group).__name__ == "IpcChannels" else "rccl")
+            self.transport_note = getattr(group, "transport_note", None)
             if group.world > 1:
                 with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
                     group.warmup(device or next(mods[0].parameters()).device)
         elif dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
             dev = device or next(mods[0].parameters()).device
-            if transport == "auto":
-                transport = self._auto_transport(ranks, dev, transport_options, watchdog)
-            elif transport == "ipc":
-                from .ipc import IpcChannels
-
-                opts = dict(transport_options or {})
-                # one slot per message a link carries in a step: a sender never
-                # blocks inside a step (with fewer, a looping placement can
-                # deadlock: rank 0 would wait for a slot rank 1 frees only
-                # after rank 0's own later chunk has run)
-                opts.setdefault("slots", self.chunks * self.virtual)
-                self.chan = IpcChannels(ranks, wrap=self.virtual > 1, device=dev, recv_bytes=self.recv_bytes(),
-                                        **opts)
-            elif transport == "rccl":
-                self.chan = Channels(ranks, wrap=self.virtual > 1)
-                with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
-                    self.chan.warmup(dev)
-            else:
-                raise ValueError(f"transport must be 'auto', 'rccl' or 'ipc', got {transport!r}")
-            self.transport = transport
+            self.chan, self.transport, self.transport_note = make_transport(
+                ranks, device=dev, chunks=self.chunks, virtual=self.virtual, recv_bytes=self.recv_bytes(),
+                transport=transport, transport_options=transport_options, watchdog=watchdog)
         else:
             self.chan = None
         if self.chan is not None:
@@ -274,52 +260,6 @@ class PipelineEngine:
             self.watchdog.describe = self.describe
         self._setup_skips(group, skip_shapes, skip_routes)
 
-    def _auto_transport(self, ranks, dev, transport_options, watchdog) -> str:
-        """``transport="auto"``: stage boundaries that take no CU from compute.
-
-        An RCCL receive is a kernel that spins on its CUs until the data lands
-        (footprint of torch's ``rcclGenericKernel``: 256 threads, 19.7 KiB LDS,
-        ~270 registers -- it can never share a CU with a 256x256 GEMM block),
-        and the engine posts its receives ahead, so one stays resident through
-        most of a phase.  ``profiles/cu_hold_r5.txt`` measures what k such
-        blocks cost the PP=1 step.  The IPC links move data with the DMA engines
-        (the link's copy stream, ``sdma``) and order it with command-processor
-        stream waits: no CU at all -- the reference's own design (copies on
-        dedicated copy streams, event waits: /root/reference/README.md:193-237,
-        332-369).  Ranks sharing one GPU (rehearsals) copy on the producer's
-        stream (``inline``).  The links are self-tested first
-        (:meth:`IpcChannels.self_test`); if any rank fails, every rank falls
-        back to RCCL and :attr:`transport_note` says why.  CPU: RCCL-style
-        channels over gloo.  Collective."""
-        if dev.type != "cuda":
-            self.chan = Channels(ranks, wrap=self.virtual > 1)
-            self.chan.warmup(dev)
-            return "rccl"
-        from .ipc import IpcChannels, ranks_share_a_device, verified_ipc
-
-        shared = ranks_share_a_device(dev)
-        opts = dict(transport_options or {})
-        opts.setdefault("slots", self.chunks * self.virtual)
-        opts.setdefault("engine", "inline" if shared else "sdma")
-
-        def make_rccl():
-            if shared:
-                raise RuntimeError("IPC links failed their self-test and RCCL refuses two ranks on one GPU: "
-                                   + str(self.transport_note))
-            ch = Channels(ranks, wrap=self.virtual > 1)
-            with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
-                ch.warmup(dev)
-            return ch
-
-        with (watchdog.watch("IPC link self-test") if watchdog is not None else _null()):
-            self.chan, why = verified_ipc(
-                lambda: IpcChannels(ranks, wrap=self.virtual > 1, device=dev, recv_bytes=self.recv_bytes(), **opts),
-                make_rccl, dev)
-        if why is not None:
-            self.transport_note = f"IPC self-test failed, fell back to RCCL: {why}"
-            warnings.warn(self.transport_note)
-            return "rccl"
-        return f"ipc-{opts['engine']}"
 
     def close(self) -> None:
         """Releases the transport (IPC links: senders unmap, then receivers
@@ -775,3 +715,87 @@ class PipelineEngine:
                 lines.append(f"[mipipe engine] rank {self.rank}: {len(left)} transfer(s) left in flight:")
                 lines.extend(f"[mipipe engine]   {u}" for u in left[:32])
         print("\n".join(lines), file=sys.stderr, flush=True)
+
+
+def make_transport(ranks: Sequence[int], *, device: torch.device, chunks: int, virtual: int, recv_bytes: int,
+                   transport: str = "auto", transport_options: Optional[dict] = None, watchdog=None):
+    """The stage-boundary channels of one pipeline rank: ``(channels, name, note)``.
+
+    What :class:`PipelineEngine` builds from ``transport=``; callable on its own
+    so a driver can set the links up before it allocates its stages (bench.py
+    does).  ``recv_bytes``: the largest activation this rank receives per
+    micro-batch.  Collective over ``ranks``.
+
+    ``transport="auto"``: stage boundaries that take no CU from compute.
+    An RCCL receive is a kernel that spins on its CUs until the data lands
+    (footprint of torch's ``rcclGenericKernel``: 256 threads, 19.7 KiB LDS,
+    ~270 registers -- it can never share a CU with a 256x256 GEMM block),
+    and the engine posts its receives ahead, so one stays resident through
+    most of a phase.  ``profiles/cu_hold_r5.txt`` measures what k such
+    blocks cost the PP=1 step.  The IPC links move data with the DMA engines
+    (the link's copy stream, ``sdma``: ``hipMemcpyDeviceToDeviceNoCU``) and
+    order it with command-processor stream waits: no CU at all -- the
+    reference's own design (copies on dedicated copy streams, event waits:
+    /root/reference/README.md:193-237, 332-369).  Ranks sharing one GPU
+    (rehearsals) copy on the producer's stream (``inline``).  The links are
+    self-tested first (:meth:`IpcChannels.self_test`); if any rank fails,
+    every rank falls back to RCCL and the note says why.  CPU: RCCL-style
+    channels over gloo."""
+    dev = torch.device(device)
+    wrap = virtual > 1
+    note = None
+    if transport == "auto":
+        if dev.type != "cuda":
+            chan = Channels(ranks, wrap=wrap)
+            chan.warmup(dev)
+            name = "rccl"
+        else:
+            from .ipc import IpcChannels, ranks_share_a_device, verified_ipc
+
+            shared = ranks_share_a_device(dev)
+            opts = dict(transport_options or {})
+            opts.setdefault("slots", chunks * virtual)
+            opts.setdefault("engine", "inline" if shared else "sdma")
+            fallback = {}
+
+            def make_rccl():
+                if shared:
+                    raise RuntimeError("IPC links failed their self-test and RCCL refuses two ranks on one GPU: "
+                                       + str(fallback.get("why")))
+                ch = Channels(ranks, wrap=wrap)
+                with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
+                    ch.warmup(dev)
+                return ch
+
+            with (watchdog.watch("IPC link self-test") if watchdog is not None else _null()):
+                chan, why = verified_ipc(
+                    lambda: IpcChannels(ranks, wrap=wrap, device=dev, recv_bytes=recv_bytes, **opts), make_rccl, dev)
+            if why is not None:
+                note = f"IPC self-test failed, fell back to RCCL: {why}"
+                warnings.warn(note)
+                name = "rccl"
+            else:
+                name = f"ipc-{opts['engine']}"
+    elif transport == "ipc":
+        from .ipc import IpcChannels
+
+        opts = dict(transport_options or {})
+        # one slot per message a link carries in a step: a sender never
+        # blocks inside a step (with fewer, a looping placement can
+        # deadlock: rank 0 would wait for a slot rank 1 frees only
+        # after rank 0's own later chunk has run)
+        opts.setdefault("slots", chunks * virtual)
+        chan = IpcChannels(ranks, wrap=wrap, device=dev, recv_bytes=recv_bytes, **opts)
+        name = "ipc"
+    elif transport == "rccl":
+        chan = Channels(ranks, wrap=wrap)
+        with (watchdog.watch("RCCL channel warm-up") if watchdog is not None else _null()):
+            chan.warmup(dev)
+        name = "rccl"
+    else:
+        raise ValueError(f"transport must be 'auto', 'rccl' or 'ipc', got {transport!r}")
+    try:
+        chan.transport_name, chan.transport_note = name, note
+    except AttributeError:  # channels without a __dict__: the engine names them by type
+        pass
+    return chan, name, note
