@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="enc12_d4096")
     ap.add_argument("--micro-batch", type=int, default=None,
-                    help="sequences per micro-batch (default 64 for enc12_d4096, 8 for ref_main (the reference's) "
+                    help="sequences per micro-batch (default 128 for enc12_d4096, 8 for ref_main (the reference's) "
                          "and gpt2_xl)")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--num-layers", type=int, default=None, help="override the model's layer count (tests)")
@@ -665,14 +665,16 @@ def _config(args):
 
 def _default_micro_batch(cfg) -> int:
     # ref_main: the reference's own micro-batch (batch 32 / chunks 4 = 8 sequences).
-    # enc12_d4096: 64 x 128 = 8192 tokens per GEMM, sized for 288 GB of HBM (57 GiB peak at
-    # PP=1): +3.5 % over 32 x 128 on the same box (profiles/microbatch_sizing.txt).
+    # enc12_d4096: 128 x 128 = 16,384 tokens per GEMM, sized for 288 GB of HBM (89 GiB peak at
+    # PP=1): +3.5 % for 64 over 32 (round 2), then +2.2 % for 128 over 64 at the power cap (the
+    # optimizer, grad-norm and per-launch costs amortised over twice the tokens; same box,
+    # interleaved: profiles/microbatch_sizing.txt).
     # gpt2_xl: 18 x 1024 tokens -- the 1600-wide GEMM outputs (attention out-proj, fc2 and
     # the dgrads into the residual stream) are 7 256-wide tile columns, so M = 18,432 makes
     # 504 tiles = 98 % of two rounds of the 256 CUs (8 x 1024: 224 tiles, 88 % of one):
     # PP=1 54.6k (mb 8) -> 58.3k (mb 9) -> 59.8k tok/s (mb 18), 208 GiB peak with
     # checkpoint='always' (profiles/microbatch_sizing.txt).
-    return {"gpt2_xl": 18, "tiny": 8, "ref_main": 8}.get(cfg.name, 64)
+    return {"gpt2_xl": 18, "tiny": 8, "ref_main": 8}.get(cfg.name, 128)
 
 
 def _baseline_note(ref_match: bool, checkpoint: str) -> str:
