@@ -194,7 +194,7 @@ def main() -> int:
         auto_ckpt = "except_last" if pp == 8 else "never"
     if args.checkpoint == "auto":
         args.checkpoint = auto_ckpt
-    mb = args.micro_batch or _default_micro_batch(cfg)
+    mb = args.micro_batch or _default_micro_batch(cfg, pp)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
     splits = {"auto": (False, True), "on": (True,), "off": (False,)}[args.split_decoder]
@@ -663,17 +663,21 @@ def _config(args):
     return cfg
 
 
-def _default_micro_batch(cfg) -> int:
+def _default_micro_batch(cfg, pp: int = 1) -> int:
     # ref_main: the reference's own micro-batch (batch 32 / chunks 4 = 8 sequences).
     # enc12_d4096: 128 x 128 = 16,384 tokens per GEMM, sized for 288 GB of HBM (89 GiB peak at
     # PP=1): +3.5 % for 64 over 32 (round 2), then +2.2 % for 128 over 64 at the power cap (the
     # optimizer, grad-norm and per-launch costs amortised over twice the tokens; same box,
-    # interleaved: profiles/microbatch_sizing.txt).
+    # interleaved: profiles/microbatch_sizing.txt).  Except the full-node PP=8 run (config #3,
+    # 'except_last', chunks 32): there 128 predicts 817k job tok/s against 868k for 64 (every rank
+    # emulated, profiles/plan_table_r5.txt), so PP=8 keeps 64.
     # gpt2_xl: 18 x 1024 tokens -- the 1600-wide GEMM outputs (attention out-proj, fc2 and
     # the dgrads into the residual stream) are 7 256-wide tile columns, so M = 18,432 makes
     # 504 tiles = 98 % of two rounds of the 256 CUs (8 x 1024: 224 tiles, 88 % of one):
     # PP=1 54.6k (mb 8) -> 58.3k (mb 9) -> 59.8k tok/s (mb 18), 208 GiB peak with
     # checkpoint='always' (profiles/microbatch_sizing.txt).
+    if cfg.name == "enc12_d4096" and pp == 8:
+        return 64
     return {"gpt2_xl": 18, "tiny": 8, "ref_main": 8}.get(cfg.name, 128)
 
 

@@ -1,7 +1,7 @@
 """Which PP=8 stage plan is fastest?  Every alternative the planner can produce,
 each rank emulated on ONE MI355X.
 
-For a BASELINE config (#3: enc12_d4096, chunks 32, micro-batch 128 -- the
+For a BASELINE config (#3: enc12_d4096, chunks 32, micro-batch 64 -- the
 bench's default -- 'except_last'; #4: GPT-2-XL, chunks 8, micro-batch 18,
 'always'),
 the plans are: unit costs {analytic FLOPs, measured engine-context costs} x
@@ -41,13 +41,13 @@ from pp_rank_emulation import run_rank  # noqa: E402
 
 # the bench's defaults per model and PP (bench.py: chunks, _default_micro_batch, checkpoint 'auto'): BASELINE
 # config #2 (enc12, chunks 4 x PP, 'never'), #3 (its PP=8 run: 'except_last'), #4 (GPT-2-XL, chunks 8 at PP=8)
-CONFIG = {"enc12_d4096": (32, 128, "except_last"), "gpt2_xl": (8, 18, "always")}
+CONFIG = {"enc12_d4096": (32, 64, "except_last"), "gpt2_xl": (8, 18, "always")}
 
 
 def bench_defaults(name: str, pp: int):
     if name == "gpt2_xl":
         return (8 if pp == 8 else 4 * pp), 18, "always"
-    return 4 * pp, 128, ("except_last" if pp == 8 else "never")
+    return 4 * pp, (64 if pp == 8 else 128), ("except_last" if pp == 8 else "never")
 HOP_MS = 0.15
 XGMI_BYTES_PER_S = 100e9
 
