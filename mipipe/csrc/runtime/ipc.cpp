@@ -1,6 +1,9 @@
 // Device-memory P2P transport between processes, completed on the GPU: see ipc.h.
 #include "ipc.h"
 
+#include <algorithm>
+#include <vector>
+
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,6 +27,10 @@ namespace {
 
 constexpr uint64_t kMagic = 0x6d69706970654c32ull;  // "mipipeL2"
 constexpr int kMaxSlots = 1024;
+// Device mode: the slots live in allocations of at most ~1 GiB each (one IPC handle per chunk).  Importing a single
+// 3 GiB allocation from another process stalled inside hipIpcOpenMemHandle (profiles/ipc_import_stall_r5.txt).
+constexpr int64_t kChunkBytes = int64_t(1) << 30;
+constexpr int kMaxChunks = 64;
 constexpr int64_t kFlagStride = 64;  // one flag word per 64-byte line
 
 void check(hipError_t e, const char* what) {
@@ -69,8 +76,11 @@ struct Shared {
   std::atomic<uint32_t> receiver_detached;   // the receiver has unmapped the freed flags
   std::atomic<uint64_t> sent;                // messages the sender has enqueued
   std::atomic<uint64_t> released;            // messages the receiver has released (enqueued)
-  hipIpcMemHandle_t ring;                    // receiver's full flags + slots
+  hipIpcMemHandle_t ring;                    // receiver's full flags (device mode)
   hipIpcMemHandle_t freed;                   // sender's freed flags
+  int32_t nchunks;                           // device mode: the slot allocations
+  int32_t slots_per_chunk;
+  hipIpcMemHandle_t chunk[kMaxChunks];
   SlotCtl slots[kMaxSlots];
 };
 
@@ -141,13 +151,29 @@ std::unique_ptr<Link> Link::create(const std::string& name, int device, int64_t 
   } else {
     DeviceGuard g(device);
     void* d = nullptr;
-    const size_t bytes = size_t(flag_bytes(nslots)) + size_t(nslots) * size_t(slot_bytes);
-    check(hipMalloc(&d, bytes), "hipMalloc(ring)");
+    check(hipMalloc(&d, size_t(flag_bytes(nslots))), "hipMalloc(full flags)");
     check(hipMemset(d, 0, size_t(flag_bytes(nslots))), "hipMemset(full flags)");
     check(hipDeviceSynchronize(), "hipDeviceSynchronize(ring)");
     L->ring_ = static_cast<char*>(d);
     L->owns_ring_ = true;
-    check(hipIpcGetMemHandle(&sh->ring, d), "hipIpcGetMemHandle(ring)");
+    check(hipIpcGetMemHandle(&sh->ring, d), "hipIpcGetMemHandle(full flags)");
+    int64_t spc = std::max<int64_t>(1, std::min<int64_t>(nslots, kChunkBytes / slot_bytes));
+    int64_t nch = (nslots + spc - 1) / spc;
+    if (nch > kMaxChunks) {
+      spc = (nslots + kMaxChunks - 1) / kMaxChunks;
+      nch = (nslots + spc - 1) / spc;
+    }
+    sh->nchunks = int32_t(nch);
+    sh->slots_per_chunk = int32_t(spc);
+    for (int64_t c = 0; c < nch; ++c) {
+      const int64_t n = std::min(spc, nslots - c * spc);
+      void* q = nullptr;
+      check(hipMalloc(&q, size_t(n) * size_t(slot_bytes)), "hipMalloc(slot chunk)");
+      L->chunk_.push_back(static_cast<char*>(q));
+      check(hipIpcGetMemHandle(&sh->chunk[c], q), "hipIpcGetMemHandle(slot chunk)");
+    }
+    IPC_TRACE("create %s: %lld slots of %lld B in %lld chunk(s)", name.c_str(), (long long)nslots,
+              (long long)slot_bytes, (long long)nch);
     L->events_ = new hipEvent_t[nslots];
     for (int k = 0; k < nslots; ++k)
       check(hipEventCreateWithFlags(&L->events_[k], hipEventDisableTiming), "hipEventCreate(slot)");
@@ -197,9 +223,14 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
     DeviceGuard g(device);
     void* d = nullptr;
     IPC_TRACE("attach %s: opening the ring handle", name.c_str());
-    check(hipIpcOpenMemHandle(&d, sh->ring, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(ring)");
-    IPC_TRACE("attach %s: ring mapped at %p", name.c_str(), d);
+    check(hipIpcOpenMemHandle(&d, sh->ring, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(full flags)");
     L->ring_ = static_cast<char*>(d);
+    for (int c = 0; c < sh->nchunks; ++c) {
+      void* q = nullptr;
+      check(hipIpcOpenMemHandle(&q, sh->chunk[c], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(slot chunk)");
+      L->chunk_.push_back(static_cast<char*>(q));
+    }
+    IPC_TRACE("attach %s: ring mapped (%d chunk(s))", name.c_str(), sh->nchunks);
     void* f = nullptr;
     check(hipMalloc(&f, size_t(flag_bytes(sh->nslots))), "hipMalloc(freed flags)");
     check(hipMemset(f, 0, size_t(flag_bytes(sh->nslots))), "hipMemset(freed flags)");
@@ -239,6 +270,7 @@ Link::~Link() {
       }
       if (sender_) {
         if (ring_) (void)hipIpcCloseMemHandle(ring_);
+        for (char* q : chunk_) (void)hipIpcCloseMemHandle(q);
         sh_->sender_detached.store(1, std::memory_order_release);
         // The receiver maps our freed flags until it detaches; freeing memory a
         // peer still maps can block until it lets go (two ranks tearing down
@@ -250,7 +282,10 @@ Link::~Link() {
         sh_->receiver_detached.store(1, std::memory_order_release);
         const bool mapped = sh_->sender_ready.load(std::memory_order_acquire) &&
                             !sh_->sender_detached.load(std::memory_order_acquire);
-        if (owns_ring_ && !mapped) (void)hipFree(ring_);
+        if (owns_ring_ && !mapped) {
+          (void)hipFree(ring_);
+          for (char* q : chunk_) (void)hipFree(q);
+        }
         IPC_TRACE("  ring %s", mapped ? "left mapped by the peer (not freed)" : "freed");
       }
       if (events_)
@@ -329,8 +364,9 @@ void Link::unlink() { shm_unlink(name_.c_str()); }
 
 char* Link::slot(uint64_t seq) const {
   const int k = int(seq % uint64_t(sh_->nslots));
-  const int64_t base = host_mode() ? 0 : flag_bytes(sh_->nslots);
-  return ring_ + base + int64_t(k) * sh_->slot_bytes;
+  if (host_mode()) return ring_ + int64_t(k) * sh_->slot_bytes;
+  const int64_t spc = sh_->slots_per_chunk;
+  return chunk_[size_t(int64_t(k) / spc)] + (int64_t(k) % spc) * sh_->slot_bytes;
 }
 
 std::string Link::describe() const {

@@ -37,6 +37,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace mipipe {
 namespace ipc {
@@ -116,7 +117,8 @@ class Link {
   Shared* sh_ = nullptr;
   size_t map_bytes_ = 0;
   int fd_ = -1;
-  char* ring_ = nullptr;          // receiver's allocation: full flags, then the slots (device, or in the shm map)
+  char* ring_ = nullptr;          // device: the receiver's full flags; host: the slots in the shm map
+  std::vector<char*> chunk_;      // device: the receiver's slot allocations (each <= ~1 GiB)
   bool owns_ring_ = false;
   char* freed_ = nullptr;         // sender's allocation: freed flags (device mode)
   bool owns_freed_ = false;
