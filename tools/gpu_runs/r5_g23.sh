@@ -6,6 +6,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-export PYTHONUNBUFFERED=1
-timeout -k 10 480 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29615 bench.py --gpus 8 --shared-gpu --micro-batch 32 --steps 2 --warmup 1 --no-bubble > gpurun_out/pp8_shared.log 2>&1 || { tail -40 gpurun_out/pp8_shared.log; exit 1; }
+export PYTHONUNBUFFERED=1 MIPIPE_BENCH_PROGRESS=1
+timeout -k 10 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29615 bench.py --gpus 8 --shared-gpu --micro-batch 32 --steps 2 --warmup 1 --no-bubble > gpurun_out/pp8_shared.log 2>&1 &
+pid=$!
+while kill -0 $pid 2>/dev/null; do sleep 20; echo "[$(date +%T)] $(grep '^\[bench' gpurun_out/pp8_shared.log | tail -1)" >> gpurun_out/pp8_heartbeat.txt; done
+wait $pid || { tail -5 gpurun_out/pp8_heartbeat.txt; grep -v "amdgpu.ids\|^\[W\|^W20" gpurun_out/pp8_shared.log | tail -30; exit 1; }
 grep '"metric"' gpurun_out/pp8_shared.log | cut -c1-1500
