@@ -430,6 +430,11 @@ def main() -> int:
                          f"{'pre' if cfg.norm_first else 'post'}-norm) + embedding/decoder V={V}",
                 "params": total_params,
                 "global_batch": m * mb * dp,
+                "tokens_per_gpu_per_step": m * mb * dp * S // max(1, world),
+                "micro_batch_note": ("enc12 default: 128 sequences at PP <= 4, 64 at PP = 8 (config #3: 128 predicts "
+                                     "6 % less there, profiles/plan_table_r5.txt), so the N = 8 run carries half the "
+                                     "per-GPU tokens of N <= 4" if cfg.name == "enc12_d4096" and not args.micro_batch
+                                     else None),
                 "seq_len": S,
                 "micro_batch": mb,
                 "chunks": m,
