@@ -1155,15 +1155,21 @@ PYBIND11_MODULE(_C, m) {
       .def("release",
            [](ipc::Link& L, uint64_t seq, int64_t consumer) { L.release(seq, reinterpret_cast<hipStream_t>(consumer)); },
            py::arg("seq"), py::arg("consumer_stream"))
+      // several messages at once: one counter write for the in-order prefix
+      .def("release_many",
+           [](ipc::Link& L, std::vector<uint64_t> seqs, int64_t consumer) {
+             L.release(seqs, reinterpret_cast<hipStream_t>(consumer));
+           },
+           py::arg("seqs"), py::arg("consumer_stream"))
       .def("done", &ipc::Link::done)
       .def("abort", &ipc::Link::abort)
       .def("drain", &ipc::Link::drain, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
       .def("message_bytes", &ipc::Link::message_bytes)
       .def("unlink", &ipc::Link::unlink)
-      .def("open_peer_flags", &ipc::Link::open_peer_flags, py::call_guard<py::gil_scoped_release>())
       .def("describe", &ipc::Link::describe)
       .def_property_readonly("copy_stream", [](const ipc::Link& L) { return reinterpret_cast<int64_t>(L.copy_stream()); })
       .def_property_readonly("inline_copy", &ipc::Link::inline_copy)
+      .def_property_readonly("dma_engine", &ipc::Link::dma_engine)
       .def_property_readonly("nslots", &ipc::Link::nslots)
       .def_property_readonly("slot_bytes", &ipc::Link::slot_bytes)
       .def_property_readonly("host_mode", &ipc::Link::host_mode)
@@ -1177,6 +1183,17 @@ PYBIND11_MODULE(_C, m) {
         py::arg("src_device"), py::arg("dst_device"), py::arg("engine") = 0);
   m.def("enable_peer_access", [](std::vector<int> d) { rt::enable_peer_access(d); });
   m.def("can_access_peer", [](int d, int q) { return rt::can_access_peer(d, q); });
+  m.def("copy_nocu",
+        [](Tensor dst, Tensor src, int64_t stream) {
+          MP_CHECK(dst.is_cuda() && src.is_cuda() && dst.nbytes() == src.nbytes(), "copy_nocu: equal device tensors");
+          return rt::copy_nocu(dst.data_ptr(), src.data_ptr(), src.nbytes(), reinterpret_cast<hipStream_t>(stream));
+        },
+        py::arg("dst"), py::arg("src"), py::arg("stream"));
+  m.def("hip_runtime_version", []() {
+    int v = 0;
+    (void)hipRuntimeGetVersion(&v);
+    return v;
+  });
   m.def("range_push", [](const std::string& s) { rt::range_push(s); });
   m.def("range_pop", []() { rt::range_pop(); });
   m.def("mark", [](const std::string& s) { rt::mark(s); });

@@ -163,6 +163,13 @@ void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_
   }
 }
 
+std::string copy_nocu(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDeviceNoCU, stream);
+  if (e == hipSuccess) return std::string();
+  (void)hipGetLastError();
+  return hipGetErrorString(e);
+}
+
 bool can_access_peer(int device, int peer) {
   int ok = 0;
   check(hipDeviceCanAccessPeer(&ok, device, peer), "hipDeviceCanAccessPeer");

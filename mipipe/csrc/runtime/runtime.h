@@ -35,6 +35,10 @@ void peer_copy(void* dst, int dst_device, const void* src, int src_device, size_
 // hipMemcpyAsync for pointers or sizes that are not 16-byte multiples).
 void blit_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 
+// One hipMemcpyDeviceToDeviceNoCU copy on `stream` (the DMA engines only): "" if
+// the runtime accepted it, else its error (diagnostics: which runtime refuses it).
+std::string copy_nocu(void* dst, const void* src, size_t bytes, hipStream_t stream);
+
 // Enables peer access between every ordered pair of `devices` (idempotent).
 void enable_peer_access(const std::vector<int>& devices);
 bool can_access_peer(int device, int peer);

@@ -1,10 +1,13 @@
-"""Multi-process synchronous pipeline (GPipe) over RCCL -- one rank per MI355X.
+"""Multi-process synchronous pipeline (GPipe) -- one rank per MI355X.
 
-This is the scale-out form of :class:`mipipe.Pipe` (SURVEY §5.8 (b), §7.2 step
+This is the scale-out form of :class:`mipipe.Pipe` (SURVEY §5.8, §7.2 step
 5): instead of one process driving every GPU from worker threads with peer
 copies, each GPU is one process (``torchrun --nproc-per-node N``) that owns
 slices of the model, and activations / gradients move between neighbouring
-ranks with RCCL send/recv over xGMI.  It keeps the reference's semantics:
+ranks over xGMI -- by default through self-tested device-memory IPC links
+(DMA copies into the receiver's slot ring, :mod:`mipipe.parallel.ipc`), with
+RCCL send/recv (:class:`~mipipe.parallel.p2p.Channels`) as the fall-back every
+rank switches to together.  It keeps the reference's semantics:
 
 * micro-batching of the mini-batch on dim 0 into ``chunks`` micro-batches;
 * synchronous fill-drain: every forward of the step, then every backward in
@@ -34,10 +37,14 @@ activations cost nothing, and the extra boundary messages ride idle xGMI links.
 Optionally ``schedule="1f1b"`` (PipeDream-flush, ``virtual == 1``): same
 bubble, activation memory bounded by the number of stages instead of chunks.
 
-Transport: :class:`~mipipe.parallel.p2p.Channels` -- one communicator per link
-direction; all receives of a phase are posted before the first compute, in the
-order the peer sends, so each transfer lands while earlier micro-batches
-compute.  Per-stage busy time is measured with HIP events (bubble %).
+Transport (:func:`make_transport`): ``auto`` (default) = the IPC links, whose
+zero-copy receives are posted for the whole phase (a posted receive costs
+nothing: the consumer's stream waits only when it reaches the micro-batch);
+``rccl`` = :class:`~mipipe.parallel.p2p.Channels`, one communicator per link
+direction, each receive posted just before the action that consumes it (a
+posted RCCL receive is a kernel resident on CUs until its data lands, so it
+is kept out of the way of the GEMMs until needed).  Per-stage busy time is
+measured with HIP events (bubble %).
 """
 from __future__ import annotations
 
@@ -161,11 +168,13 @@ class PipelineEngine:
             data-parallel replicas pass their count, so the gradient all-reduce
             SUM is the mean (:mod:`mipipe.parallel.data_parallel`).
         transport: how activations and gradients move between ranks when the
-            engine builds its own channels: ``"rccl"`` (send/recv of the
-            process group; default) or ``"ipc"`` (device-memory IPC links,
-            :class:`~mipipe.parallel.ipc.IpcChannels`: DMA copies into the
-            receiver's slots, no RCCL kernels; works with several ranks on
-            one GPU).  ``transport_options`` go to the IpcChannels.
+            engine builds its own channels (:func:`make_transport`):
+            ``"auto"`` (default: self-tested IPC links, every rank falling
+            back to RCCL together on any failure), ``"rccl"`` (send/recv of
+            the process group) or ``"ipc"`` (device-memory IPC links,
+            :class:`~mipipe.parallel.ipc.IpcChannels`, without the self-test;
+            works with several ranks on one GPU).  ``transport_options`` go to
+            the IpcChannels.
     """
 
     def __init__(
@@ -187,7 +196,7 @@ class PipelineEngine:
         watchdog: Union[None, float, Watchdog] = None,
         sync_debug: Optional[bool] = None,
         grad_divisor: float = 1.0,
-        transport: str = "rccl",
+        transport: str = "auto",
         transport_options: Optional[dict] = None,
     ) -> None:
         if checkpoint not in ("always", "except_last", "never"):
@@ -425,24 +434,38 @@ class PipelineEngine:
         if self.watchdog is not None:
             self.watchdog.pending.clear()
 
-        # Post every activation receive of the forward phase up front, in the
-        # order the upstream rank sends them (chunk-major, micro-batch minor).
         recv_x = [[None] * m for _ in range(v)]
         recv_w = [[None] * m for _ in range(v)]
-        with label_range("post recvs: activations"):
-            # zero-copy transports (IPC links) hand out the receive slot itself as the
-            # buffer, held until the step ends: only with a slot per message of the step
-            zc = getattr(chan, "zero_copy", False) and getattr(chan, "slots", 0) >= m * v
-            for c in range(v):
-                if not self._first(c):
+        # zero-copy transports (IPC links) hand out the receive slot itself as the
+        # buffer, held until the step ends: only with a slot per message of the step
+        zc = getattr(chan, "zero_copy", False) and getattr(chan, "slots", 0) >= m * v
+
+        def post_act_recv(c: int, i: int) -> None:
+            if self._first(c) or recv_w[c][i] is not None:
+                return
+            if zc:
+                recv_x[c][i], work = chan.recv_act_view(self.act_shapes[c], self.act_dtype)
+            else:
+                recv_x[c][i] = self._new_act(c)
+                work = chan.recv_act(recv_x[c][i])
+            recv_w[c][i] = self._track(f"recv activation: virtual stage {self.vstage[c]} micro-batch {i} "
+                                       f"from rank {(self.rank - 1) % n}", work)
+
+        # A zero-copy receive only reserves a slot (the consumer's stream waits
+        # when it reaches the micro-batch), so every activation receive of the
+        # forward phase is posted up front, in the order the upstream rank sends
+        # them (chunk-major, micro-batch minor).  Any other receive (RCCL) is a
+        # kernel resident on CUs from its posting until its data lands, next to
+        # the GEMMs: those are posted lazily -- each before the action that
+        # consumes it, plus the next action's right after an action is issued
+        # (one action ahead, so the transfer still lands under compute).  Either
+        # way every link's receives are posted in the order its sender sends.
+        lazy = chan is not None and not zc
+        if chan is not None and zc:
+            with label_range("post recvs: activations"):
+                for c in range(v):
                     for i in range(m):
-                        if zc:
-                            recv_x[c][i], work = chan.recv_act_view(self.act_shapes[c], self.act_dtype)
-                        else:
-                            recv_x[c][i] = self._new_act(c)
-                            work = chan.recv_act(recv_x[c][i])
-                        recv_w[c][i] = self._track(f"recv activation: virtual stage {self.vstage[c]} micro-batch {i} "
-                                                   f"from rank {(self.rank - 1) % n}", work)
+                        post_act_recv(c, i)
         # ... and every skip receive (each skip has its own directed link).
         sk_rx: Dict = {}
         sk_grad_rx: Dict = {}
@@ -628,6 +651,13 @@ class PipelineEngine:
             stage_in[c][i] = rng[c][i] = skip_in[c][i] = skip_out[c][i] = None
 
         actions = self._actions_of(self.rank, training)
+
+        def post_for(kind: str, c: int, i: int) -> None:
+            if kind == "F":
+                post_act_recv(c, i)
+            else:
+                post_grad_recv(c, i)
+
         started_backward = False
         defer = ops.deferred_wgrad() if (training and self.defer_wgrad) else None
         wd = self.watchdog
@@ -635,9 +665,11 @@ class PipelineEngine:
         if armed is not None:
             armed.__enter__()
         try:
-            for kind, c, i in actions:
+            for idx, (kind, c, i) in enumerate(actions):
                 self._mark(f"{'forward' if kind == 'F' else 'backward'} virtual stage {self.vstage[c]} "
                            f"micro-batch {i}")
+                if lazy and kind == "F":
+                    post_act_recv(c, i)
                 if kind == "F":
                     with label_range(f"F vs{self.vstage[c]} mb{i}"), torch.set_grad_enabled(training):
                         forward(c, i)
@@ -647,9 +679,9 @@ class PipelineEngine:
                         if defer is not None:
                             defer.__enter__()
                         with label_range("post recvs: gradients"):
-                            if self.schedule == "gpipe":
-                                # Post all gradient receives of the drain phase at once,
-                                # in the downstream rank's send order (reverse).
+                            if self.schedule == "gpipe" and not lazy:
+                                # Post all (zero-copy) gradient receives of the drain phase at
+                                # once, in the downstream rank's send order (reverse).
                                 for cc in reversed(range(v)):
                                     for k in reversed(range(m)):
                                         post_grad_recv(cc, k)
@@ -658,6 +690,8 @@ class PipelineEngine:
                     with label_range(f"B vs{self.vstage[c]} mb{i}"):
                         post_grad_recv(c, i)
                         backward(c, i)
+                if lazy and idx + 1 < len(actions):
+                    post_for(*actions[idx + 1])  # one action ahead
                 if self.sync_debug and self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
             if defer is not None and started_backward:

@@ -14,7 +14,17 @@ For the chosen ``engine step`` range (default: the last one of each rank) the
 window runs from the earliest step start (host clock, shared by every process
 of a node) to the last kernel end of the step on any rank.  Per rank:
 
-* ``busy``     -- union of the rank's kernel intervals in the window (GPU time);
+* ``busy``     -- union of the rank's kernel intervals in the window (GPU time),
+  EXCLUDING the runtime's stream-operation kernels: on this ROCm a
+  ``hipStreamWaitValue64`` is dispatched as ``__amd_rocclr_streamOpsWait``, a
+  kernel that spins on a CU until the flag flips, and a
+  ``hipStreamWriteValue64`` as ``__amd_rocclr_streamOpsWrite`` -- counting the
+  spin as work understated the bubble;
+* ``spin``     -- union of those stream-op kernels (ms) and their counts
+  (``waits/writes`` per step), reported separately, with the runtime's copy
+  kernels (``copy k.``, ``__amd_rocclr_copyBuffer*``: a copy the runtime ran
+  on the CUs) and, with a memory-copy trace, the copies the DMA engines ran
+  (``DMA cp.``);
 * ``lead``     -- window start -> the rank's first kernel (fill: waiting for
   upstream activations);
 * ``tail``     -- the rank's last kernel -> window end (drain);
@@ -73,7 +83,15 @@ def load(db: str):
             label = name
         regions.append((label, a, b))
     kernels = con.execute("select start, end, name from kernels order by start").fetchall()
-    return regions, kernels
+    try:  # recorded with --memory-copy-trace (tools/profile_ranks.py --copy-trace)
+        copies = con.execute("select start, end, size from memory_copies order by start").fetchall()
+    except sqlite3.Error:
+        copies = []
+    return regions, kernels, copies
+
+
+_STREAM_OP = "__amd_rocclr_streamOps"
+_COPY_KERNEL = "__amd_rocclr_copy"
 
 
 def main() -> None:
@@ -88,7 +106,7 @@ def main() -> None:
     paths = sorted({p for pat in args.dbs for p in glob.glob(pat, recursive=True)})
     ranks = []
     for p in paths:
-        regions, kernels = load(p)
+        regions, kernels, dma = load(p)
         steps = sorted((a, b) for n, a, b in regions if n == "engine step")
         if not steps:
             print(f"{p}: no 'engine step' ranges (run with --marker-trace)")
@@ -103,18 +121,22 @@ def main() -> None:
             if ends:
                 limit = ends[0]
         # kernels of this step: started after the step began, before the limit
-        ks = [(a, b) for a, b, _ in kernels if s0 <= a < limit]
+        ks = [(a, b) for a, b, n in kernels if s0 <= a < limit and _STREAM_OP not in n]
+        ops = [(a, b, n) for a, b, n in kernels if s0 <= a < limit and _STREAM_OP in n]
+        copies = sum(1 for a, _, n in kernels if s0 <= a < limit and _COPY_KERNEL in n)
+        dmas = [(a, b, z) for a, b, z in dma if s0 <= a < limit]
         acts = [(n, a, b) for n, a, b in regions if s0 <= a and b <= s1 and n != "engine step"]
-        ranks.append((p, s0, s1, ks, acts))
+        ranks.append((p, s0, s1, ks, acts, ops, copies, dmas))
     if not ranks:
         return
     w0 = min(r[1] for r in ranks)
     w1 = max(max((b for _, b in r[3]), default=r[2]) for r in ranks)
     span = w1 - w0
     print(f"# window {span / 1e6:.3f} ms over {len(ranks)} rank(s)")
-    print(f"{'rank db':<40} {'busy ms':>8} {'lead ms':>8} {'tail ms':>8} {'bubble':>7}   host ms per action kind")
+    print(f"{'rank db':<40} {'busy ms':>8} {'lead ms':>8} {'tail ms':>8} {'bubble':>7} {'spin ms':>8} "
+          f"{'waits/writes':>12} {'copy k.':>7} {'DMA cp.':>7}   host ms per action kind")
     bubbles = []
-    for p, s0, s1, ks, acts in ranks:
+    for p, s0, s1, ks, acts, ops, copies, dmas in ranks:
         busy = _union(_clip(ks, w0, w1))
         b = _total(busy)
         lead = (busy[0][0] - w0) if busy else span
@@ -128,8 +150,12 @@ def main() -> None:
                 kinds[m.group(1)] += e - a
         host = ", ".join(f"{k} {v / 1e6:.2f}" for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]))
         name = p if len(p) <= 40 else "..." + p[-37:]
-        print(f"{name:<40} {b / 1e6:8.2f} {lead / 1e6:8.2f} {tail / 1e6:8.2f} {100 * bub:6.1f}%   {host}")
-    print(f"mean bubble {100 * sum(bubbles) / len(bubbles):.2f}%")
+        spin = _total(_union(_clip([(a, e) for a, e, _ in ops], w0, w1)))
+        nw = sum(1 for _, _, n in ops if "Wait" in n)
+        nwr = len(ops) - nw
+        print(f"{name:<40} {b / 1e6:8.2f} {lead / 1e6:8.2f} {tail / 1e6:8.2f} {100 * bub:6.1f}% {spin / 1e6:8.2f} "
+              f"{f'{nw}/{nwr}':>12} {copies:7d} {len(dmas):7d}   {host}")
+    print(f"mean bubble {100 * sum(bubbles) / len(bubbles):.2f}% (stream-op spin kernels excluded from busy)")
     if len(ranks) > 1:
         # ranks sharing one GPU (--shared-gpu): how full the device was
         dev = _union([iv for r in ranks for iv in _clip(r[3], w0, w1)])

@@ -38,6 +38,8 @@ def main() -> int:
     ap.add_argument("--nproc", type=int, required=True)
     ap.add_argument("--out", default="gpurun_out/profile_ranks")
     ap.add_argument("--no-profile", action="store_true", help="run the ranks without rocprofv3")
+    ap.add_argument("--copy-trace", action="store_true",
+                    help="also record the runtime's memory copies (--memory-copy-trace): which engine moved what")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     args = ap.parse_args()
     extra = [a for a in args.bench_args if a != "--"]
@@ -48,8 +50,9 @@ def main() -> int:
             args.nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(args.nproc)] + extra
         if not args.no_profile:
-            cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "-d", os.path.join(args.out, f"rank{r}"),
-                   "-o", "rank", "--"] + cmd
+            cmd = (["rocprofv3", "--kernel-trace", "--marker-trace"] + (["--memory-copy-trace"] if args.copy_trace
+                                                                          else [])
+                   + ["-d", os.path.join(args.out, f"rank{r}"), "-o", "rank", "--"] + cmd)
         procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT))
     rc = 0
     for p in procs:
