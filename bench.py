@@ -3,7 +3,9 @@
 
 Metric (BASELINE.json): tokens/sec for the 12-layer Transformer (d_model 4096,
 nhead 16) at PP = 1/2/4/8, plus the pipeline bubble.  One process per GPU,
-pipeline stages connected by RCCL send/recv, GPipe schedule, chunks = 4 x PP
+pipeline stages connected by self-tested device-memory IPC links (DMA copies
+into the receiver's slots; RCCL send/recv as the common fall-back), GPipe
+schedule, chunks = 4 x PP
 (BASELINE configs #2/#3: PP=2 chunks=8, PP=8 chunks=32), fixed micro-batch, so
 per-GPU work is constant as PP grows ("weak" scaling).
 
@@ -89,7 +91,7 @@ def parse():
     ap.add_argument("--chunks-per-rank", dest="virtual", default="auto",
                     help="model chunks per rank (looping placement); 'auto' = shortest simulated step")
     ap.add_argument("--impl", default="engine", choices=["engine", "pipe"],
-                    help="engine = one process per GPU over RCCL (default; what torchrun launches); "
+                    help="engine = one process per GPU (default; what torchrun launches); "
                          "pipe = the single-process mipipe.Pipe driving --gpus devices with peer copies")
     ap.add_argument("--watchdog", type=float, default=300.0,
                     help="seconds without pipeline progress before a rank reports its pending transfers and "
@@ -99,9 +101,10 @@ def parse():
                          "RCCL all-reduces overlapped with the deferred weight gradients). Default 1: PP = world")
     ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc"],
                     help="stage-boundary transport of the engine: auto (default) = self-tested device-memory IPC "
-                         "links (SDMA copies on the links' copy streams into the receiver's slots, command-processor "
-                         "stream waits: no CU taken from compute; profiles/cu_hold_r5.txt), every rank falling back "
-                         "to RCCL together if a link fails its self-test; rccl = send/recv of the process group "
+                         "links (payload and completion flag both DMA copies on the links' copy streams: no kernel "
+                         "there; the consumer's own stream waits for the flag; profiles/ipc_cu_free_r6.txt), every "
+                         "rank falling back to RCCL together if a link fails its set-up or self-test; rccl = "
+                         "send/recv of the process group "
                          "(each receive a resident kernel on CUs); ipc = the IPC links without the self-test "
                          "(mipipe.parallel.ipc)")
     ap.add_argument("--shared-gpu", action="store_true",
@@ -133,6 +136,8 @@ def parse():
 
 
 def main() -> int:
+    t_main = time.perf_counter()
+    startup = {}  # start-up breakdown (s), reported in the JSON
     args = parse()
     if os.environ.get("MIPIPE_BENCH_PROGRESS", "0") != "0":
         import faulthandler
@@ -207,14 +212,17 @@ def main() -> int:
     cost_fn = None
     unit_ms = None
     plan_report = None
+    startup["process_init"] = time.perf_counter() - t_main  # torch import, process group
     if plan_mode == "measured" and pp > 1:
         from mipipe.parallel.calibrate import CalibrationError, calibrated_costs, engine_unit_costs
 
+        t_ = time.perf_counter()
         try:
             unit_ms = calibrated_costs(cfg, mb, m, args.checkpoint, device=device, dtype=dtype)
             cost_fn = lambda split: engine_unit_costs(cfg, unit_ms, split)  # noqa: E731
         except CalibrationError as exc:  # raised on every rank alike: all fall back together
             print(f"warning: {exc}; planning with analytic costs", file=sys.stderr)
+        startup["calibration"] = time.perf_counter() - t_
     if args.virtual == "auto":
         virtual, plan = choose_virtual(cfg, pp, m, split_options=splits, bwd_ratio=bwd_ratio, micro_batch=mb,
                                        cost_fn=cost_fn, objective=args.plan_objective)
@@ -233,6 +241,7 @@ def main() -> int:
         from mipipe.parallel.calibrate import select_plan_by_emulation
         from mipipe.parallel.stage import candidate_plans
 
+        t_ = time.perf_counter()
         cands = candidate_plans(cfg, pp, m, bwd_ratio, mb, cost_fn, split_options=splits)
         if len(cands) > 1:
             plan, plan_report = select_plan_by_emulation(cfg, cands, prank, m, mb, args.checkpoint, unit_ms,
@@ -243,6 +252,7 @@ def main() -> int:
             plan_report = {"method": "one candidate within 6 % of the model's best: no emulation needed",
                            "candidates": [{"v": plan.virtual, "split_decoder": plan.split_decoder,
                                            "balance": list(plan.balance)}], "chosen": 0}
+        startup["plan_emulation"] = time.perf_counter() - t_
     from mipipe.parallel.watchdog import Watchdog
 
     wd = Watchdog(args.watchdog) if args.watchdog > 0 else None
@@ -254,9 +264,15 @@ def main() -> int:
         from mipipe.parallel.engine import make_transport
 
         item = torch.empty((), dtype=dtype).element_size()
+        t_ = time.perf_counter()
         early_chan, _, _ = make_transport(list(range(world)), device=device, chunks=m, virtual=virtual,
                                           recv_bytes=max(torch.Size(s_).numel() for s_ in act_shapes) * item,
                                           transport=args.transport, watchdog=wd)
+        startup["transport"] = time.perf_counter() - t_
+        if getattr(early_chan, "setup_s", None) is not None:  # IPC links: set-up / self-test split
+            startup["transport_link_setup"] = early_chan.setup_s
+            startup["transport_self_test"] = early_chan.selftest_s
+    t_ = time.perf_counter()
     torch.manual_seed(1234 + prank)  # same initial weights in every data-parallel replica
     # Build only this rank's chunks (analytic plan; nothing else is instantiated).
     from mipipe.models.long_skip import unet_pairs
@@ -292,6 +308,7 @@ def main() -> int:
                             skip_shapes={"skip": ((mb, S, E), dtype)}, watchdog=wd,
                             group=groups.channels if groups is not None else early_chan,
                             grad_divisor=dp, transport=args.transport)
+    startup["stages_and_engine"] = time.perf_counter() - t_
     # explicit recompute (issued before each gradient wait, as the engine does)
     from mipipe.pipeline import checkpoint_stop_for
     sim_t, sim_busy = simulate_step([plan.stage_cost(g) * 3.0 / (1.0 + bwd_ratio) for g in range(pp * virtual)],
@@ -335,6 +352,7 @@ def main() -> int:
 
     armed = wd.watch("bench start") if wd is not None else contextlib.nullcontext()
     armed.__enter__()
+    t_ = time.perf_counter()
     for k in range(args.warmup):
         mark(f"warmup step {k}")
         st = train_step()
@@ -343,6 +361,8 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     sync()
+    startup["warmup_steps"] = time.perf_counter() - t_
+    startup["total_before_timed_steps"] = time.perf_counter() - t_main
     tele = _telemetry(device) if on_gpu else None
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -420,7 +440,7 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": _scaling_label(cfg, args, pp, m, mb),
             "vs_baseline": round(value / REF_TOKENS_PER_S[args.checkpoint], 2) if ref_match else None,
             "dtype": args.dtype,
             "data": "synthetic (random tokens, random-init weights)",
@@ -431,10 +451,10 @@ def main() -> int:
                 "params": total_params,
                 "global_batch": m * mb * dp,
                 "tokens_per_gpu_per_step": m * mb * dp * S // max(1, world),
-                "micro_batch_note": ("enc12 default: 128 sequences at PP <= 4, 64 at PP = 8 (config #3: 128 predicts "
-                                     "6 % less there, profiles/plan_table_r5.txt), so the N = 8 run carries half the "
-                                     "per-GPU tokens of N <= 4" if cfg.name == "enc12_d4096" and not args.micro_batch
-                                     else None),
+                "micro_batch_note": ("enc12 default: 128 sequences at every N (chunks 4 x N), so every N carries "
+                                     "the same tokens per GPU per step (weak scaling); N = 8 also runs config #3's "
+                                     "'except_last' (see work_note and like_for_like)"
+                                     if cfg.name == "enc12_d4096" and not args.micro_batch else None),
                 "seq_len": S,
                 "micro_batch": mb,
                 "chunks": m,
@@ -458,6 +478,8 @@ def main() -> int:
                 "plan_costs": "measured (engine-context unit costs)" if cost_fn is not None else "analytic FLOPs",
                 "plan_selection": plan_report,
             },
+            "like_for_like": _like_for_like(cfg, args, pp, mb, unit_ms) if pp > 1 else None,
+            "startup_s": {k: round(v, 3) for k, v in startup.items()},
             "bubble_pct": None if bubble is None else round(bubble, 2),
             "work_note": (f"checkpoint={args.checkpoint!r} re-runs the forward of {stop_n} of {m} micro-batches: "
                           f"~{1.0 + stop_n / m / 3.0:.2f}x the per-GPU compute of a 'never' step (the PP=1 "
@@ -668,21 +690,58 @@ def _config(args):
     return cfg
 
 
+def _scaling_label(cfg, args, pp: int, m: int, mb: int) -> str:
+    """``weak`` when the tokens per GPU per step are what the same flags give at
+    N = 1 (default chunks 4 x PP, the same micro-batch at every N), ``strong``
+    when the whole job's tokens are (an explicit --chunks, or GPT-2-XL's fixed
+    config #4 chunks at PP = 8)."""
+    m1 = args.chunks or 4
+    n1 = m1 * (args.micro_batch or _default_micro_batch(cfg, 1))  # sequences per step at N = 1 (= per GPU)
+    per_gpu, total = m * mb / pp, m * mb * args.dp
+    if abs(per_gpu - n1) < 1e-9:
+        return "weak"
+    if abs(total - n1) < 1e-9:
+        return "strong"
+    # neither fixed (GPT-2-XL's config #4: chunks 8 at PP = 8): the closer one
+    return "weak" if abs(per_gpu / n1 - 1) <= abs(total / n1 - 1) else "strong"
+
+
+def _like_for_like(cfg, args, pp: int, mb: int, unit_ms):
+    """The PP = 1 rate at THIS run's micro-batch and checkpoint mode, for reading
+    an N > 1 value against N = 1 without mixing in a different micro-batch or
+    recompute share: one GPU running every unit of the model per micro-batch,
+    priced by the engine-context unit costs this run calibrated on its own GPUs
+    (mipipe.parallel.calibrate: recompute, weight-gradient flush, optimizer and
+    host issue included).  None where no costs were measured (analytic plan,
+    --shared-gpu rehearsals, CPU)."""
+    out = {"micro_batch": mb, "checkpoint": args.checkpoint, "pp1_tokens_per_s": None,
+           "source": "no measured unit costs in this run (analytic plan)"}
+    if unit_ms:
+        from mipipe.parallel.calibrate import engine_unit_costs
+
+        ms = sum(engine_unit_costs(cfg, unit_ms, False))  # one micro-batch through the whole model, one GPU
+        if ms > 0:
+            out["pp1_tokens_per_s"] = round(mb * cfg.seq_len / (ms / 1e3), 1)
+            out["source"] = ("engine-context unit costs calibrated in this run (ms per micro-batch, summed over "
+                             "the whole model): an estimate of the N = 1 rate at this micro-batch and checkpoint "
+                             "mode, not a separate N = 1 run")
+    return out
+
+
 def _default_micro_batch(cfg, pp: int = 1) -> int:
     # ref_main: the reference's own micro-batch (batch 32 / chunks 4 = 8 sequences).
     # enc12_d4096: 128 x 128 = 16,384 tokens per GEMM, sized for 288 GB of HBM (89 GiB peak at
     # PP=1): +3.5 % for 64 over 32 (round 2), then +2.2 % for 128 over 64 at the power cap (the
     # optimizer, grad-norm and per-launch costs amortised over twice the tokens; same box,
-    # interleaved: profiles/microbatch_sizing.txt).  Except the full-node PP=8 run (config #3,
-    # 'except_last', chunks 32): there 128 predicts 817k job tok/s against 868k for 64 (every rank
-    # emulated, profiles/plan_table_r5.txt), so PP=8 keeps 64.
+    # interleaved: profiles/microbatch_sizing.txt).  The same 128 at every N, the full-node PP=8
+    # run included (config #3, 'except_last', chunks 32), so the scaling curve is weak scaling --
+    # the same tokens per GPU per step at every N -- although 64 predicts
+    # 868k job tok/s there against 817k for 128 (profiles/plan_table_r5.txt; --micro-batch 64).
     # gpt2_xl: 18 x 1024 tokens -- the 1600-wide GEMM outputs (attention out-proj, fc2 and
     # the dgrads into the residual stream) are 7 256-wide tile columns, so M = 18,432 makes
     # 504 tiles = 98 % of two rounds of the 256 CUs (8 x 1024: 224 tiles, 88 % of one):
     # PP=1 54.6k (mb 8) -> 58.3k (mb 9) -> 59.8k tok/s (mb 18), 208 GiB peak with
     # checkpoint='always' (profiles/microbatch_sizing.txt).
-    if cfg.name == "enc12_d4096" and pp == 8:
-        return 64
     return {"gpt2_xl": 18, "tiny": 8, "ref_main": 8}.get(cfg.name, 128)
 
 

@@ -1277,6 +1277,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm256_kernel(GemmArgs g) {
                          EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
 }
 
+#ifdef MIPIPE_GEMM_AB
 // ============================================================================
 // 4-wave variant: the same 256x256x64 block tile, LDS
 // images, staging offsets and epilogues, computed by 4 waves instead of 8 --
@@ -1569,6 +1570,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(GemmArgs g) {
     staged_store<EPI, W, NJ, 256, true>(smem, acc, wm, wn, lane, tid, m0, n0, g.M, g.N, g.ldc, out,
                                   EPI == kEpiStoreBf16 ? reinterpret_cast<const bf16_t*>(g.res) : nullptr, g.ldr);
 }
+#endif  // MIPIPE_GEMM_AB (the 4-wave kernel: A/B builds only, profiles/gemm4w_r5.txt)
 
 }  // namespace big
 
@@ -1624,17 +1626,24 @@ void launch_big(const GemmArgs& g, hipStream_t s) {
 // whole-tile ping-pong).  The A/B schedules 0-6 are compiled in only with
 // -DMIPIPE_GEMM_AB (python -m mipipe.build --gemm-ab), for tools/gemm_sched_ab.py
 // and the like; without it gemm_set_schedule() accepts 7 alone.
-// 256-wide blocks: the 4-wave kernel (gemm4w_kernel) or the 8-wave one.
-// gemm_set_waves(4 / 8) or MIPIPE_GEMM_WAVES picks; 0 = default (8).
+// 256-wide blocks: the 4-wave kernel (gemm4w_kernel, -DMIPIPE_GEMM_AB builds
+// only: 2-11 % slower at the power cap, profiles/gemm4w_r5.txt) or the 8-wave
+// one.  gemm_set_waves(4 / 8) or MIPIPE_GEMM_WAVES picks in an A/B build; the
+// product build has the 8-wave kernel alone.
 int g_gemm_waves = -1;
 int gemm_waves() {
+#ifdef MIPIPE_GEMM_AB
   if (g_gemm_waves < 0) {
     const char* e = getenv("MIPIPE_GEMM_WAVES");
     g_gemm_waves = e ? atoi(e) : 0;
   }
   return g_gemm_waves == 4 ? 4 : 8;
+#else
+  return 8;
+#endif
 }
 
+#ifdef MIPIPE_GEMM_AB
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA, int X = 0>
 void launch_4w(const GemmArgs& g, hipStream_t s) {
   constexpr int smem = big::kSmemBytes;  // the epilogue's staging image (130 KiB); the main loop uses 128 KiB
@@ -1647,10 +1656,12 @@ void launch_4w(const GemmArgs& g, hipStream_t s) {
   hipLaunchKernelGGL((big::gemm4w_kernel<A_KC, B_KC, EPI, ACT, EXTRA, X>), dim3(big_tiles(g, 256), g.k_splits),
                      dim3(256), smem, s, g);
 }
+#endif
 
 template <bool A_KC, bool B_KC, int EPI, int ACT, bool EXTRA>
 void launch_big_w(const GemmArgs& g, hipStream_t s) {
   const bool narrow = big_width(g) == 128;
+#ifdef MIPIPE_GEMM_AB
   if (!narrow && g.at == nullptr && gemm_waves() == 4) {
     if constexpr (A_KC && !B_KC && EPI != kEpiStoreBf16 && !EXTRA) {
       if (g.colsum != nullptr) {
@@ -1661,6 +1672,7 @@ void launch_big_w(const GemmArgs& g, hipStream_t s) {
     launch_4w<A_KC, B_KC, EPI, ACT, EXTRA>(g, s);
     return;
   }
+#endif
   if constexpr (A_KC && B_KC && EPI == kEpiStoreBf16 && !(ACT == kActGelu && EXTRA)) {
     if (g.at != nullptr) {  // forward GEMM that also writes A^T (gemm_emit_ok)
       if (narrow) launch_big<A_KC, B_KC, EPI, ACT, 4, 128, EXTRA, big::kXEmit>(g, s);
@@ -1823,7 +1835,7 @@ bool gemm_ab_build() {
 }
 void gemm_set_width(int w) { g_gemm_width = w; }
 void gemm_set_rounds(int on) { g_gemm_rounds = on; }
-void gemm_set_waves(int w) { g_gemm_waves = w; }
+void gemm_set_waves(int w) { g_gemm_waves = w; }  // 4 takes effect in -DMIPIPE_GEMM_AB builds only
 int gemm_get_waves() { return gemm_waves(); }
 void gemm_set_splitk(int n) { g_gemm_splitk = n; }
 int gemm_get_schedule() { return big::gemm_sched(); }

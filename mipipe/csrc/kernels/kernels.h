@@ -184,7 +184,7 @@ bool gemm_set_schedule(int mode);
 bool gemm_ab_build();
 void gemm_set_width(int w);    // 256-row GEMM block width: 0 auto, 128, 256
 void gemm_set_rounds(int on);  // 1: multi-round grids launched one round at a time (default), 0: one launch
-void gemm_set_waves(int w);   // 256x256 GEMM blocks: 4 (gemm4w_kernel, 128x128 per wave) or 8 waves; 0 default
+void gemm_set_waves(int w);   // 256x256 GEMM blocks: 4 (gemm4w_kernel, -DMIPIPE_GEMM_AB builds only) or 8 waves; 0 default
 int gemm_get_waves();
 void gemm_set_splitk(int n);  // split-K factor: 0 off, 1 auto (gemm_splitk_factor), n >= 2 forced (A/B tools)
 int gemm_get_schedule();

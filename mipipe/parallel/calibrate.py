@@ -370,7 +370,7 @@ def calibrated_costs(cfg: LMConfig, micro_batch: int, chunks: int, checkpoint: s
             costs = measure_engine_costs(cfg, micro_batch, chunks, checkpoint, device=device, dtype=dtype)
         costs = {k: float(costs[k]) for k in kinds}
     except Exception as exc:  # noqa: BLE001 -- reported on every rank below, identically
-        ok, err, costs = 0.0, exc, {k: 0.0 for k in kinds}
+        ok, err, costs = 0.0, repr(exc), {k: 0.0 for k in kinds}  # the text: no traceback keeps tensors alive
     if distributed:
         # ONE collective whatever happened locally: a rank whose measurement
         # failed must not leave the others waiting in a different collective
@@ -380,10 +380,10 @@ def calibrated_costs(cfg: LMConfig, micro_batch: int, chunks: int, checkpoint: s
         n = dist.get_world_size(group)
         if vec[0] < n:
             raise CalibrationError(f"calibration failed on {n - int(vec[0])} of {n} ranks"
-                                   + (f" (here: {err!r})" if err is not None else ""))
+                                   + (f" (here: {err})" if err is not None else ""))
         costs = {k: v / n for k, v in zip(kinds, vec[1:])}
     elif err is not None:
-        raise CalibrationError(f"calibration failed: {err!r}") from err
+        raise CalibrationError(f"calibration failed: {err}")
     if found is None and (not distributed or dist.get_rank() == 0):
         try:
             os.makedirs(cache_dir, exist_ok=True)
@@ -476,7 +476,15 @@ def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int,
             for i, plan in enumerate(candidates):
                 walls[i * pp + prank] = float(emulate(plan, prank))
         except Exception as exc:  # noqa: BLE001 -- reported on every rank below, identically
-            err = exc
+            # the text only: the exception's traceback holds the emulation's frames (stages, optimizer, engine
+            # GPU tensors) alive in a cycle
+            err = repr(exc)
+            del exc
+            import gc
+
+            gc.collect()
+            if device.type == "cuda":
+                torch.cuda.empty_cache()
             walls[-1] = 1.0
     distributed = dist.is_available() and dist.is_initialized()
     if distributed:
@@ -486,7 +494,7 @@ def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int,
         walls = w.cpu()
     report = {"method": "emulated rank walls (loop-back engine), IPC hop", "candidates": []}
     if walls[-1] > 0:
-        report["method"] = "model (emulation failed" + (f": {err!r}" if err is not None else " on another rank") + ")"
+        report["method"] = "model (emulation failed" + (f": {err}" if err is not None else " on another rank") + ")"
         return candidates[0], report
     stop = checkpoint_stop_for(checkpoint, chunks)
     hop = HOP_LATENCY_MS + micro_batch * cfg.seq_len * cfg.d_model * 2 / HOP_BYTES_PER_S * 1e3

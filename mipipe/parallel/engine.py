@@ -760,17 +760,20 @@ def make_transport(ranks: Sequence[int], *, device: torch.device, chunks: int, v
     does).  ``recv_bytes``: the largest activation this rank receives per
     micro-batch.  Collective over ``ranks``.
 
-    ``transport="auto"``: stage boundaries that take no CU from compute.
-    An RCCL receive is a kernel that spins on its CUs until the data lands
-    (footprint of torch's ``rcclGenericKernel``: 256 threads, 19.7 KiB LDS,
-    ~270 registers -- it can never share a CU with a 256x256 GEMM block),
-    and the engine posts its receives ahead, so one stays resident through
-    most of a phase.  ``profiles/cu_hold_r5.txt`` measures what k such
-    blocks cost the PP=1 step.  The IPC links move data with the DMA engines
-    (the link's copy stream, ``sdma``: ``hipMemcpyDeviceToDeviceNoCU``) and
-    order it with command-processor stream waits: no CU at all -- the
-    reference's own design (copies on dedicated copy streams, event waits:
-    /root/reference/README.md:193-237, 332-369).  Ranks sharing one GPU
+    ``transport="auto"``: stage boundaries that keep kernels off the GEMMs'
+    CUs.  An RCCL send/receive is a kernel that spins on its CUs until the
+    data has moved (footprint of torch's ``rcclGenericKernel``: 256 threads,
+    19.7 KiB LDS, ~270 registers -- it can never share a CU with a 256x256
+    GEMM block); ``profiles/cu_hold_r5.txt`` measures what such a block
+    costs the PP=1 step.  The IPC links move the payload AND the completion
+    flag with the DMA engines (the link's copy stream, ``sdma``: two
+    ``hipMemcpyDeviceToDeviceNoCU`` copies -- no kernel on that stream); the
+    consumer's own stream waits for the flag in order with its work (a
+    ``hipStreamWaitValue64``, which this ROCm runs as a one-wave kernel that
+    spins only while that stream would idle anyway) and releases the slot
+    with one stream write per link and step (profiles/ipc_cu_free_r6.txt) --
+    the reference's own design (copies on dedicated copy streams, event
+    waits: /root/reference/README.md:193-237, 332-369).  Ranks sharing one GPU
     (rehearsals) copy on the producer's stream (``inline``).  The links are
     self-tested first (:meth:`IpcChannels.self_test`); if any rank fails,
     every rank falls back to RCCL and the note says why.  CPU: RCCL-style

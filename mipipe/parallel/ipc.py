@@ -178,6 +178,7 @@ class IpcChannels:
     """
 
     host_staged = False
+    setup_s = selftest_s = None  # set by verified_ipc
 
     def __init__(self, ranks: Sequence[int], wrap: bool = False, *, device: torch.device, recv_bytes: int,
                  slots: int = 64, engine: Optional[str] = None, timeout: float = 300.0) -> None:
@@ -519,15 +520,18 @@ def verified_ipc(make_ipc, make_fallback, device: torch.device):
     every rank always reaches the same agreement.  Returns ``(channels,
     reason)`` -- ``reason`` is ``None`` when IPC passed, else what failed on
     which rank (for the bench JSON).  Collective."""
+    t0 = time.perf_counter()
     try:
         chan = make_ipc()
     except LinkSetupError as exc:
         return make_fallback(), str(exc)
+    t1 = time.perf_counter()
     try:
         reason = chan.self_test()
     except Exception as exc:  # noqa: BLE001 -- every rank must still reach the agreement
         reason = f"self-test raised {type(exc).__name__}: {exc}"
     if _agree(reason is None, device):
+        chan.setup_s, chan.selftest_s = t1 - t0, time.perf_counter() - t1  # for the bench's start-up breakdown
         return chan, None
     why = _reasons(reason)
     chan.abort()  # not closed: a link that failed may never drain; process teardown unmaps it

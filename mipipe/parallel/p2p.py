@@ -1,4 +1,5 @@
-"""Point-to-point transport between pipeline ranks over RCCL.
+"""Point-to-point transport between pipeline ranks over RCCL:
+the engine's ``transport="rccl"`` and the common fall-back of ``"auto"``.
 
 On ROCm the ``nccl`` backend of ``torch.distributed`` *is* RCCL; between two
 MI355X GPUs of a node a send/recv pair moves over the single xGMI link that

@@ -370,9 +370,12 @@ class Pipe(nn.Module):
 
     # -- streams -------------------------------------------------------------------
     def _ensure_copy_streams(self) -> List[List[AbstractStream]]:
-        """One dedicated copy stream per (partition, micro-batch), created once and
-        cached -- reusing streams keeps the caching allocator's per-stream pools
-        small (``/root/reference/pipe.py:417-424``)."""
+        """Copy streams per (partition, micro-batch), created once and cached --
+        reusing streams keeps the caching allocator's per-stream pools small
+        (``/root/reference/pipe.py:417-424``).  ``copy_streams=None`` gives the
+        reference's one dedicated stream per (partition, micro-batch); the
+        default (1) shares one per partition across its micro-batches, a
+        measured deviation (profiles/pipe_gap_r5.txt)."""
         if not self._copy_streams:
             k = self.copy_streams_per_partition
             for device in self.devices:

@@ -81,6 +81,18 @@ def test_bench_json_contract(nproc, extra, expect):
     assert REQUIRED <= set(rec)
     assert rec["n_gpus"] == nproc and rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    # weak scaling means the same tokens per GPU per step as the N = 1 run of the same flags (chunks 4 x N)
+    assert rec["config"]["tokens_per_gpu_per_step"] == 4 * rec["config"]["micro_batch"] * rec["config"]["seq_len"]
+    # start-up breakdown, and (N > 1) the PP = 1 rate at this run's micro-batch / checkpoint
+    su = rec["startup_s"]
+    assert su["total_before_timed_steps"] >= su["warmup_steps"] >= 0 and su["process_init"] >= 0
+    if nproc > 1:
+        lfl = rec["like_for_like"]
+        assert lfl["micro_batch"] == rec["config"]["micro_batch"] and lfl["checkpoint"] == rec["config"]["checkpoint"]
+        assert "pp1_tokens_per_s" in lfl and lfl["source"]
+        assert "transport" in su or "--skips" in extra  # with skips the engine builds its links itself
+    else:
+        assert rec["like_for_like"] is None
     cfg = rec["config"]
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(cfg)
     assert cfg["parallelism"] == f"pp{nproc}"
@@ -179,3 +191,28 @@ def test_bench_emulated_plan_pick_cpu(tmp_path):
     else:
         chosen = sel["candidates"][0]
     assert chosen["v"] == cfg["virtual_chunks_per_rank"] and chosen["balance"] == cfg["balance"]
+    # measured costs: the like-for-like PP = 1 rate is priced from them, and the start-up is broken down
+    assert rec["like_for_like"]["pp1_tokens_per_s"] > 0
+    assert {"calibration", "plan_emulation", "transport", "warmup_steps"} <= set(rec["startup_s"])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_scaling_label_and_default_micro_batch(n):
+    """The default enc12 run keeps 128 sequences per micro-batch and 4 x N chunks at every N: the same tokens per
+    GPU per step, so 'weak' is the truthful label at N = 1, 2, 4, 8; an explicit --chunks
+    fixes the job's work instead ('strong')."""
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from mipipe.models import CONFIGS
+
+    cfg = CONFIGS["enc12_d4096"]
+    mb = bench._default_micro_batch(cfg, n)
+    assert mb == 128
+    ns = argparse.Namespace(chunks=None, micro_batch=None, dp=1)
+    assert bench._scaling_label(cfg, ns, n, 4 * n, mb) == "weak"
+    fixed = argparse.Namespace(chunks=8, micro_batch=None, dp=1)
+    assert bench._scaling_label(cfg, fixed, n, 8, mb) == ("weak" if n == 1 else "strong")
