@@ -455,11 +455,15 @@ class PipelineEngine:
         # when it reaches the micro-batch), so every activation receive of the
         # forward phase is posted up front, in the order the upstream rank sends
         # them (chunk-major, micro-batch minor).  Any other receive (RCCL) is a
-        # kernel resident on CUs from its posting until its data lands, next to
-        # the GEMMs: those are posted lazily -- each before the action that
-        # consumes it, plus the next action's right after an action is issued
-        # (one action ahead, so the transfer still lands under compute).  Either
-        # way every link's receives are posted in the order its sender sends.
+        # kernel on CUs, ordered on the GPU after the work the compute stream
+        # had when it was posted and resident until its data lands: those are
+        # posted one action ahead -- the next action's receive just BEFORE an
+        # action is issued, so its kernel starts with that action and its
+        # transfer lands under that action's compute (posted after it, the
+        # transfer would sit exposed between the two actions; posted per phase,
+        # the kernel would stay resident across every wait of the phase).
+        # profiles/rccl_fallback_r6.txt prices the choice.  Either way every
+        # link's receives are posted in the order its sender sends.
         lazy = chan is not None and not zc
         if chan is not None and zc:
             with label_range("post recvs: activations"):
@@ -668,8 +672,12 @@ class PipelineEngine:
             for idx, (kind, c, i) in enumerate(actions):
                 self._mark(f"{'forward' if kind == 'F' else 'backward'} virtual stage {self.vstage[c]} "
                            f"micro-batch {i}")
-                if lazy and kind == "F":
-                    post_act_recv(c, i)
+                if lazy:
+                    post_for(kind, c, i)  # (normally posted one action ago)
+                    if idx + 1 < len(actions):
+                        nk, nc, ni = actions[idx + 1]
+                        if nk == "F" or out_meta[nc][ni] is not None:  # a gradient needs its forward's shape
+                            post_for(nk, nc, ni)
                 if kind == "F":
                     with label_range(f"F vs{self.vstage[c]} mb{i}"), torch.set_grad_enabled(training):
                         forward(c, i)
@@ -690,8 +698,6 @@ class PipelineEngine:
                     with label_range(f"B vs{self.vstage[c]} mb{i}"):
                         post_grad_recv(c, i)
                         backward(c, i)
-                if lazy and idx + 1 < len(actions):
-                    post_for(*actions[idx + 1])  # one action ahead
                 if self.sync_debug and self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
             if defer is not None and started_backward:
