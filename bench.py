@@ -64,6 +64,10 @@ def parse():
                          "and gpt2_xl)")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--num-layers", type=int, default=None, help="override the model's layer count (tests)")
+    ap.add_argument("--act-dropout", type=float, default=None,
+                    help="override the dropout between the MLP's activation and its second linear (default: the "
+                         "config's -- enc12 / ref_main: = dropout, as torch's TransformerEncoderLayer; gpt2_xl: 0, "
+                         "as GPT-2's MLP)")
     ap.add_argument("--chunks", type=int, default=None, help="micro-batches per step (default 4 x PP)")
     ap.add_argument("--checkpoint", default="auto", choices=["auto", "never", "except_last", "always"],
                     help="auto = the BASELINE.json config for this model and PP: enc12 'except_last' at PP=8 "
@@ -446,7 +450,9 @@ def main() -> int:
             "data": "synthetic (random tokens, random-init weights)",
             "config": {
                 "model": f"{cfg.name}: {cfg.num_layers}x {'causal decoder' if cfg.causal else 'TransformerEncoder'}Layer(d_model={E}, nhead={cfg.nhead}, "
-                         f"dim_feedforward={cfg.dim_feedforward}, dropout={cfg.dropout}, {cfg.activation}, "
+                         f"dim_feedforward={cfg.dim_feedforward}, dropout={cfg.dropout}"
+                         f"{'' if cfg.act_dropout is None else f' (after the activation: {cfg.act_dropout})'}, "
+                         f"{cfg.activation}, "
                          f"{'pre' if cfg.norm_first else 'post'}-norm) + embedding/decoder V={V}",
                 "params": total_params,
                 "global_batch": m * mb * dp,
@@ -687,6 +693,8 @@ def _config(args):
         cfg.seq_len = args.seq_len
     if args.num_layers:
         cfg.num_layers = args.num_layers
+    if getattr(args, "act_dropout", None) is not None:
+        cfg.act_dropout = args.act_dropout
     return cfg
 
 

@@ -21,7 +21,7 @@ from torch import Tensor, nn
 
 from .. import ops
 from ..ops.linear import mark_gemm_weight
-from .transformer import transformer_blocks
+from .transformer import FeedForwardBlock, transformer_blocks
 
 __all__ = [
     "Encoder",
@@ -175,6 +175,10 @@ class LMConfig:
     causal: bool = False
     learned_positions: bool = False
     scale_embedding: bool = True
+    # dropout between the MLP's activation and its second linear: None = `dropout` (torch's
+    # TransformerEncoderLayer: linear2(dropout(act(linear1(x))))); GPT-2's MLP has none there
+    # (c_fc -> gelu -> c_proj -> resid dropout)
+    act_dropout: Optional[float] = None
     notes: str = ""
 
     def params(self) -> int:
@@ -194,7 +198,9 @@ CONFIGS = {
     "ref_main": LMConfig("ref_main", 16, 2048, 32, 2048, 28782, 128, notes="reference main.py model"),
     # BASELINE.json config #4: GPT-2-XL 1.5B (pre-norm, causal, GELU, learned positions).
     "gpt2_xl": LMConfig("gpt2_xl", 48, 1600, 25, 6400, 50257, 1024, dropout=0.1, activation="gelu",
-                        norm_first=True, causal=True, learned_positions=True, scale_embedding=False),
+                        norm_first=True, causal=True, learned_positions=True, scale_embedding=False,
+                        act_dropout=0.0,
+                        notes="GPT-2's block: attention / residual / embedding dropout 0.1, none after the GELU"),
     # Tiny config for smoke tests.
     "tiny": LMConfig("tiny", 2, 256, 4, 512, 1000, 64, dropout=0.1),
 }
@@ -210,6 +216,10 @@ def build_lm_blocks(cfg: LMConfig, *, device=None, dtype=None) -> List[nn.Module
     blocks += transformer_blocks(cfg.num_layers, cfg.d_model, cfg.nhead, cfg.dim_feedforward, cfg.dropout,
                                  cfg.activation, norm_first=cfg.norm_first, causal=cfg.causal,
                                  device=device, dtype=dtype)
+    if cfg.act_dropout is not None:
+        for b in blocks:
+            if isinstance(b, FeedForwardBlock):
+                b.fc_in.dropout = cfg.act_dropout
     if cfg.norm_first:
         blocks.append(FinalNorm(cfg.d_model, device=device, dtype=dtype))
     blocks.append(Decoder(cfg.vocab, cfg.d_model, device=device, dtype=dtype))
