@@ -3,7 +3,9 @@ ADVICE r5): a rank whose link construction or self-test fails -- here an
 injected fault (``MIPIPE_IPC_FAULT=<phase>:<rank>``) -- must make EVERY rank
 fall back together, within seconds, instead of leaving the others in a
 barrier until the watchdog ends the job.  Host-mode links (shared memory)
-over gloo: the same agreement code the device links go through."""
+over gloo: the same agreement code the device links go through; the GPU cases
+run the device links (ranks sharing one MI355X) through the same agreement,
+with the real self-test."""
 import os
 import socket
 import time
@@ -22,40 +24,45 @@ def _port() -> int:
     return p
 
 
-def _worker(rank, world, port, fault, q):
+def _worker(rank, world, port, fault, q, gpu=False, engine=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if fault:
         os.environ["MIPIPE_IPC_FAULT"] = fault
+    if gpu:
+        torch.cuda.set_device(0)  # every rank on the one GPU (RCCL refuses that: gloo for the agreement)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mipipe.parallel.ipc import IpcChannels, verified_ipc
 
-        dev = torch.device("cpu")
+        dev = torch.device("cuda", 0) if gpu else torch.device("cpu")
         t0 = time.perf_counter()
-        chan, why = verified_ipc(lambda: IpcChannels(list(range(world)), device=dev, recv_bytes=1024, slots=4),
+        chan, why = verified_ipc(lambda: IpcChannels(list(range(world)), device=dev, recv_bytes=1 << 20, slots=4,
+                                                     engine=engine),
                                  lambda: "fallback", dev)
         dt = time.perf_counter() - t0
         kind = "fallback" if chan == "fallback" else type(chan).__name__
         if kind == "IpcChannels":
             # the links carry a message each way after passing
-            x = torch.full((256,), float(rank))
+            x = torch.full((256,), float(rank), device=dev)
             if rank + 1 < world:
-                chan.send_act(x)
+                chan.send_act(x).wait()
             if rank > 0:
-                y = torch.empty(256)
+                y = torch.empty(256, device=dev)
                 chan.recv_act(y).wait()
-                assert torch.equal(y, torch.full((256,), float(rank - 1)))
+                if gpu:
+                    torch.cuda.synchronize()
+                assert torch.equal(y.cpu(), torch.full((256,), float(rank - 1)))
             chan.close()
         q.put((rank, kind, why, dt))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, fault):
+def _run(world, fault, gpu=False, engine=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fault, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fault, q, gpu, engine)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -85,3 +92,23 @@ def test_ipc_setup_fault_on_one_rank_falls_back_everywhere(fault):
         assert dt < 30.0, (r, dt)
     if phase != "selftest":
         assert all("set-up failed" in why for _, why, _ in out.values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["sdma", "inline"])
+def test_gpu_ipc_links_pass_and_carry(engine):
+    """Device links of 3 ranks on one MI355X: set-up, the real self-test (every word of a whole-slot message per
+    link), then a message each way."""
+    out = _run(3, None, gpu=True, engine=engine)
+    assert all(kind == "IpcChannels" and why is None for kind, why, _ in out.values()), out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", ["attach:1", "selftest:0"])
+def test_gpu_ipc_setup_fault_falls_back_everywhere(fault):
+    """A fault on one rank's device links: every rank gets the fall-back within seconds."""
+    out = _run(3, fault, gpu=True, engine="sdma")
+    _, bad = fault.split(":")
+    for r, (kind, why, dt) in out.items():
+        assert kind == "fallback" and f"rank {bad}" in why and "injected fault" in why, (r, out)
+        assert dt < 60.0, (r, dt)
