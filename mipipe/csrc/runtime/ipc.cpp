@@ -265,7 +265,9 @@ std::unique_ptr<Link> Link::attach(const std::string& name, int device, int engi
     for (size_t i = 0; i < tags.size(); ++i) tags[i] = lap_tag(i < tags.size() / 2 ? 0 : 1);
     check(hipMemcpy(w, tags.data(), size_t(2 * kFlagStride), hipMemcpyHostToDevice), "hipMemcpy(lap tags)");
     L->tags_ = static_cast<char*>(w);
-    check(hipStreamCreateWithFlags(&L->copy_stream_, hipStreamNonBlocking), "hipStreamCreate(copy)");
+    // from the runtime's process-lifetime pool, never destroyed: torch's caching allocator records events on it
+    // for every send source (record_stream) and may do so after the link is gone, when such a tensor is freed
+    L->copy_stream_ = rt::stream_acquire(device, 0);
     const int64_t n = sh->nslots;
     L->events_ = new hipEvent_t[n];
     for (int k = 0; k < n; ++k)
@@ -313,7 +315,7 @@ Link::~Link() {
       }
       if (events_)
         for (int64_t k = 0; k < sh_->nslots; ++k) (void)hipEventDestroy(events_[k]);
-      if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
+      // copy_stream_ belongs to the runtime's stream pool (see attach)
     }
   } catch (...) {
   }

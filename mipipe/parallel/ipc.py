@@ -315,6 +315,13 @@ class IpcChannels:
         r = self.rank
         prev_g, next_g = self.ranks[(r - 1) % n], self.ranks[(r + 1) % n]
         t0 = time.perf_counter()
+
+        def left() -> float:
+            # a send whose slot is still held blocks the host (the release counter is polled): within the
+            # self-test's budget, so a peer that never releases -- it failed before its own self-test -- ends
+            # this one in time too (the exception becomes the reason in verified_ipc)
+            return max(0.1, timeout - (time.perf_counter() - t0))
+
         with torch.cuda.stream(side):
             for rd in range(rounds):
                 for kind, link, dst in (("act", self._act_out, next_g), ("grad", self._grad_out, prev_g)):
@@ -322,7 +329,7 @@ class IpcChannels:
                         continue
                     peer_slot = int(link.slot_bytes) // 4
                     msg = pattern(peer_slot, kind, me, dst, rd, dev)
-                    self._send(link, msg)
+                    self._send(link, msg, left())
                 for kind, link, src in (("act", self._act_in, prev_g), ("grad", self._grad_in, next_g)):
                     if link is None:
                         continue
@@ -342,14 +349,14 @@ class IpcChannels:
             for i in range(max([(-rounds) % int(link.nslots) for _, link, _ in outs + ins] or [0])):
                 for _, link, _ in outs:
                     if i < (-rounds) % int(link.nslots):
-                        self._send(link, filler)
+                        self._send(link, filler, left())
                 for _, link, _ in ins:
                     if i < (-rounds) % int(link.nslots):
                         _, work = self._recv_view(link, (64,), torch.int32)
                         work.wait()
                 self.end_step()
             for kind, link, dst in outs:
-                self._send(link, pattern(int(link.slot_bytes) // 4, kind, me, dst, rounds, dev))
+                self._send(link, pattern(int(link.slot_bytes) // 4, kind, me, dst, rounds, dev), left())
             for kind, link, src in ins:
                 words = int(link.slot_bytes) // 4
                 t, work = self._recv_view(link, (words,), torch.int32)
@@ -401,7 +408,7 @@ class IpcChannels:
             self._copy_streams[id(link)] = s
         return s
 
-    def _send(self, link, t: Tensor):
+    def _send(self, link, t: Tensor, timeout: Optional[float] = None):
         if link is None:
             raise RuntimeError(f"rank {self.rank}: no link in that direction")
         src = t.detach()
@@ -412,9 +419,10 @@ class IpcChannels:
             # source block alive until then
             if not link.inline_copy:
                 record_stream(src, self._copy_stream(link))
-            seq = link.send(src, torch.cuda.current_stream(src.device).cuda_stream, self.timeout)
+            seq = link.send(src, torch.cuda.current_stream(src.device).cuda_stream,
+                            self.timeout if timeout is None else timeout)
         else:
-            seq = link.send(src, 0, self.timeout)
+            seq = link.send(src, 0, self.timeout if timeout is None else timeout)
         return _SendWork(link, seq, src.device)
 
     def _recv(self, link, t: Tensor):
@@ -491,7 +499,8 @@ class IpcChannels:
             if stuck:
                 raise RuntimeError("mipipe ipc: links did not drain in 60 s: " + "; ".join(stuck))
             torch.cuda.synchronize(self.device)
-        # the ExternalStream wrappers go before the links destroy their streams
+        # the links' copy streams come from the runtime's process-lifetime pool (tensors recorded on them may
+        # outlive the links); only the wrappers go
         self._copy_streams = {}
         self._act_out = self._grad_out = None
         self._links = [x for x in self._links if not x.is_sender]

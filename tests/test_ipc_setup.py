@@ -25,6 +25,9 @@ def _port() -> int:
 
 
 def _worker(rank, world, port, fault, q, gpu=False, engine=None):
+    import faulthandler
+
+    faulthandler.enable()  # a crash in a rank prints where
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if fault:
         os.environ["MIPIPE_IPC_FAULT"] = fault
