@@ -115,3 +115,37 @@ def test_gpu_ipc_setup_fault_falls_back_everywhere(fault):
     for r, (kind, why, dt) in out.items():
         assert kind == "fallback" and f"rank {bad}" in why and "injected fault" in why, (r, out)
         assert dt < 60.0, (r, dt)
+
+
+def test_link_message_bytes_tagged_and_slot_reuse_host():
+    """One process, host-mode link pair over 2 slots: the byte count of a message is reported only while its
+    slot still holds it (-1 before it is sent, -2 once a later message took the slot), a send into a slot whose
+    message is not released yet waits (the release counter) and times out cleanly, and data survive reuse."""
+    import uuid
+
+    from mipipe import _native_loader
+
+    k = _native_loader.kernels()
+    name = f"/mipipe-test-{uuid.uuid4().hex[:8]}"
+    rx = k.IpcLink.create(name, -1, 2, 1024)
+    tx = k.IpcLink.attach(name, -1, 0, 5.0)
+    try:
+        a, b, c = (torch.full((n,), float(n), dtype=torch.float32) for n in (25, 50, 75))
+        assert tx.send(a, 0, 1.0) == 0 and tx.send(b, 0, 1.0) == 1
+        assert rx.message_bytes(0) == 100 and rx.message_bytes(1) == 200 and rx.message_bytes(2) == -1
+        with pytest.raises(RuntimeError, match="timed out"):
+            tx.send(c, 0, 0.2)  # slot 0 still holds message 0
+        s0, s1 = rx.post(), rx.post()
+        out = torch.empty(25)
+        rx.wait(s0, out, 0, 1.0)
+        assert torch.equal(out, a)
+        assert tx.send(c, 0, 1.0) == 2  # slot 0 again, after message 0's release
+        assert rx.message_bytes(0) == -2 and rx.message_bytes(2) == 300
+        out = torch.empty(50)
+        rx.wait(s1, out, 0, 1.0)
+        assert torch.equal(out, b)
+        out = torch.empty(75)
+        rx.wait(rx.post(), out, 0, 1.0)
+        assert torch.equal(out, c)
+    finally:
+        del tx, rx
