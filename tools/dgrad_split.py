@@ -14,12 +14,23 @@ groups = defaultdict(list)
 for i, (a, b, n, g) in enumerate(ks):
     if "gemm256_kernel<true, false, 0, 0" in n and g == 524288:
         prev = ks[i - 1][2]
-        prevs = ("ln_bwd" if "ln_bwd" in prev else "dgrad" if "gemm256_kernel<true, false, 0, 0" in prev else
-                 "attn_bwd" if "attn_bwd" in prev else prev[:40])
-        groups[f"dgrad after {prevs}"].append(b - a)
+        nxt = ks[i + 1][2] if i + 1 < len(ks) else ""
+        if "attn_bwd" in prev:
+            label = "qkv dgrad (after attention bwd)"
+        elif "gemm256_kernel<true, false, 0, 0" in prev:
+            label = "fc1 dgrad (+ residual gradient; after fc2's dgrad)"
+        elif "gemm256_kernel<true, false, 0, 0" in nxt:
+            label = "fc2 dgrad (ReLU mask folded; before fc1's)"
+        elif "attn_bwd" in nxt:
+            label = "out-proj dgrad (plain; before attention bwd)"
+        else:
+            label = f"dgrad between {prev[:30]} and {nxt[:30]}"
+        groups[label].append(b - a)
     elif "gemm256_kernel<true, true, 0, 0" in n and g == 524288:
         groups["fwd out/fc2 (K 4096)"].append(b - a)
     elif "gemm256_kernel<true, true, 0, 1" in n and g == 524288:
         groups["fwd fc1 relu+dropout"].append(b - a)
 for k, v in sorted(groups.items()):
-    print(f"{k:<40} n={len(v):5d} median {statistics.median(v) / 1e3:8.1f} us  mean {statistics.mean(v) / 1e3:8.1f}")
+    q = statistics.quantiles(v, n=10) if len(v) > 1 else [v[0]] * 9
+    print(f"{k:<52} n={len(v):5d} median {statistics.median(v) / 1e3:8.1f} us  p10 {q[0] / 1e3:8.1f}  "
+          f"p90 {q[-1] / 1e3:8.1f}")
