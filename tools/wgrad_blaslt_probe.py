@@ -1,6 +1,7 @@
 """A/B: deferred weight-gradient GEMM (main_grad fp32 += dY^T X over 4 micro-batch
 segments) on the mipipe K-segmented kernel vs hipBLASLt through torch (bf16 in,
-fp32 out).  enc12_d4096 shapes: T = 4 x 4096 tokens."""
+fp32 out).  enc12_d4096 shapes: T = 4 x SEG tokens (argv[1], default 4096; the step's flush today: 16384).
+"addmm x4" accumulates one micro-batch segment per call (no concatenation copy)."""
 import statistics
 import sys
 
@@ -27,8 +28,8 @@ def timeit(fn, iters=10):
     return statistics.median(ts) * 1e3
 
 
-seg, nseg = 4096, 4
-for name, N, K in (("qkv", 12288, 4096), ("out", 4096, 4096), ("dec", 28928, 4096)):
+seg, nseg = (int(sys.argv[1]) if len(sys.argv) > 1 else 4096), 4
+for name, N, K in (("out", 4096, 4096), ("qkv", 12288, 4096)):
     dys = [torch.randn(seg, N, device="cuda").to(torch.bfloat16) for _ in range(nseg)]
     xs = [torch.randn(seg, K, device="cuda").to(torch.bfloat16) for _ in range(nseg)]
     main = torch.zeros(N, K, device="cuda")
@@ -42,6 +43,7 @@ for name, N, K in (("qkv", 12288, 4096), ("out", 4096, 4096), ("dec", 28928, 409
         ("addmm_new", lambda: torch.addmm(main, dyc.t(), xc, out_dtype=torch.float32)),
         ("cat+addmm", lambda: torch.addmm(main, torch.cat(dys).t(), torch.cat(xs), out_dtype=torch.float32, out=main)),
         ("mm_bf16", lambda: torch.mm(dyc.t(), xc)),
+        ("addmm x4", lambda: [torch.addmm(main, d.t(), x, out_dtype=torch.float32, out=main) for d, x in zip(dys, xs)]),
     ):
         try:
             t = timeit(fn)
