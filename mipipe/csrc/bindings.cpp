@@ -558,7 +558,8 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
                                                                            double p, bool save_preact,
                                                                            std::optional<Tensor> res,
                                                                            std::optional<Tensor> xt,
-                                                                           bool aux_grad) {
+                                                                           bool aux_grad,
+                                                                           std::optional<Tensor> bits) {
   check_gemm_2d(x, "x");
   check_gemm_2d(w, "w");
   check_same_dtype(x, w, "linear_fwd");
@@ -603,6 +604,15 @@ std::tuple<Tensor, std::optional<Tensor>, int64_t, int64_t> py_linear_fwd(Tensor
     g.at = xt->data_ptr();
     g.ldat = row_stride(*xt, "xt");
   }
+  if (bits) {  // the output's nonzero mask as bits, for the consumer's dgrad (kActReluBits)
+    check_cuda(*bits, "bits");
+    MP_CHECK(bits->scalar_type() == at::kByte && bits->dim() == 2 && bits->size(0) == M && bits->size(1) * 8 == N &&
+                 bits->stride(1) == 1,
+             "linear_fwd: bits must be uint8 [M, N / 8] with unit column stride");
+    g.bits = bits->data_ptr();
+    g.ldbits = bits->stride(0);
+    MP_CHECK(dt == at::kBFloat16 && gemm_bits_ok(g), "linear_fwd: this launch cannot write bits (gemm_bits_ok)");
+  }
   gemm_run(dt, g, cur_stream(x));
   return {y, pre, (int64_t)seed, (int64_t)offset};
 }
@@ -640,13 +650,21 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res, std::opti
     check_same_dtype(dy, *res, "linear_dgrad res");
     MP_CHECK(res->size(0) == M && res->size(1) == K, "linear_dgrad: res must be [M, K]");
   }
-  MP_CHECK(act == kActNone || act == kActRelu || act == kActGelu || act == kActSavedGrad, "linear_dgrad: bad act");
+  MP_CHECK(act == kActNone || act == kActRelu || act == kActGelu || act == kActSavedGrad || act == kActReluBits,
+           "linear_dgrad: bad act");
   if (act != kActNone) {
     MP_CHECK(saved.has_value() && dt == at::kBFloat16 && !res, "linear_dgrad: the activation backward needs bf16 "
              "operands, the saved tensor and no residual addend");
-    check_gemm_2d(*saved, "saved");
-    check_same_dtype(dy, *saved, "linear_dgrad saved");
-    MP_CHECK(saved->size(0) == M && saved->size(1) == K, "linear_dgrad: saved must be [M, K]");
+    if (act == kActReluBits) {
+      check_cuda(*saved, "saved");
+      MP_CHECK(saved->scalar_type() == at::kByte && saved->dim() == 2 && saved->size(0) == M &&
+                   saved->size(1) * 8 == K && saved->stride(1) == 1,
+               "linear_dgrad: the ReLU bit mask must be uint8 [M, K / 8] with unit column stride");
+    } else {
+      check_gemm_2d(*saved, "saved");
+      check_same_dtype(dy, *saved, "linear_dgrad saved");
+      MP_CHECK(saved->size(0) == M && saved->size(1) == K, "linear_dgrad: saved must be [M, K]");
+    }
     MP_CHECK(p >= 0.0 && p < 1.0, "linear_dgrad: bad p");
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
@@ -669,9 +687,9 @@ Tensor py_linear_dgrad(Tensor dy, Tensor w, std::optional<Tensor> res, std::opti
   g.a_kc = true; g.b_kc = false; g.epi = kEpiStoreAct;
   if (act != kActNone) {
     g.dact_in = saved->data_ptr();
-    g.ldd = row_stride(*saved, "saved");
+    g.ldd = act == kActReluBits ? saved->stride(0) : row_stride(*saved, "saved");
     g.dact = (int)act;
-    if (act == kActRelu) {  // the saved output's sign is the mask as well
+    if (act == kActRelu || act == kActReluBits) {  // the saved output's sign (or its bit) is the mask as well
       g.dact_scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
     } else {
       g.p = (float)p;
@@ -1252,7 +1270,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_width", &gemm_set_width, "256-row GEMM block width: 0 auto (grid-quantisation rule), 128, 256");
   m.def("linear_fwd", &py_linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("p"),
         py::arg("save_preact"), py::arg("res") = py::none(), py::arg("xt") = py::none(),
-        py::arg("aux_grad") = false);
+        py::arg("aux_grad") = false, py::arg("bits") = py::none());
+  m.def("linear_bits_ok",
+        [](int64_t M, int64_t N, int64_t K, int64_t act, double p) {
+          GemmArgs g;
+          g.M = (int)M; g.N = (int)N; g.K = (int)K; g.act = (int)act; g.p = (float)p;
+          g.a_kc = true; g.b_kc = true; g.epi = kEpiStoreAct;
+          return gemm_supported(M, N, K) && gemm_bits_ok(g);
+        },
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"), py::arg("p"),
+        "whether linear_fwd can also write the ReLU output's nonzero mask as bits (kActReluBits)");
   m.def("gemm_emit_ok", &gemm_emit_ok, py::arg("act"), py::arg("p"), py::arg("aux"),
         "whether linear_fwd can also write x^T for this activation / dropout / pre-activation output");
   m.def("linear_wgrad_xt_segments", &py_linear_wgrad_xt_segments, py::arg("dys"), py::arg("xts"),

@@ -244,7 +244,10 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (g.dact_in != nullptr)
+          if (g.dact_in != nullptr && g.dact == kActReluBits)
+            out[r] *= (reinterpret_cast<const uint8_t*>(g.dact_in)[(int64_t)(row0 + r) * g.ldd + (col >> 3)] >> (col & 7)) & 1
+                          ? g.dact_scale : 0.f;
+          else if (g.dact_in != nullptr)
             out[r] *= g.dact_scale *
                       dact_f(g.dact, bf2f(reinterpret_cast<const bf16_t*>(g.dact_in)[(int64_t)(row0 + r) * g.ldd + col]));
           if (g.res != nullptr) out[r] += bf2f(reinterpret_cast<const bf16_t*>(g.res)[(int64_t)(row0 + r) * g.ldr + col]);
@@ -501,7 +504,12 @@ __device__ __forceinline__ void staged_store(char* smem, const f32x4 (&acc)[8][N
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_grad_f(v[e]);
         }
-        if (dact_in != nullptr) {  // activation backward: x act'(saved)
+        if (dact_in != nullptr && dact == kActReluBits) {  // the ReLU (+ dropout) mask as bits: one byte
+          const uint32_t mb =
+              reinterpret_cast<const uint8_t*>(dact_in)[(int64_t)grow(row) * ldd + ((n0 + 8 * c8) >> 3)];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= (mb >> e) & 1 ? dact_scale : 0.f;
+        } else if (dact_in != nullptr) {  // activation backward: x act'(saved)
           const bf16x8 sv = *reinterpret_cast<const bf16x8*>(dact_in + (int64_t)grow(row) * ldd + n0 + 8 * c8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= dact_scale * dact_f(dact, (float)sv[e]);
@@ -656,6 +664,12 @@ __device__ __forceinline__ void staged_store_act(char* smem, const f32x4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
         *reinterpret_cast<bf16x8*>(C + (int64_t)row * g.ldc + col) = o;
+        if (g.bits != nullptr) {  // the output's nonzeros, for the consumer's dgrad (kActReluBits)
+          uint32_t mb = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mb |= (v[e] != 0.f ? 1u : 0u) << e;
+          reinterpret_cast<uint8_t*>(g.bits)[(int64_t)row * g.ldbits + (col >> 3)] = (uint8_t)mb;
+        }
       }
     }
     __syncthreads();
@@ -1848,6 +1862,11 @@ bool gemm_rowsum_ok(const GemmArgs& g) {
 // The A^T emission is compiled into every forward variant but the GELU one
 // with an extra epilogue (dropout / pre-activation output): that one would
 // spill its main loop's registers (scratch reloads inside the K loop).
+bool gemm_bits_ok(const GemmArgs& g) {
+  // the staged EXTRA epilogue of the 256-row kernel (dropout), one launch or per-round chunks of whole tiles
+  return g.epi == kEpiStoreBf16 && g.act == kActRelu && g.p > 0.f && g.k_splits <= 1 && g.N % 8 == 0 && use_big(g);
+}
+
 bool gemm_emit_ok(int act, float p, bool aux) { return !(act == kActGelu && (p > 0.f || aux)); }
 
 bool gemm_colsum_ok(const GemmArgs& g) {
@@ -1955,7 +1974,8 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
       c.bias = byte_off(g.bias, (int64_t)lo * 2);
       c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * 2));
       c.res = byte_off(g.res, (int64_t)lo * 2);
-      c.dact_in = byte_off(g.dact_in, (int64_t)lo * 2);
+      c.dact_in = byte_off(g.dact_in, g.dact == kActReluBits ? (int64_t)lo / 8 : (int64_t)lo * 2);
+      c.bits = const_cast<char*>(byte_off(g.bits, (int64_t)lo / 8));
     } else {
       c.M = hi - lo;
       c.mask_row0 = g.mask_row0 + lo;
@@ -1967,7 +1987,8 @@ bool launch_by_rounds(const GemmArgs& g, F&& run) {
       c.at = const_cast<char*>(byte_off(g.at, (int64_t)lo * 2));  // A^T columns of this chunk's rows
       c.aux = const_cast<char*>(byte_off(g.aux, (int64_t)lo * g.ldc * 2));
       c.res = byte_off(g.res, (int64_t)lo * g.ldr * 2);
-      c.dact_in = byte_off(g.dact_in, (int64_t)lo * g.ldd * 2);
+      c.dact_in = byte_off(g.dact_in, (int64_t)lo * g.ldd * (g.dact == kActReluBits ? 1 : 2));
+      c.bits = const_cast<char*>(byte_off(g.bits, (int64_t)lo * g.ldbits));
     }
     run(c);
   }

@@ -64,6 +64,10 @@ enum Activation : int { kActNone = 0, kActRelu = 1, kActGelu = 2 };
 // Backward-only activation code: the saved tensor IS act'(pre) (a GELU forward
 // GEMM wrote it with GemmArgs::aux_grad), so the backward is one multiply.
 constexpr int kActSavedGrad = 3;
+// Backward-only: the saved tensor is a 1-bit mask of a ReLU (+ dropout) output's nonzeros, [M][ld bytes], bit
+// (col & 7) of byte col / 8 -- written by the forward GEMM (GemmArgs::bits) so the consumer's dgrad epilogue
+// reads 1/16 of the bytes the saved bf16 output costs.
+constexpr int kActReluBits = 4;
 
 template <typename T>
 void bias_act_dropout_fwd(const T* x, const T* bias, T* y, int64_t rows, int cols, int act, float p, uint64_t seed,
@@ -163,12 +167,18 @@ struct GemmArgs {
   // (tools/wgrad_layout_probe.py).
   void* at = nullptr;
   int64_t ldat = 0;
+  // Forward ReLU + dropout (the EXTRA epilogue): also write the output's nonzero mask as bits (kActReluBits),
+  // [M][ldbits bytes]; gemm_bits_ok(g) says whether this launch can.
+  void* bits = nullptr;
+  int64_t ldbits = 0;
   const void* a_seg[kMaxSegs] = {};
   const void* b_seg[kMaxSegs] = {};
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 // True if gemm_bf16 can fold g.rowsum into g (the wgrad layout, no split-K, >= 16 tile columns).
 bool gemm_rowsum_ok(const GemmArgs& g);
+// True if this forward GEMM (ReLU, dropout, the staged EXTRA epilogue) can write GemmArgs::bits.
+bool gemm_bits_ok(const GemmArgs& g);
 // True if the forward GEMM with this epilogue can write A^T (GemmArgs::at).
 bool gemm_emit_ok(int act, float p, bool aux);
 // True if gemm_bf16 can fold g.colsum into g (B I-contiguous, fp32 out, no split-K, >= W/16 tile rows).

@@ -152,7 +152,11 @@ class ActFold:
 
     def ready_for(self, x2: Tensor) -> bool:
         s = self.saved
-        return s is not None and s.shape == x2.shape and s.dtype == x2.dtype == torch.bfloat16
+        if s is None or x2.dtype != torch.bfloat16:
+            return False
+        if self.act == KACT_RELU_BITS:  # the output's nonzeros as bits, [rows, cols / 8]
+            return s.dtype == torch.uint8 and tuple(s.shape) == (x2.shape[0], x2.shape[1] // 8)
+        return s.shape == x2.shape and s.dtype == x2.dtype
 
 
 class _Linear(torch.autograd.Function):
@@ -187,11 +191,18 @@ class _Linear(torch.autograd.Function):
             # GELU'(pre) itself on the bf16 path (aux_grad), so the backward --
             # a separate pass or the consumer's dgrad epilogue -- is one multiply
             aux_grad = _GELU_SAVE_GRAD and act == 2 and save and x2.dtype == torch.bfloat16
-            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2, xt, aux_grad)
+            # ReLU (+ dropout) folded into the consumer's dgrad: hand it the output's nonzeros as bits (1/16 of
+            # the bytes its epilogue would re-read from the bf16 output; profiles/gemm_roofline_r6.txt)
+            bits = None
+            if (fold_out is not None and act == 1 and p > 0.0 and save and _RELU_BITS and x2.dtype == torch.bfloat16
+                    and k.linear_bits_ok(x2.shape[0], w.shape[0], x2.shape[1], act, p)):
+                bits = torch.empty((x2.shape[0], w.shape[0] // 8), dtype=torch.uint8, device=x2.device)
+            y, preact, seed, offset = k.linear_fwd(x2, w, bias, act, p, act == 2 and save, r2, xt, aux_grad, bits)
             if aux_grad:
                 saved_act = KACT_SAVED_GRAD
             res = None  # added in the epilogue
         else:
+            bits = None
             y = torch.matmul(x2, w.t())
             if act != 0 or p > 0.0 or bias is not None:
                 pre_bias = y
@@ -206,7 +217,10 @@ class _Linear(torch.autograd.Function):
         ctx.fold_out = ctx.fold_in = None
         fold_saved = None
         if fold_out is not None and fused_tile and act != 0 and x2.dtype == torch.bfloat16 and saved is not None:
-            fold_out.offer(saved_act, saved, p, seed, offset)
+            if bits is not None:
+                fold_out.offer(KACT_RELU_BITS, bits, p, seed, offset)
+            else:
+                fold_out.offer(saved_act, saved, p, seed, offset)
             ctx.fold_out = fold_out
         if fold_in is not None and fused_tile and fold_in.ready_for(x2) and ctx.needs_input_grad[0]:
             ctx.fold_in = fold_in
@@ -339,6 +353,10 @@ _XT_MIN_TILES = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_TILES", "0"))
 # backward folds into the consumer's dgrad (GELU without dropout after it).
 _GELU_SAVE_GRAD = os.environ.get("MIPIPE_GELU_SAVE_GRAD", "0") == "1"
 KACT_SAVED_GRAD = 3  # kernels.h kActSavedGrad
+KACT_RELU_BITS = 4   # kernels.h kActReluBits
+# ReLU (+ dropout) outputs handed to the consumer's folded dgrad as a bit mask (MIPIPE_RELU_BITS=0: the bf16
+# output itself, for A/B runs)
+_RELU_BITS = os.environ.get("MIPIPE_RELU_BITS", "1") != "0"
 
 
 def _defer(w: Tensor, dy: Tensor, x: Tensor, transposed: bool = False) -> None:

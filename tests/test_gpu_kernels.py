@@ -905,6 +905,46 @@ def test_feedforward_act_fold_matches_unfolded(k, activation, norm_first):
         assert ((a - b).abs().max() / (b.abs().max() + 1e-12)).item() < 2e-2
 
 
+def test_relu_bits_fold_bit_exact(k):
+    """ReLU + dropout folded into fc_out's dgrad through the 1-bit nonzero mask the forward GEMM writes
+    (kActReluBits) == the same fold re-reading the bf16 output, bit for bit; the bits are the output's
+    nonzeros.  Shapes large enough for the 256-row kernel (the one that writes bits)."""
+    import sys
+
+    from mipipe.models.transformer import FeedForwardBlock
+
+    L = sys.modules["mipipe.ops.linear"]  # the module (mipipe.ops re-exports a function of that name)
+    torch.manual_seed(41)
+    blk = FeedForwardBlock(1024, 2048, 0.2, "relu", device=DEV, dtype=torch.bfloat16)
+    x0 = torch.randn(16, 256, 1024, device=DEV).to(torch.bfloat16)
+    assert k.linear_bits_ok(16 * 256, 2048, 1024, 1, 0.2)
+    grads, offered = [], []
+    old = L._RELU_BITS
+    try:
+        for bits in (True, False):
+            L._RELU_BITS = bits
+            for prm in blk.parameters():
+                prm.grad = None
+            x = x0.clone().requires_grad_()
+            torch.cuda.manual_seed(6)
+            f = ActFold()
+            h, xr = blk.fc_in.forward_fanout(x, True, f)
+            offered.append((f.act, None if f.saved is None else f.saved.clone(), h.detach().clone()))
+            out = blk.fc_out(xr, h, f)
+            out.float().square().sum().backward()
+            assert f.saved is None and f.grad is None  # folded and consumed
+            grads.append([x.grad.clone()] + [prm.grad.clone() for prm in blk.parameters()])
+    finally:
+        L._RELU_BITS = old
+    (act_b, bits_t, h_b), (act_y, _, _) = offered
+    assert act_b == L.KACT_RELU_BITS and act_y == 1
+    nz = (h_b.reshape(-1, 2048) != 0).to(torch.uint8).view(-1, 256, 8)
+    packed = (nz << torch.arange(8, device=DEV, dtype=torch.uint8)).sum(-1, dtype=torch.int32).to(torch.uint8)
+    assert torch.equal(bits_t, packed.view(-1, 256))
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
 def test_act_fold_rejects_second_consumer(k):
     """The fold is only valid when h has one consumer: a second use is caught."""
     torch.manual_seed(32)
