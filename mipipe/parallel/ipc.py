@@ -170,10 +170,11 @@ class IpcChannels:
             or ``"inline"`` (one-way 15.7 us at 1 MiB against ~150 us through a
             copy stream; the 2-rank shared-GPU step +3.2 %:
             profiles/ipc_stream_ordered.txt).  ``"sdma"`` / ``"inline-sdma"``
-            copy with ``hipMemcpyDeviceToDeviceNoCU``: the copy engines only,
-            never a blit kernel on the CUs (what transport ``auto`` uses across
-            GPUs; profiles/nocu_copy_r5.txt).
-        timeout: seconds a host-mode wait may block before it raises (the
+            copy payload and completion flag with ``hipMemcpyDeviceToDeviceNoCU``:
+            the copy engines only, no kernel on the copy stream (what transport
+            ``auto`` uses across GPUs; profiles/ipc_cu_free_r6.txt).
+        timeout: seconds a host wait may block before it raises -- a host-mode
+            receive, or a send whose slot still holds an unreleased message (the
             engine's watchdog usually fires first).
     """
 
