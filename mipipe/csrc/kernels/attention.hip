@@ -38,9 +38,25 @@ template <int D>
 struct Img {
   static constexpr int kRowBytes = 2 * D;
   static constexpr int kChunks = D / 8;          // 16-byte chunks per row
-  static constexpr int kMask = kChunks >= 16 ? 15 : kChunks - 1;
   static constexpr int kBytes = kRows * kRowBytes;
-  __device__ static __forceinline__ int f(int r) { return ((((r & 3) << 2) | ((r >> 2) & 3))) & kMask; }
+  // 16-byte chunk c of row r sits at chunk c ^ f(r).  f is chosen (exhaustive
+  // search over the linear maps of r mod 16, tools/lds_swizzle_check.py) so that
+  // the three access patterns of these images are bank-conflict free on CDNA4:
+  //   * row-fragment ds_read_b128 (rows rb + 0..15, chunks 4 s + 0..3): the 16-lane
+  //     groups {0-3,12-15,20-27} etc. read rows {0-3,12-15} at chunk c and rows
+  //     4-11 at c ^ 1 -- 16 distinct 16-byte slots of the 256-byte bank row;
+  //   * column-fragment ds_read_b64_tr_b16 (rows 8 g + q (+4), 32-byte column
+  //     strips): 32-lane halves cover 16 distinct slots;
+  //   * the scattered bf16 writes of the S = 128 kernels (P~ / dS, and the
+  //     backward's outputs staged through the chunk images).
+  // The previous map ((r & 3) << 2 | (r >> 2) & 3, masked) cost 4 extra cycles
+  // per ds_read_b128 on 256- and 512-byte rows and 12 (+ 2 per transposing read)
+  // on the 128-byte rows of D = 64 / the S = 128 kernels' chunk images.
+  __device__ static __forceinline__ int f(int r) {
+    if constexpr (kChunks >= 16) return (((r ^ (r >> 2)) & 1) << 1) | ((r & 2) << 1) | (r & 8);
+    else if constexpr (kChunks == 8) return ((((r >> 1) ^ (r >> 2)) & 1) << 1) | ((r >> 1) & 4);
+    else return (((r & 3) << 2) | ((r >> 2) & 3)) & (kChunks - 1);
+  }
   __device__ static __forceinline__ int off(int r, int c16) { return r * kRowBytes + ((c16 ^ f(r)) << 4); }
 };
 

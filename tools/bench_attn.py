@@ -1,4 +1,5 @@
-"""Attention kernel timing at the enc12 shape (B=32, S=128, H=16, D=256), fused vs general backward."""
+"""Attention kernel timing at the enc12 shape (micro-batch 128: B=128, S=128, H=16, D=256): whole-sequence
+kernels (1) or the general ones (0)."""
 import statistics
 import sys
 
@@ -25,7 +26,7 @@ def timeit(fn, iters=20):
     return statistics.median(ts) * 1e3
 
 
-B, S, H, D = (int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (32, 128, 16, 256)))
+B, S, H, D = (int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (128, 128, 16, 256)))
 causal = len(sys.argv) > 5 and sys.argv[5] == "causal"
 P = float(sys.argv[6]) if len(sys.argv) > 6 else 0.2
 qkv = torch.randn(B, S, 3, H, D, device="cuda").to(torch.bfloat16)
