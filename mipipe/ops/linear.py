@@ -334,17 +334,19 @@ _FUSE_BIAS = os.environ.get("MIPIPE_FUSE_BIAS", "1") != "0"
 # (C^T = X^T . dY, ~15 % faster than reading both operands I-contiguous:
 # profiles/wgrad_layout_probe.txt) comes from -- MIPIPE_WGRAD_XT:
 #   auto (default): the flush transposes x (transpose_b16, a streaming kernel)
-#        for weights with at least _XT_MIN_N output features, where the GEMM
+#        for weights with more than 4608 output features, where the GEMM
 #        saving outgrows the transpose (~N_out / 3600 x its cost) -- and the
 #        bias gradient folds into the GEMM (split-K grids included) instead of
-#        a column-sum pass over dY;
+#        a column-sum pass over dY.  Measured: GPT-2-XL's qkv (4800 outputs)
+#        +0.5 % on the step, every weight (1600 outputs too) -1.4 %
+#        (tools/gpu_runs/r6_g11.sh); enc12's 4096-wide weights stay I-contiguous;
 #   emit: the forward GEMM writes x^T from its staged A tiles (every tile-path
 #        linear; +x^T bytes of activation memory, and ~40 us per forward GEMM:
 #        a wash on enc12, profiles/wgrad_xt_ab.txt);
 #   0:   never (both operands read I-contiguous), for A/B runs.
 _XT_MODE = os.environ.get("MIPIPE_WGRAD_XT", "auto")
 _EMIT_XT = _XT_MODE in ("1", "emit")
-_XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "6144"))
+_XT_MIN_N = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_N", "4608"))
 _XT_MIN_TILES = int(os.environ.get("MIPIPE_WGRAD_XT_MIN_TILES", "0"))
 # GELU forwards save GELU'(pre) rather than pre (MIPIPE_GELU_SAVE_GRAD=1).  Off by
 # default: the second erf/exp per element in the forward GEMM's epilogue cost the
