@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6 state: the GPU tier, smoke, the driver's bench command (twice), GPT-2-XL (config #4 shape, 10 steps).
+# Round 6 state: the GPU tier, smoke, the driver's bench command (twice), GPT-2-XL (config #4 shape, 20 steps after 5 warm-up).
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -14,5 +14,5 @@ for i in 1 2; do
   timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/final_bench_r6_$i.log 2>&1 || { tail -20 gpurun_out/final_bench_r6_$i.log; exit 1; }
   echo "bench $i: $(grep -o '"value": [0-9.]*' gpurun_out/final_bench_r6_$i.log) $(grep -o '"gfxclk_mhz": {[^}]*}' gpurun_out/final_bench_r6_$i.log) $(grep -o '"power_limited_pct": [0-9.]*' gpurun_out/final_bench_r6_$i.log)"
 done
-timeout -k 10 400 python -u bench.py --config gpt2_xl --steps 10 --warmup 3 --no-bubble > gpurun_out/final_gpt_r6.log 2>&1 || { tail -20 gpurun_out/final_gpt_r6.log; exit 1; }
+timeout -k 10 400 python -u bench.py --config gpt2_xl --steps 20 --warmup 5 --no-bubble > gpurun_out/final_gpt_r6.log 2>&1 || { tail -20 gpurun_out/final_gpt_r6.log; exit 1; }
 echo "gpt2_xl: $(grep -o '"value": [0-9.]*' gpurun_out/final_gpt_r6.log) $(grep -o '"gfxclk_mhz": {[^}]*}' gpurun_out/final_gpt_r6.log)"
