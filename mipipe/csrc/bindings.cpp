@@ -988,8 +988,12 @@ bool use_long(const Tensor& q, int S, int D) {
 // Returns (o, lse, seed, offset, dropout keep bits): the bits tensor (int32
 // [B*H, S/32, S]) is non-empty only for the long-sequence kernels with p > 0
 // and must be handed back to attention_bwd.
+// `words` (with the Philox draw it was made under): keep words an earlier forward of this same draw returned
+// (a checkpoint's first forward, reused by its recompute) -- read instead of made, when the draw matches.
 std::tuple<Tensor, Tensor, int64_t, int64_t, Tensor> py_attention_fwd(Tensor q, Tensor k, Tensor v, bool causal,
-                                                                      double p, double scale, int64_t kv_len) {
+                                                                      double p, double scale, int64_t kv_len,
+                                                                      std::optional<Tensor> words, int64_t words_seed,
+                                                                      int64_t words_offset) {
   AttnArgs a;
   fill_qkv(a, q, k, v);
   MP_CHECK(p >= 0.0 && p < 1.0, "attention: bad dropout p");
@@ -1008,11 +1012,17 @@ std::tuple<Tensor, Tensor, int64_t, int64_t, Tensor> py_attention_fwd(Tensor q, 
   if (q.scalar_type() == at::kFloat) {
     attention_f32_fwd(a, cur_stream(q));
   } else if (use_long(q, a.S, a.D)) {
+    bool reuse = false;
     if (p > 0.0) {
-      bits = at::empty({(int64_t)a.B * a.H, a.S / 32, a.S}, q.options().dtype(at::kInt));
+      const std::vector<int64_t> shape = {(int64_t)a.B * a.H, a.S / 32, a.S};
+      reuse = words && words->defined() && words->sizes() == at::IntArrayRef(shape) &&
+              words->scalar_type() == at::kInt && words->is_contiguous() && words->device() == q.device() &&
+              (uint64_t)words_seed == seed && (uint64_t)words_offset == offset;
+      bits = reuse ? *words : at::empty(shape, q.options().dtype(at::kInt));
       a.dmask = reinterpret_cast<uint32_t*>(bits.data_ptr());
     }
-    attention_long_fwd(a, cur_stream(q));
+    if (reuse) attention_long_fwd_words(a, cur_stream(q));
+    else attention_long_fwd(a, cur_stream(q));
   } else {
     attention_fwd(a, cur_stream(q));
   }
@@ -1243,7 +1253,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention_supported", [](int64_t S, int64_t D) { return attention_supported((int)S, (int)D); });
   m.def("attention_f32_supported", [](int64_t S, int64_t D) { return attention_f32_supported((int)S, (int)D); });
   m.def("attention_fwd", &py_attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"), py::arg("p"),
-        py::arg("scale"), py::arg("kv_len") = 0);
+        py::arg("scale"), py::arg("kv_len") = 0, py::arg("words") = py::none(), py::arg("words_seed") = 0,
+        py::arg("words_offset") = 0);
   m.def("attention_bwd", &py_attention_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("p"), py::arg("scale"), py::arg("seed"), py::arg("offset"),
         py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none(), py::arg("kv_len") = 0);

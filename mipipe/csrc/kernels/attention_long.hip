@@ -751,6 +751,14 @@ void attention_long_fwd(const AttnArgs& ai, hipStream_t s) {
   else run_fwd<false>(a, s);
 }
 
+void attention_long_fwd_words(const AttnArgs& ai, hipStream_t s) {
+  AttnArgs a = ai;
+  a.threshold = dropout_threshold(a.p);
+  const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
+  if (a.causal) hipLaunchKernelGGL((attn_long_fwd_kernel<true, 1>), grid, dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL((attn_long_fwd_kernel<false, 1>), grid, dim3(kThreads), 0, s, a);
+}
+
 void attention_long_bwd(const AttnArgs& ai, hipStream_t s) {
   AttnArgs a = ai;
   a.threshold = dropout_threshold(a.p);

@@ -242,6 +242,9 @@ bool attention_long_supported(int S, int D);
 // Keep words made inside the forward kernel (default) or by their own kernel first.
 void attention_long_set_fused_rng(bool on);
 void attention_long_fwd(const AttnArgs& a, hipStream_t s);
+// The forward reading keep words already in a.dmask (made by an earlier forward of the same Philox draw:
+// a checkpoint recompute) instead of making them.
+void attention_long_fwd_words(const AttnArgs& a, hipStream_t s);
 void attention_long_bwd(const AttnArgs& a, hipStream_t s);
 void attention_f32_fwd(const AttnArgs& a, hipStream_t s);
 void attention_f32_bwd(const AttnArgs& a, hipStream_t s);

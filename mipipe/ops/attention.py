@@ -29,15 +29,19 @@ are sliced off (and get no gradient).
 from __future__ import annotations
 
 import math
+import os
+import threading
+from collections import OrderedDict
 from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
 from torch import Tensor
 
+from ..checkpoint import is_checkpointing, is_recomputing
 from ._util import kernels_for
 
-__all__ = ["attention", "attention_packed", "attention_reference"]
+__all__ = ["attention", "attention_packed", "attention_reference", "clear_keep_words"]
 
 
 def attention_reference(q: Tensor, k: Tensor, v: Tensor, causal: bool, p: float, scale: Optional[float] = None) -> Tensor:
@@ -55,6 +59,69 @@ def attention_reference(q: Tensor, k: Tensor, v: Tensor, causal: bool, p: float,
     return torch.matmul(pr, v.float()).to(q.dtype)
 
 
+# Keep words across a checkpoint: the long-sequence forward (attention_long.hip) makes its dropout keep words
+# inside the kernel (Philox in the loop: ~1.6x the forward's VALU work) and returns them for the backward.  A
+# checkpoint's first, no-grad forward throws them away and its recompute makes the same words again from the
+# same restored Philox draw.  Instead the first forward leaves them here, keyed by (device, seed, offset), and
+# the recompute -- whose draw is that key again -- reads them (the kernel variant that loads the words).  The
+# words are bit-identical either way (tests/test_gpu_kernels.py::test_attention_keep_words_reused_bit_exact).
+# Bounded: at most MIPIPE_ATTN_KEEP_REUSE_GB (default 16) are held, oldest dropped first (a dropped entry is just
+# made again); MIPIPE_ATTN_KEEP_REUSE=0 turns it off.
+_KEEP_REUSE = os.environ.get("MIPIPE_ATTN_KEEP_REUSE", "1") != "0"
+_KEEP_LIMIT = int(float(os.environ.get("MIPIPE_ATTN_KEEP_REUSE_GB", "16")) * (1 << 30))
+_keep_words: "OrderedDict[tuple, Tensor]" = OrderedDict()
+_keep_bytes = 0
+_keep_lock = threading.Lock()
+keep_stats = {"stored": 0, "reused": 0}  # counters, for the tests
+
+
+def _i64(x: int) -> int:
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def _next_draw(device: torch.device) -> tuple:
+    """(device, seed, offset) the next Philox draw on ``device`` will return (the binding's int64 view)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    g = torch.cuda.default_generators[idx]
+    return (idx, _i64(g.initial_seed()), g.get_offset())
+
+
+def clear_keep_words() -> None:
+    """Drops every held keep-word set (the engine calls it at the end of a step)."""
+    global _keep_bytes
+    with _keep_lock:
+        _keep_words.clear()
+        _keep_bytes = 0
+
+
+def _attention_fwd(kern, q, k, v, causal, p, scale, kv_len):
+    global _keep_bytes
+    reuse = _KEEP_REUSE and p > 0 and q.is_cuda and q.dtype == torch.bfloat16 and kv_len == 0
+    words = key = None
+    if reuse and is_recomputing():
+        key = _next_draw(q.device)
+        with _keep_lock:
+            words = _keep_words.pop(key, None)
+            if words is not None:
+                _keep_bytes -= words.numel() * 4
+                keep_stats["reused"] += 1
+    if words is not None:
+        out = kern.attention_fwd(q, k, v, causal, p, scale, kv_len, words, key[1], key[2])
+    else:
+        out = kern.attention_fwd(q, k, v, causal, p, scale, kv_len)
+    bits = out[4]
+    if reuse and bits.numel() and is_checkpointing() and not torch.is_grad_enabled():
+        idx = q.device.index if q.device.index is not None else torch.cuda.current_device()
+        with _keep_lock:
+            _keep_words[(idx, out[2], out[3])] = bits
+            _keep_bytes += bits.numel() * 4
+            keep_stats["stored"] += 1
+            while _keep_bytes > _KEEP_LIMIT and _keep_words:
+                _, old = _keep_words.popitem(last=False)
+                _keep_bytes -= old.numel() * 4
+    return out
+
+
 class _AttentionPacked(torch.autograd.Function):
     """``qkv [B, S, 3, H, D]`` (contiguous) in, ``o [B, S, H, D]`` out; the
     backward produces the packed ``dqkv`` in one buffer."""
@@ -63,7 +130,7 @@ class _AttentionPacked(torch.autograd.Function):
     def forward(ctx, qkv, causal, p, scale, kv_len=0):  # type: ignore[override]
         kern = kernels_for(qkv)
         q, k, v = qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2)
-        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale, kv_len)
+        o, lse, seed, offset, bits = _attention_fwd(kern, q, k, v, causal, p, scale, kv_len)
         ctx.save_for_backward(qkv, o, lse, bits)
         ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, ctx.kv_len = causal, p, scale, seed, offset, kv_len
         return o
@@ -87,7 +154,7 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, p, scale, kv_len=0):  # type: ignore[override]
         kern = kernels_for(q)
-        o, lse, seed, offset, bits = kern.attention_fwd(q, k, v, causal, p, scale, kv_len)
+        o, lse, seed, offset, bits = _attention_fwd(kern, q, k, v, causal, p, scale, kv_len)
         ctx.save_for_backward(q, k, v, o, lse, bits)
         ctx.causal, ctx.p, ctx.scale, ctx.seed, ctx.offset, ctx.kv_len = causal, p, scale, seed, offset, kv_len
         return o

@@ -60,6 +60,7 @@ import torch.distributed as dist
 from torch import Tensor, nn
 
 from .. import ops
+from ..ops.attention import clear_keep_words as _clear_keep_words
 from ..checkpoint import enable_checkpointing, enable_recomputing
 from ..pipeline import checkpoint_stop_for
 from ..skip.tracker import use_skip_tracker
@@ -726,6 +727,9 @@ class PipelineEngine:
                 defer.__exit__(RuntimeError, None, None)
             if armed is not None:
                 armed.__exit__(None, None, None)
+            # attention keep words carried from checkpointed forwards to their recomputes (ops/attention.py):
+            # every recompute of the step has run, so any leftover (an aborted step) is dropped here
+            _clear_keep_words()
         self._mark("step done")
 
         stats.losses = losses

@@ -1147,6 +1147,49 @@ def _check_attention_packed(k, D, causal, p, S):
 
 
 @pytest.mark.parametrize("causal", [False, True])
+def test_attention_keep_words_reused_bit_exact(k, causal):
+    """A checkpoint's recompute reads the keep words its first forward made (ops/attention.py) instead of making
+    them again: output and gradients bit-identical to the same checkpointed run with the reuse off, and to a run
+    without checkpointing."""
+    import sys
+
+    from mipipe import checkpoint
+    from mipipe.ops import attention_packed
+
+    A = sys.modules["mipipe.ops.attention"]
+    B, S, H, D, p = 2, 512, 3, 64, 0.15
+    assert k.attention_long_supported(S, D)
+    torch.manual_seed(5)
+    base = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16)
+    g = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
+
+    def run(ckpt: bool, reuse: bool):
+        A._KEEP_REUSE = reuse
+        A.clear_keep_words()
+        x = base.clone().requires_grad_()
+        torch.manual_seed(7)
+        f = lambda t: attention_packed(t, causal, p, True)  # noqa: E731
+        o = checkpoint(f, x) if ckpt else f(x)
+        o.backward(g)
+        torch.cuda.synchronize()
+        return o.detach(), x.grad
+
+    old = A._KEEP_REUSE
+    try:
+        before = dict(A.keep_stats)
+        o1, g1 = run(True, True)
+        assert A.keep_stats["stored"] == before["stored"] + 1 and A.keep_stats["reused"] == before["reused"] + 1
+        assert not A._keep_words  # taken by the recompute
+        o0, g0 = run(True, False)
+        o2, g2 = run(False, True)
+    finally:
+        A._KEEP_REUSE = old
+        A.clear_keep_words()
+    assert torch.equal(o1, o0) and torch.equal(g1, g0)
+    assert torch.equal(o1, o2) and torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
 def test_attention_long_fused_rng_identical(k, causal):
     """Keep words made inside the long-sequence forward kernel (default) and by the
     stand-alone keep-bit kernel are the same words: output, LSE and stored bits match
