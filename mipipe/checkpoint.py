@@ -53,6 +53,8 @@ class _ThreadFlags(threading.local):
     def __init__(self) -> None:
         self.checkpointing = False
         self.recomputing = False
+        # a checkpointed forward whose recompute will run (grad was enabled around it)
+        self.recompute_expected = True
 
 
 _flags = _ThreadFlags()
@@ -81,6 +83,24 @@ def enable_recomputing() -> Generator[None, None, None]:
 def is_checkpointing() -> bool:
     """True while a partition runs its first (no-grad) forward under checkpointing."""
     return _flags.checkpointing
+
+
+def recompute_expected() -> bool:
+    """True while a checkpointed forward runs whose backward will recompute it:
+    state kept for the recompute (ops.attention's dropout keep words) is then
+    worth keeping.  False for a training-mode forward under ``torch.no_grad()``
+    (checkpointed, but never backpropagated)."""
+    return _flags.checkpointing and _flags.recompute_expected
+
+
+@contextmanager
+def _recompute_expected(on: bool) -> Generator[None, None, None]:
+    prev = _flags.recompute_expected
+    _flags.recompute_expected = on
+    try:
+        yield
+    finally:
+        _flags.recompute_expected = prev
 
 
 def is_recomputing() -> bool:
@@ -140,9 +160,10 @@ class Checkpointing:
         # A phony that requires grad keeps Checkpoint in the graph even when no
         # input requires grad (e.g. token ids into the first partition).
         phony = get_phony(self.batch.get_device(), requires_grad=True)
-        output = Checkpoint.apply(
-            phony, self.recomputed, self.rng_states, self.function, self.batch.atomic, *self.batch
-        )
+        with _recompute_expected(torch.is_grad_enabled()):
+            output = Checkpoint.apply(
+                phony, self.recomputed, self.rng_states, self.function, self.batch.atomic, *self.batch
+            )
         return Batch(_float_only(output))
 
     def recompute(self, batch: Batch) -> None:

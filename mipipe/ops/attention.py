@@ -38,7 +38,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from ..checkpoint import is_checkpointing, is_recomputing
+from ..checkpoint import is_recomputing, recompute_expected
 from ._util import kernels_for
 
 __all__ = ["attention", "attention_packed", "attention_reference", "clear_keep_words"]
@@ -66,7 +66,8 @@ def attention_reference(q: Tensor, k: Tensor, v: Tensor, causal: bool, p: float,
 # the recompute -- whose draw is that key again -- reads them (the kernel variant that loads the words).  The
 # words are bit-identical either way (tests/test_gpu_kernels.py::test_attention_keep_words_reused_bit_exact).
 # Bounded: at most MIPIPE_ATTN_KEEP_REUSE_GB (default 16) are held, oldest dropped first (a dropped entry is just
-# made again); MIPIPE_ATTN_KEEP_REUSE=0 turns it off.
+# made again), and only when that recompute will run (checkpoint.recompute_expected(): not for a training-mode
+# forward under no_grad); MIPIPE_ATTN_KEEP_REUSE=0 turns it off.
 _KEEP_REUSE = os.environ.get("MIPIPE_ATTN_KEEP_REUSE", "1") != "0"
 _KEEP_LIMIT = int(float(os.environ.get("MIPIPE_ATTN_KEEP_REUSE_GB", "16")) * (1 << 30))
 _keep_words: "OrderedDict[tuple, Tensor]" = OrderedDict()
@@ -110,7 +111,7 @@ def _attention_fwd(kern, q, k, v, causal, p, scale, kv_len):
     else:
         out = kern.attention_fwd(q, k, v, causal, p, scale, kv_len)
     bits = out[4]
-    if reuse and bits.numel() and is_checkpointing() and not torch.is_grad_enabled():
+    if reuse and bits.numel() and recompute_expected() and not torch.is_grad_enabled():
         idx = q.device.index if q.device.index is not None else torch.cuda.current_device()
         with _keep_lock:
             _keep_words[(idx, out[2], out[3])] = bits

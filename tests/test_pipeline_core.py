@@ -206,3 +206,25 @@ def test_checkpoint_non_float_outputs_detached():
     chk = Checkpointing(f, b)
     out = chk.checkpoint()
     assert not out[1].requires_grad
+
+
+def test_recompute_expected_only_when_backward_will_recompute():
+    """recompute_expected() (ops.attention keeps its dropout keep words for the recompute only then): True inside a
+    checkpointed forward taken with grad enabled, False for a training-mode forward under no_grad, False outside."""
+    from mipipe.checkpoint import checkpoint, recompute_expected
+
+    seen = []
+
+    def f(t):
+        seen.append((is_checkpointing(), is_recomputing(), recompute_expected()))
+        return t * 2
+
+    x = torch.ones(3, requires_grad=True)
+    y = checkpoint(f, x)
+    y.sum().backward()
+    assert seen == [(True, False, True), (False, True, False)]
+    seen.clear()
+    with torch.no_grad():
+        checkpoint(f, torch.ones(3))
+    assert seen == [(True, False, False)]
+    assert not recompute_expected()
