@@ -88,7 +88,9 @@ def parse():
     ap.add_argument("--plan-select", default="auto", choices=["auto", "emulate", "model"],
                     help="final pick of the stage plan: emulate = the few best plans of the cost model are each run "
                          "on every rank alone (loop-back engine, a few steps) and the fastest by measured walls "
-                         "wins (mipipe.parallel.calibrate.select_plan_by_emulation; profiles/plan_table_r5.txt); "
+                         "wins, after single units were moved off each candidate's slowest measured rank "
+                         "(mipipe.parallel.calibrate.select_plan_by_emulation; profiles/plan_table_r5.txt, "
+                         "plan_refine_r6.txt); "
                          "model = the cost model's choice.  auto = emulate with measured costs on GPUs at PP > 1")
     ap.add_argument("--split-decoder", default="auto", choices=["auto", "on", "off"],
                     help="cut the LM head along the vocabulary into two pipeline units")
@@ -248,8 +250,11 @@ def main() -> int:
         t_ = time.perf_counter()
         cands = candidate_plans(cfg, pp, m, bwd_ratio, mb, cost_fn, split_options=splits)
         if len(cands) > 1:
+            # ranks sharing one GPU measure each other's time slices: walls of a refinement move (two ranks
+            # emulating) are not comparable with the all-rank ones, so --shared-gpu skips the refinement
             plan, plan_report = select_plan_by_emulation(cfg, cands, prank, m, mb, args.checkpoint, unit_ms,
-                                                         device=device, dtype=dtype, replica=replica)
+                                                         device=device, dtype=dtype, replica=replica,
+                                                         refine_rounds=0 if args.shared_gpu else 6)
             virtual = plan.virtual
         else:
             plan, virtual = cands[0], cands[0].virtual

@@ -451,7 +451,7 @@ def emulate_rank_ms(cfg: LMConfig, plan, rank: int, chunks: int, micro_batch: in
 def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int, micro_batch: int,
                              checkpoint: str, unit_ms: Dict[str, float], *, device: torch.device,
                              dtype: torch.dtype = torch.bfloat16, replica: int = 0, group=None,
-                             steps: int = 2, emulate=None):
+                             steps: int = 2, emulate=None, refine_rounds: int = 6):
     """Picks the fastest of ``candidates`` (:func:`~mipipe.parallel.stage.candidate_plans`)
     from MEASURED walls: every pipeline rank emulates its own rank of every
     candidate at once (:func:`emulate_rank_ms`, replica 0 only under data
@@ -459,7 +459,10 @@ def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int,
     and each candidate's job step is simulated from its walls
     (:func:`~mipipe.parallel.stage.simulate_from_walls`, IPC hop).  Identical
     on every rank.  Returns ``(plan, report)``; if any rank's emulation fails,
-    every rank returns the model's first candidate (report says why).
+    every rank returns the model's first candidate (report says why).  The
+    candidates are then refined from their measured walls, best first
+    (:func:`refine_plan_by_walls`; ``refine_rounds`` emulated moves in all,
+    0: off) and the fastest refined plan is returned.
     ``emulate(plan, prank) -> ms``: test hook."""
     from ..pipeline import checkpoint_stop_for
     from .stage import HOP_BYTES_PER_S, HOP_LATENCY_MS, simulate_from_walls
@@ -509,4 +512,110 @@ def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int,
         if best is None or t < best[0]:
             best = (t, i)
     report["chosen"] = best[1]
-    return candidates[best[1]], report
+    plan = candidates[best[1]]
+    if refine_rounds > 0:
+        # every candidate, best simulated first, within a shared budget of emulation rounds: a plan the cost
+        # model got wrong can beat the pick once its slowest rank is unloaded (PP=8: +2.5 %,
+        # profiles/plan_refine_r6.txt)
+        def step_of(p, w):
+            return simulate_from_walls(p, w, engine_unit_costs(cfg, unit_ms, p.split_decoder), chunks, stop, hop)[0]
+
+        order = sorted(range(k), key=lambda i: (report["candidates"][i]["step_ms"], i))
+        budget, refined = refine_rounds, []
+        for i in order:
+            if budget <= 0:
+                break
+            p_i, hist = refine_plan_by_walls(candidates[i], walls[i * pp:(i + 1) * pp].tolist(),
+                                             report["candidates"][i]["step_ms"], prank=prank, emulate=emulate,
+                                             replica=replica, group=group, device=device,
+                                             rounds=min(3, budget), step_of=step_of)
+            budget -= sum(1 for h in hist if "move" in h)
+            t_i = min([report["candidates"][i]["step_ms"]] + [h["step_ms"] for h in hist if h.get("accepted")])
+            refined.append({"candidate": i, "balance": list(p_i.balance), "step_ms": t_i, "moves": hist})
+            if any("stopped" in h for h in hist):
+                break
+            if t_i < best[0]:
+                best, plan = (t_i, i), p_i
+        report["refinement"] = refined
+        report["chosen"] = best[1]
+        report["chosen_balance"] = list(plan.balance)
+    return plan, report
+
+
+def _move_candidates(plan, walls: Sequence[float]):
+    """Single-unit boundary moves off the slowest measured rank, best first: each virtual stage of that rank
+    (keeping >= 1 unit) gives its boundary unit to an adjacent virtual stage owned by another rank.  The unit's
+    share of the slow rank's wall is priced by its unit cost (``plan.costs``) and only moves predicted to lower
+    the larger of the two walls are kept, the lowest predicted maximum first (ties: lower virtual stage)."""
+    pp, n = plan.ranks, len(plan.balance)
+    slow = max(range(pp), key=lambda r: (walls[r], -r))
+    mine = sum(plan.costs[i] for s in plan.vstages(slow) for i in plan.slice(s)) or 1.0
+    moves = []
+    for s in plan.vstages(slow):
+        if plan.balance[s] <= 1:
+            continue
+        sl = plan.slice(s)
+        for nb in (s - 1, s + 1):
+            if not (0 <= nb < n) or nb % pp == slow:
+                continue
+            unit = sl.start if nb < s else sl.stop - 1
+            c = walls[slow] * plan.costs[unit] / mine
+            peak = max(walls[nb % pp] + c, walls[slow] - c)
+            if peak < walls[slow]:
+                moves.append((peak, s, nb))
+    moves.sort()
+    return slow, [(s, nb) for _, s, nb in moves]
+
+
+def refine_plan_by_walls(plan, walls: Sequence[float], step_ms: float, *, prank: int, emulate,
+                         replica: int = 0, group=None, device=None, rounds: int = 4, step_of=None):
+    """Moves single units off the slowest MEASURED rank of the chosen plan.
+
+    The unit-cost model balances what it prices; the emulated walls also carry what it does not (the loss and
+    decoder's optimizer share on the last rank, the embedding gradient on the first, the recompute of
+    ``except_last``): at PP=8, micro-batch 128 the chosen plan's walls spread 476-584 ms
+    (profiles/plan_table_r5.txt).  Each round takes the best move of :func:`_move_candidates`, re-emulates ONLY
+    the two ranks whose virtual stages changed (a rank's wall depends on its own stages alone), gathers the walls
+    with one all-reduce, and keeps the move if the simulated job step (``step_of(plan, walls)``) is shorter;
+    the first move that does not help ends the search.  Identical decisions on every rank (same walls); a rank
+    whose emulation raises ends the search for all.  Returns ``(plan, history)``."""
+    from .stage import StagePlan
+
+    pp = plan.ranks
+    walls = list(walls)
+    history = []
+    distributed = dist.is_available() and dist.is_initialized()
+    for _ in range(rounds):
+        slow, moves = _move_candidates(plan, walls)
+        if not moves:
+            break
+        s, nb = moves[0]
+        bal = list(plan.balance)
+        bal[s] -= 1
+        bal[nb] += 1
+        new = StagePlan(bal, plan.costs, plan.virtual, plan.split_decoder)
+        changed = {s % pp, nb % pp}
+        buf = torch.zeros(pp + 1, dtype=torch.float64)
+        if replica == 0 and prank in changed:
+            try:
+                buf[prank] = float(emulate(new, prank))
+            except Exception as exc:  # noqa: BLE001 -- every rank stops below, identically
+                history.append({"error": repr(exc)})
+                del exc
+                buf[-1] = 1.0
+        if distributed:
+            w = buf.to(device) if dist.get_backend(group) == "nccl" else buf
+            dist.all_reduce(w, group=group)
+            buf = w.cpu()
+        if buf[-1] > 0:
+            history.append({"stopped": "emulation failed"})
+            break
+        new_walls = [float(buf[r]) if r in changed else walls[r] for r in range(pp)]
+        t = step_of(new, new_walls)
+        ok = t < step_ms
+        history.append({"slowest_rank": slow, "move": [s, nb], "rank_walls_ms": [round(x, 1) for x in new_walls],
+                        "step_ms": round(t, 1), "accepted": ok})
+        if not ok:
+            break
+        plan, walls, step_ms = new, new_walls, t
+    return plan, history

@@ -113,3 +113,49 @@ def test_select_plan_falls_back_together_when_a_rank_fails():
     assert res[0][0] == res[1][0] == [9, 9]  # the model's first candidate on both ranks
     assert all(r[1].startswith("model (emulation failed") and r[2] == 0 for r in res.values())
     assert "boom" in res[1][1]
+
+
+def _refine_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        cfg = _cfg()
+        um = _unit_ms(cfg)
+        costs = engine_unit_costs(cfg, um, False)
+        start = plan_stages(cfg, 2, 1, 8, False, costs=costs)
+        calls = []
+
+        def emulate(plan, r):  # the unit costs, plus work the cost model does not see on the last rank
+            calls.append(tuple(plan.balance))
+            return sum(costs[i] for s in plan.vstages(r) for i in plan.slice(s)) * 8 + (30.0 if r == 1 else 0.0)
+
+        plan, rep = select_plan_by_emulation(cfg, [start], rank, 8, 2, "never", um, device=CPU, emulate=emulate)
+        assert rep["chosen_balance"] == list(plan.balance)
+        q.put((rank, list(start.balance), list(plan.balance), rep["refinement"][0]["moves"], len(calls)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_refinement_moves_units_off_the_slowest_measured_rank():
+    """The chosen plan is refined from its measured walls: single units move off the rank the walls show
+    slowest (here: extra work on the last rank that the unit costs miss) while the simulated step improves;
+    every rank takes the same moves, and a rank re-emulates only when its stages changed."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_refine_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=300) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (s0, p0, h0, _), (s1, p1, h1, _) = res[0], res[1]
+    assert p0 == p1 and h0 == h1 and s0 == s1
+    assert sum(p0) == sum(s0) and all(k >= 1 for k in p0)
+    accepted = [h for h in h0 if h.get("accepted")]
+    assert accepted and p0[1] < s0[1]  # units left the slow last rank
+    walls = [h["rank_walls_ms"] for h in accepted]
+    assert max(walls[-1]) < max(walls[0]) or len(walls) == 1
+    # each round re-emulated only the two ranks whose stages changed
+    assert res[0][3] == 1 + len(h0) and res[1][3] == 1 + len(h0)

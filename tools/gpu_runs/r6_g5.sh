@@ -22,6 +22,10 @@ sel = c["plan_selection"] or {}
 print(f"PP={n}: {d['value']} tok/s (time-sliced), v={c['virtual_chunks_per_rank']}, transport {c['transport']}, "
       f"plan_costs {c['plan_costs']!r}, selection {sel.get('method')!r}, {len(sel.get('candidates', []))} candidates")
 print("  startup_s", d["startup_s"])
+for rf in sel.get("refinement", []):
+    print(f"  refined candidate {rf['candidate']}: {len([h for h in rf['moves'] if h.get('accepted')])} moves kept, "
+          f"step {rf['step_ms']} ms")
+print("  chosen", sel.get("chosen"), sel.get("chosen_balance"))
 print("  like_for_like", d["like_for_like"])
 PY
   echo "  wall of the whole run: $((SECONDS - t0)) s"
