@@ -522,24 +522,39 @@ def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int,
 
         order = sorted(range(k), key=lambda i: (report["candidates"][i]["step_ms"], i))
         budget, refined = refine_rounds, []
-        for i in order:
-            if budget <= 0:
-                break
-            p_i, hist = refine_plan_by_walls(candidates[i], walls[i * pp:(i + 1) * pp].tolist(),
-                                             report["candidates"][i]["step_ms"], prank=prank, emulate=emulate,
-                                             replica=replica, group=group, device=device,
-                                             rounds=min(3, budget), step_of=step_of)
-            budget -= sum(1 for h in hist if "move" in h)
-            t_i = min([report["candidates"][i]["step_ms"]] + [h["step_ms"] for h in hist if h.get("accepted")])
-            refined.append({"candidate": i, "balance": list(p_i.balance), "step_ms": t_i, "moves": hist})
-            if any("stopped" in h for h in hist):
-                break
-            if t_i < best[0]:
-                best, plan = (t_i, i), p_i
+        pick = (best, plan)
+        try:
+            plan = _refine_all(order, budget, refined, candidates, walls, report, pp, prank, emulate, replica,
+                               group, device, step_of, best, plan)
+        except Exception as exc:  # noqa: BLE001 -- deterministic code on identical walls: every rank is here
+            refined.append({"error": repr(exc)})
+            best, plan = pick
+            report["chosen"] = best[1]
         report["refinement"] = refined
-        report["chosen"] = best[1]
         report["chosen_balance"] = list(plan.balance)
     return plan, report
+
+
+def _refine_all(order, budget, refined, candidates, walls, report, pp, prank, emulate, replica, group, device,
+                step_of, best, plan):
+    """The refinement loop of :func:`select_plan_by_emulation`: candidates best first, one shared budget of
+    emulated moves; returns the fastest refined plan (``report["chosen"]``: its candidate index)."""
+    for i in order:
+        if budget <= 0:
+            break
+        p_i, hist = refine_plan_by_walls(candidates[i], walls[i * pp:(i + 1) * pp].tolist(),
+                                         report["candidates"][i]["step_ms"], prank=prank, emulate=emulate,
+                                         replica=replica, group=group, device=device, rounds=min(3, budget),
+                                         step_of=step_of)
+        budget -= sum(1 for h in hist if "move" in h)
+        t_i = min([report["candidates"][i]["step_ms"]] + [h["step_ms"] for h in hist if h.get("accepted")])
+        refined.append({"candidate": i, "balance": list(p_i.balance), "step_ms": t_i, "moves": hist})
+        if t_i < best[0]:
+            best, plan = (t_i, i), p_i
+        if any("stopped" in h for h in hist):
+            break
+    report["chosen"] = best[1]
+    return plan
 
 
 def _move_candidates(plan, walls: Sequence[float]):
