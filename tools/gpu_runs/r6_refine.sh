@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1 MIPIPE_CALIB_DIR="$GRAFT_REPO_ROOT/gpurun_out/calib_refine"
-timeout -k 10 900 python -u tools/plan_refine_probe.py --config enc12_d4096 --pp 8 --rounds 8 --refine-all > gpurun_out/refine_pp8.log 2>&1
+timeout -k 10 900 python -u tools/plan_refine_probe.py --config enc12_d4096 --pp 8 --rounds 8 --refine-all --replan > gpurun_out/refine_pp8.log 2>&1
 rc=$?
 cat gpurun_out/refine_pp8.log | grep -v "^#.*rank\b" | tail -30
 exit $rc

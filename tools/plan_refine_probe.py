@@ -32,6 +32,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--refine-all", action="store_true", help="refine every candidate, not only the pick")
+    ap.add_argument("--replan", action="store_true", help="re-plan from wall-corrected unit costs")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     pp = args.pp
@@ -91,6 +92,36 @@ def main() -> int:
         results.append((t, c, walls))
     pick = min(results, key=lambda x: x[0])
     print(f"bench pick (no refinement): v={pick[1].virtual} step {pick[0]:.1f} ms", flush=True)
+    if args.replan:
+        # wall-corrected unit costs: every unit's cost scaled by its rank's measured / modelled ratio, averaged
+        # over the emulated candidates of the same decoder split; plans re-made from them and emulated
+        from mipipe.parallel.stage import plan_stages
+
+        for split in sorted({c.split_decoder for _, c, _ in results}):
+            base = engine_unit_costs(cfg, unit_ms, split)
+            acc = [0.0] * len(base)
+            n = 0
+            for t, c, walls in results:
+                if c.split_decoder != split:
+                    continue
+                n += 1
+                for r in range(pp):
+                    units = [u for s_ in c.vstages(r) for u in c.slice(s_)]
+                    model = sum(base[u] for u in units) * m or 1.0
+                    for u in units:
+                        acc[u] += base[u] * walls[r] / model
+            corrected = [a / n for a in acc]
+            for v in (1, 2, 3):
+                try:
+                    p_ = plan_stages(cfg, pp, v, m, split, bwd_ratio, costs=corrected, objective="makespan")
+                except ValueError:
+                    continue
+                p_ = StagePlan(list(p_.balance), base, v, split)  # priced with the measured unit costs again
+                walls = [emu(p_, r) for r in range(pp)]
+                t = step_of(p_, walls)
+                print(f"replanned v={v} split={split} {p_.balance}: walls {[round(w) for w in walls]}, step {t:.1f} ms,"
+                      f" {m * mb * cfg.seq_len / t * 1e3:,.0f} tok/s", flush=True)
+                results.append((t, p_, walls))
     final = []
     for t, c, walls in (results if args.refine_all else [pick]):
         print(f"refining v={c.virtual} {c.balance}", flush=True)
