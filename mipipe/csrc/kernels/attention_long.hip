@@ -10,7 +10,7 @@
 //
 //   forward (a wave = 64 queries):  S^T = K Q^T   (keys in registers, query on the lane)
 //                                   O  += P V     (P^T registers are the A operand)
-//   dK, dV  (a wave = 64 keys):     S = Q K^T, dP = dO V^T   (key on the lane)
+//   dK, dV  (a wave = 64 keys; the default 8-wave kernel: 32): S = Q K^T, dP = dO V^T (key on the lane)
 //                                   dV^T += dO^T P_drop,  dK^T += Q^T dS
 //   dQ      (a wave = 64 queries):  S^T, dP^T = V dO^T, dQ += dS K
 //
@@ -573,6 +573,165 @@ __global__ void __launch_bounds__(kThreads, 1) attn_long_dkdv_kernel(AttnArgs a)
   }
 }
 
+// ------------------------------------------------------------------ dK, dV, 8 waves
+// The same computation with 8 waves of 32 keys per 256-key block (512
+// threads): half the accumulators per wave (dK / dV 64 registers, S / dP 32),
+// so two waves share each SIMD -- the 4-wave kernel's one wave per SIMD (256
+// VGPRs + ~200 AGPRs) leaves its MFMA and VALU issue mostly idle, waiting on
+// its own dependency chains.  Same LDS: the Q / dO tiles double-buffered and
+// each wave's [32][64] K and V images.  Query blocks wholly before a wave's
+// keys (causal) are skipped.
+constexpr int kThreads8 = 512;
+constexpr int kImg32 = 32 * D * 2;  // [32][64] bf16
+
+template <bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kThreads8, 2) attn_long_dkdv8_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg + 2 * 2 * kTile * 4 + 8 * 2 * kImg32];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, li = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kt = (int)blockIdx.y;
+  const int bh = blockIdx.x, b = bh / a.H, hh = bh % a.H;
+  const int k0w = kt * kBlockRows + wave * 32;  // this wave's keys k0w .. k0w + 31
+  const bool active = k0w < a.S;
+  const int64_t hoff = (int64_t)b * a.sb_qkv + (int64_t)hh * a.sh_qkv;
+  const int64_t ooff = (int64_t)b * a.sb_o + (int64_t)hh * a.sh_o;
+  const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + hoff;
+  const bf16_t* dO = reinterpret_cast<const bf16_t*>(a.dout) + ooff;
+  constexpr bool drop = DROP;
+  const float pscale = drop ? 1.f / (1.f - a.p) : 1.f;
+  const float sl2 = a.scale * kLog2e;
+
+  char* kimg_w = lds + 4 * kImg + 4 * kTile * 4 + wave * 2 * kImg32;
+  char* vimg_w = kimg_w + kImg32;
+  {
+    const int key = min(k0w + li, a.S - 1);
+    const bf16_t* kr = reinterpret_cast<const bf16_t*>(a.k) + hoff + (int64_t)key * a.ld_qkv;
+    const bf16_t* vr = reinterpret_cast<const bf16_t*>(a.v) + hoff + (int64_t)key * a.ld_qkv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * h + j;
+      *reinterpret_cast<u32x4*>(kimg_w + ioff(li, c)) = *reinterpret_cast<const u32x4*>(kr + 8 * c);
+      *reinterpret_cast<u32x4*>(vimg_w + ioff(li, c)) = *reinterpret_cast<const u32x4*>(vr + 8 * c);
+    }
+  }
+  f32x16 dk[2], dv[2];  // [dt]: rows d, columns keys
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    dk[dt] = zero16();
+    dv[dt] = zero16();
+  }
+
+  const int qstart = CAUSAL ? (kt * kBlockRows) / kTile : 0;
+  const int ntiles = a.S / kTile;
+  u32x4 sq, so;  // one 16-byte piece of the Q / dO tile per thread
+  float st_l = 0.f;
+  const int sr = tid >> 3, sc = tid & 7;
+  auto gload = [&](int t) {
+    sq = *reinterpret_cast<const u32x4*>(Q + (int64_t)(t * kTile + sr) * a.ld_qkv + 8 * sc);
+    so = *reinterpret_cast<const u32x4*>(dO + (int64_t)(t * kTile + sr) * a.ld_o + 8 * sc);
+    if (tid < 2 * kTile) {
+      const int64_t i = (int64_t)bh * a.S + t * kTile + (tid & (kTile - 1));
+      st_l = tid < kTile ? a.lse[i] * kLog2e : a.delta[i];
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* base = lds + buf * 2 * kImg;
+    *reinterpret_cast<u32x4*>(base + ioff(sr, sc)) = sq;
+    *reinterpret_cast<u32x4*>(base + kImg + ioff(sr, sc)) = so;
+    if (tid < 2 * kTile) reinterpret_cast<float*>(lds + 4 * kImg)[buf * 2 * kTile + tid] = st_l;
+  };
+  if (qstart < ntiles) {
+    gload(qstart);
+    lstore(0);
+  }
+  __syncthreads();
+  const int tw = !active ? ntiles : (CAUSAL ? max(qstart, k0w / kTile) : qstart);
+  for (int t = qstart; t < tw; ++t) {
+    gload(min(t + 1, ntiles - 1));
+    lstore(((t - qstart) & 1) ^ 1);
+    __syncthreads();
+  }
+  for (int t = tw; t < ntiles; ++t) {
+    const int buf = (t - qstart) & 1;
+    const char* qimg = lds + buf * 2 * kImg;
+    const char* oimg = qimg + kImg;
+    const float* lse2 = reinterpret_cast<const float*>(lds + 4 * kImg) + buf * 2 * kTile;
+    const float* dlt = lse2 + kTile;
+    const int q0 = t * kTile;
+    gload(min(t + 1, ntiles - 1));
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int qrow = q0 + 32 * qb;
+      if (CAUSAL && qrow + 31 < k0w) continue;  // every query of the block is before the wave's keys
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kb_ = row_frag(kimg_w, li, s, h);
+        const bf16x8 vb_ = row_frag(vimg_w, li, s, h);
+        sacc = mfma(row_frag(qimg, 32 * qb + li, s, h), kb_, sacc);
+        dpacc = mfma(row_frag(oimg, 32 * qb + li, s, h), vb_, dpacc);
+      }
+      const int key = k0w + li;
+      uint32_t word = 0xFFFFFFFFu;
+      if (drop) word = a.dmask[((int64_t)bh * (a.S >> 5) + (qrow >> 5)) * a.S + key];
+      float pr[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2 + 32 * qb + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pr[4 * g + j] = __builtin_amdgcn_exp2f(fmaf(sacc[4 * g + j], sl2, -lv[j]));
+      }
+      if (CAUSAL && k0w + 31 > qrow) {  // diagonal block (wave-uniform branch)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key > qrow + arow(r, h)) pr[r] = 0.f;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dlt + 32 * qb + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const float dsel = drop ? keep_or_zero(dpacc[r], word, arow(r, h)) : dpacc[r];
+          sacc[r] = drop ? keep_or_zero(pr[r], word, arow(r, h)) : pr[r];
+          dpacc[r] = pr[r] * (drop ? fmaf(dsel, pscale, -dv4[j]) : dsel - dv4[j]);
+        }
+      }
+      const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 1);
+      const bf16x8 sb0 = pack8(dpacc, 0), sb1 = pack8(dpacc, 1);
+#pragma unroll
+      for (int st_ = 0; st_ < 2; ++st_)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int r0 = 32 * qb + 16 * st_ + 4 * h, c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+          dv[dt] = mfma(col_frag(oimg, r0, c0, lane), st_ ? pb1 : pb0, dv[dt]);
+          dk[dt] = mfma(col_frag(qimg, r0, c0, lane), st_ ? sb1 : sb0, dk[dt]);
+        }
+    }
+    lstore(buf ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  const int key = k0w + li;
+  if (key >= a.S) return;
+  bf16_t* dK = reinterpret_cast<bf16_t*>(a.dk) + hoff + (int64_t)key * a.ld_qkv;
+  bf16_t* dV = reinterpret_cast<bf16_t*>(a.dv) + hoff + (int64_t)key * a.ld_qkv;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 32 * dt + 8 * g + 4 * h;
+      bf16x4 kv, vv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kv[j] = (__bf16)(dk[dt][4 * g + j] * a.scale);
+        vv[j] = (__bf16)(dv[dt][4 * g + j] * pscale);
+      }
+      *reinterpret_cast<bf16x4*>(dK + d0) = kv;
+      *reinterpret_cast<bf16x4*>(dV + d0) = vv;
+    }
+}
+
 // ------------------------------------------------------------------ dQ
 template <bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads, 2) attn_long_dq_kernel(AttnArgs a) {
@@ -724,11 +883,25 @@ void run_fwd(const AttnArgs& a, hipStream_t s) {
   }
 }
 
+// dK/dV with 8 waves of 32 keys (1, default: GPT-2-XL's backward 535 -> 441 us, profiles/attn_long_dkdv8_r6.txt)
+// or 4 waves of 64 (0); MIPIPE_ATTN_DKDV8 for A/B runs.
+const int g_dkdv8 = [] {
+  const char* e = getenv("MIPIPE_ATTN_DKDV8");
+  return e == nullptr ? 1 : atoi(e);
+}();
+
 template <bool CAUSAL>
 void run_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.S * a.H;
   hipLaunchKernelGGL(attn_long_delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, a);
   const dim3 grid(a.B * a.H, (a.S + kBlockRows - 1) / kBlockRows);
+  if (g_dkdv8) {
+    if (a.p > 0.f) hipLaunchKernelGGL((attn_long_dkdv8_kernel<CAUSAL, true>), grid, dim3(kThreads8), 0, s, a);
+    else hipLaunchKernelGGL((attn_long_dkdv8_kernel<CAUSAL, false>), grid, dim3(kThreads8), 0, s, a);
+    if (a.p > 0.f) hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL, false>), grid, dim3(kThreads), 0, s, a);
+    return;
+  }
   if (a.p > 0.f) {
     hipLaunchKernelGGL((attn_long_dkdv_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
     hipLaunchKernelGGL((attn_long_dq_kernel<CAUSAL, true>), grid, dim3(kThreads), 0, s, a);
