@@ -159,3 +159,22 @@ def test_refinement_moves_units_off_the_slowest_measured_rank():
     assert max(walls[-1]) < max(walls[0]) or len(walls) == 1
     # each round re-emulated only the two ranks whose stages changed
     assert res[0][3] == 1 + len(h0) and res[1][3] == 1 + len(h0)
+
+
+def test_move_candidates_looping_plan():
+    """Moves for a v=2 plan: only the slowest rank's virtual stages give units, each to an adjacent virtual stage of
+    ANOTHER rank, never emptying a stage, and only moves priced to lower the larger of the two walls."""
+    from mipipe.parallel.calibrate import _move_candidates
+
+    cfg = _cfg()
+    costs = engine_unit_costs(cfg, _unit_ms(cfg), False)
+    plan = plan_stages(cfg, 2, 2, 8, False, costs=costs)
+    rank_cost = [plan.rank_cost(r) * 8 for r in range(2)]
+    walls = [rank_cost[0], rank_cost[1] * 1.5]  # rank 1 measured far slower than its units price
+    slow, moves = _move_candidates(plan, walls)
+    assert slow == 1 and moves
+    for s, nb in moves:
+        assert s % 2 == 1 and nb % 2 == 0 and abs(s - nb) == 1 and plan.balance[s] > 1
+    # balanced walls: nothing is predicted to help
+    _, none = _move_candidates(plan, [100.0, 100.0])
+    assert none == []
