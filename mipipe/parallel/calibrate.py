@@ -513,6 +513,7 @@ def select_plan_by_emulation(cfg: LMConfig, candidates, prank: int, chunks: int,
             best = (t, i)
     report["chosen"] = best[1]
     plan = candidates[best[1]]
+    report["chosen_balance"] = list(plan.balance)
     if refine_rounds > 0:
         # every candidate, best simulated first, within a shared budget of emulation rounds: a plan the cost
         # model got wrong can beat the pick once its slowest rank is unloaded (PP=8: +2.5 %,
