@@ -2,7 +2,7 @@
 each rank emulated on ONE MI355X.
 
 For a BASELINE config (#3: enc12_d4096, chunks 32, micro-batch 64 -- the
-bench's default -- 'except_last'; #4: GPT-2-XL, chunks 8, micro-batch 18,
+bench's default until round 6, 128 since -- 'except_last'; #4: GPT-2-XL, chunks 8, micro-batch 18,
 'always'),
 the plans are: unit costs {analytic FLOPs, measured engine-context costs} x
 objective {makespan, balance} x chunks per rank v (the decoder split chosen per
@@ -47,7 +47,7 @@ CONFIG = {"enc12_d4096": (32, 64, "except_last"), "gpt2_xl": (8, 18, "always")}
 def bench_defaults(name: str, pp: int):
     if name == "gpt2_xl":
         return (8 if pp == 8 else 4 * pp), 18, "always"
-    return 4 * pp, (64 if pp == 8 else 128), ("except_last" if pp == 8 else "never")
+    return 4 * pp, 128, ("except_last" if pp == 8 else "never")  # micro-batch 128 at every N since round 6
 HOP_MS = 0.15
 XGMI_BYTES_PER_S = 100e9
 
