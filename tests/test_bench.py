@@ -187,10 +187,15 @@ def test_bench_emulated_plan_pick_cpu(tmp_path):
         assert sel["method"].startswith("emulated"), sel["method"]
         chosen = sel["candidates"][sel["chosen"]]
         assert all(len(c["rank_walls_ms"]) == 2 and min(c["rank_walls_ms"]) > 0 for c in sel["candidates"])
-        assert chosen["step_ms"] == min(c["step_ms"] for c in sel["candidates"])
+        # the pick: the fastest candidate, or the fastest after moving units off slow ranks (refine_plan_by_walls)
+        refined = {r["candidate"]: r["step_ms"] for r in sel.get("refinement", []) if "candidate" in r}
+        best = min([c["step_ms"] for c in sel["candidates"]] + list(refined.values()))
+        assert refined.get(sel["chosen"], chosen["step_ms"]) == best
+        assert cfg["balance"] == sel["chosen_balance"]
     else:
         chosen = sel["candidates"][0]
-    assert chosen["v"] == cfg["virtual_chunks_per_rank"] and chosen["balance"] == cfg["balance"]
+        assert chosen["balance"] == cfg["balance"]
+    assert chosen["v"] == cfg["virtual_chunks_per_rank"]
     # measured costs: the like-for-like PP = 1 rate is priced from them, and the start-up is broken down
     assert rec["like_for_like"]["pp1_tokens_per_s"] > 0
     assert {"calibration", "plan_emulation", "transport", "warmup_steps"} <= set(rec["startup_s"])
